@@ -1,0 +1,271 @@
+/*
+ * otsdb_agg.h — C-ABI of the MI355X-native OpenTSDB query-time aggregation
+ * engine (libotsdb_agg.so).
+ *
+ * This is the drop-in boundary for ONE path of OpenTSDB: the query-time
+ * aggregation that today runs as a chain of Java iterators
+ *
+ *   Span/RowSeq points -> Downsampler | FillingDownsampler -> RateSpan
+ *                      -> AggregationIterator (cross-series group-by)
+ *
+ * created by SpanGroup.iterator() (src/core/SpanGroup.java:525-530) for every
+ * group that TsdbQuery.GroupByAndAggregateCB.call builds
+ * (src/core/TsdbQuery.java:992-1113).  A JNI shim replaces
+ * the per-group lazy iterators with ONE batched call per query: every group of
+ * the query is evaluated on the GPU and handed back as arrays, which a Java
+ * array-backed SeekableView/DataPoints then serves to the unchanged callers
+ * (HttpJsonSerializer.java:821-869, CliQuery.java:126).
+ *
+ * Conventions: plain C types only, no torch/HIP types in the signatures.
+ * Every entry point returns an otsdb_status; on failure the thread-local
+ * message is available from otsdb_last_error().  Status codes map 1:1 onto the
+ * Java exceptions the reference path throws (see otsdb_status).
+ */
+#ifndef OTSDB_AGG_H
+#define OTSDB_AGG_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OTSDB_ABI_VERSION 1
+
+/* ------------------------------------------------------------------------ */
+/* Status codes — 1:1 with the exceptions of the reference path.             */
+/* ------------------------------------------------------------------------ */
+typedef enum {
+  OTSDB_OK = 0,
+  /* IllegalDataException: corrupted cell (Internal.java:307-321), `none`
+   * aggregator fed more than one value (Aggregators.java:446-460).          */
+  OTSDB_E_ILLEGAL_DATA = 1,
+  /* IllegalStateException: "Got Infinity" (AggregationIterator.java:640-643),
+   * non-increasing timestamps in a rate (RateSpan.java:129-134), empty long
+   * median (Aggregators.java:408-410).                                      */
+  OTSDB_E_ILLEGAL_STATE = 2,
+  /* IllegalArgumentException: bad spec (DownsamplingSpecification.java:116+,
+   * Downsampler "cannot use the NONE aggregator for downsampling").        */
+  OTSDB_E_ILLEGAL_ARGUMENT = 3,
+  /* NoSuchElementException: unknown aggregator (Aggregators.java:222-228). */
+  OTSDB_E_NO_SUCH_ELEMENT = 4,
+  /* Valid in the reference but not implemented by this engine (calendar
+   * downsampling, rollups, histograms, scalar fill): the Java side keeps its
+   * own iterators for such queries.                                         */
+  OTSDB_E_UNSUPPORTED = 5,
+  /* HIP runtime failure / out of device memory.                            */
+  OTSDB_E_DEVICE = 6,
+  /* Caller-provided output capacity too small (otsdb_result.capacity).      */
+  OTSDB_E_CAPACITY = 7
+} otsdb_status;
+
+/* ------------------------------------------------------------------------ */
+/* Aggregators registry (Aggregators.java:175-203).  Ids are stable.         */
+/* ------------------------------------------------------------------------ */
+typedef enum {
+  OTSDB_AGG_SUM = 0,        /* "sum"       Sum(LERP)                 */
+  OTSDB_AGG_PFSUM = 1,      /* "pfsum"     Sum(PREV)                 */
+  OTSDB_AGG_MIN = 2,        /* "min"       Min(LERP)                 */
+  OTSDB_AGG_MAX = 3,        /* "max"       Max(LERP)                 */
+  OTSDB_AGG_AVG = 4,        /* "avg"       Avg(LERP)                 */
+  OTSDB_AGG_MEDIAN = 5,     /* "median"    Median(LERP)              */
+  OTSDB_AGG_NONE = 6,       /* "none"      None(ZIM), toString "raw" */
+  OTSDB_AGG_MULT = 7,       /* "mult"      Multiply(LERP)            */
+  OTSDB_AGG_DEV = 8,        /* "dev"       StdDev(LERP)              */
+  OTSDB_AGG_DIFF = 9,       /* "diff"      Diff(LERP)                */
+  OTSDB_AGG_ZIMSUM = 10,    /* "zimsum"    Sum(ZIM)                  */
+  OTSDB_AGG_MIMMIN = 11,    /* "mimmin"    Min(MAX)                  */
+  OTSDB_AGG_MIMMAX = 12,    /* "mimmax"    Max(MIN)                  */
+  OTSDB_AGG_SQUARESUM = 13, /* "squareSum" SquareSum(ZIM)            */
+  OTSDB_AGG_COUNT = 14,     /* "count"     Count(ZIM)                */
+  OTSDB_AGG_FIRST = 15,     /* "first"     First(ZIM)                */
+  OTSDB_AGG_LAST = 16,      /* "last"      Last(ZIM)                 */
+  /* PercentileAgg(LERP), commons-math3 3.4.1 Percentile
+   * (Aggregators.java:125-173, :657-708).  LEGACY estimation: */
+  OTSDB_AGG_P999 = 17, OTSDB_AGG_P99 = 18, OTSDB_AGG_P95 = 19,
+  OTSDB_AGG_P90 = 20, OTSDB_AGG_P75 = 21, OTSDB_AGG_P50 = 22,
+  /* R_3 estimation (honoured by runLong only, Aggregators.java:690): */
+  OTSDB_AGG_EP999R3 = 23, OTSDB_AGG_EP99R3 = 24, OTSDB_AGG_EP95R3 = 25,
+  OTSDB_AGG_EP90R3 = 26, OTSDB_AGG_EP75R3 = 27, OTSDB_AGG_EP50R3 = 28,
+  /* R_7 estimation (honoured by runLong only): */
+  OTSDB_AGG_EP999R7 = 29, OTSDB_AGG_EP99R7 = 30, OTSDB_AGG_EP95R7 = 31,
+  OTSDB_AGG_EP90R7 = 32, OTSDB_AGG_EP75R7 = 33, OTSDB_AGG_EP50R7 = 34,
+  OTSDB_AGG_COUNT_IDS = 35
+} otsdb_agg_id;
+
+/* Aggregators.Interpolation (Aggregators.java:38-44), Java ordinal order. */
+typedef enum {
+  OTSDB_INTERP_DEFAULT = -1, /* use the aggregator's own method */
+  OTSDB_INTERP_LERP = 0,
+  OTSDB_INTERP_ZIM = 1,
+  OTSDB_INTERP_MAX = 2,
+  OTSDB_INTERP_MIN = 3,
+  OTSDB_INTERP_PREV = 4
+} otsdb_interp;
+
+/* FillPolicy (FillPolicy.java:22-28), Java ordinal order. */
+typedef enum {
+  OTSDB_FILL_NONE = 0,
+  OTSDB_FILL_ZERO = 1,
+  OTSDB_FILL_NAN = 2,
+  OTSDB_FILL_NULL = 3,
+  OTSDB_FILL_SCALAR = 4 /* FillingDownsampler throws "unhandled fill policy" */
+} otsdb_fill;
+
+/* ------------------------------------------------------------------------ */
+/* Query spec: one per query (all groups share it).                          */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  /* AggregationIterator window, ms, inclusive on both ends
+   * (SpanGroup ctor normalises the scan bounds to ms, SpanGroup.java:267-270;
+   * TsdbQuery passes getScanStartTimeSeconds/getScanEndTimeSeconds,
+   * TsdbQuery.java:1092-1093).                                               */
+  int64_t start_ms;
+  int64_t end_ms;
+  /* Raw query bounds (TsdbQuery.getStartTime/getEndTime, ms): used by the
+   * "all" downsampler (Downsampler.java:354-379).                            */
+  int64_t query_start_ms;
+  int64_t query_end_ms;
+  int32_t agg_id;          /* otsdb_agg_id — cross-series aggregator       */
+  int32_t interp;          /* otsdb_interp, OTSDB_INTERP_DEFAULT normally  */
+  int64_t ds_interval_ms;  /* 0 = no downsampling (raw path)               */
+  int32_t ds_agg_id;       /* downsampling function (not NONE)             */
+  int32_t fill;            /* otsdb_fill                                   */
+  int32_t run_all;         /* "0all-<agg>" downsampling                    */
+  int32_t use_calendar;    /* "<n><u>c-" downsampling -> E_UNSUPPORTED     */
+  int32_t rate;            /* RateSpan applied after downsampling          */
+  int32_t counter;         /* RateOptions.counter                          */
+  int32_t drop_resets;     /* RateOptions.drop_resets                      */
+  int32_t _pad;
+  int64_t counter_max;     /* RateOptions.counter_max (default Long.MAX)   */
+  int64_t reset_value;     /* RateOptions.reset_value (default 0)          */
+} otsdb_query_spec;
+
+/* ------------------------------------------------------------------------ */
+/* Columnar batch.  Series are given in SpanCmp order (TsdbQuery.java:      */
+/* 1862-1892); each group lists its member series in that order.            */
+/* Within a series points must be sorted by timestamp (Span/RowSeq order).  */
+/* Pointers are HOST pointers for otsdb_agg_run and DEVICE pointers for     */
+/* otsdb_agg_run_device.                                                    */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int64_t n_series;             /* S                                       */
+  int64_t n_points;             /* N = offsets[S]                          */
+  const int64_t* offsets;       /* [S+1] CSR point offsets                 */
+  const int64_t* ts_ms;         /* [N] timestamps, ms                      */
+  const int64_t* val;           /* [N] raw value bits: int64 or IEEE f64   */
+  /* Value type.  Exactly one of the following conventions:
+   *  - is_float != NULL: per point, 1 = double, 0 = long;
+   *  - else series_float != NULL: per series, 1 = double, 0 = long;
+   *  - else all values are doubles.                                       */
+  const uint8_t* is_float;      /* [N] or NULL                             */
+  const uint8_t* series_float;  /* [S] or NULL                             */
+  int64_t n_groups;             /* G                                       */
+  const int64_t* group_offsets; /* [G+1] CSR into group_members            */
+  const int64_t* group_members; /* [M] series indices, SpanCmp order       */
+} otsdb_batch;
+
+/* ------------------------------------------------------------------------ */
+/* Result: caller-allocated (sizes from otsdb_agg_plan).  Group g's points   */
+/* are [offsets[g], offsets[g+1]).  Value bits are a long when is_int=1,     */
+/* else an IEEE double (AggregationIterator.isInteger, :612-625).            */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int64_t capacity;   /* max points the ts/val/is_int arrays can hold      */
+  int64_t* offsets;   /* [G+1]                                              */
+  int64_t* ts;        /* [capacity]                                         */
+  int64_t* val;       /* [capacity] raw bits                                */
+  uint8_t* is_int;    /* [capacity]                                         */
+} otsdb_result;
+
+typedef struct {
+  int64_t n_buckets;        /* grid buckets per series (downsampled path)  */
+  int64_t max_out_points;   /* upper bound of total output points          */
+  int64_t workspace_bytes;  /* device scratch this query needs              */
+} otsdb_sizes;
+
+typedef struct otsdb_ctx otsdb_ctx;
+
+/* ---- context ------------------------------------------------------------ */
+int otsdb_abi_version(void);
+/* Creates a context bound to HIP device `device` (one process per GPU).     */
+otsdb_status otsdb_ctx_create(int device, otsdb_ctx** out);
+void otsdb_ctx_destroy(otsdb_ctx* ctx);
+/* Thread-local message of the last failing call on this thread.            */
+const char* otsdb_last_error(void);
+
+/* ---- registry (Aggregators.get / toString / interpolationMethod) -------- */
+/* Aggregators.get(name): OTSDB_E_NO_SUCH_ELEMENT for unknown names.         */
+otsdb_status otsdb_agg_lookup(const char* name, int32_t* agg_id);
+const char* otsdb_agg_name(int32_t agg_id);         /* toString()          */
+int32_t otsdb_agg_interpolation(int32_t agg_id);    /* otsdb_interp        */
+
+/* ---- query -------------------------------------------------------------- */
+/* Validates spec+batch shape and returns output/workspace sizes.            */
+otsdb_status otsdb_agg_plan(otsdb_ctx* ctx, const otsdb_query_spec* spec,
+                            const otsdb_batch* batch, otsdb_sizes* out);
+/* Host-pointer entry (the JNI shim): copies the batch to HBM, runs, copies
+ * the result back.  Synchronous.                                            */
+otsdb_status otsdb_agg_run(otsdb_ctx* ctx, const otsdb_query_spec* spec,
+                           const otsdb_batch* batch, otsdb_result* out);
+/* Device-pointer entry: batch and result live in HBM; runs on `hip_stream`
+ * (a hipStream_t passed as void*, NULL = the context's stream).  Returns
+ * after the result is complete on the device (the status needs the device
+ * error word).                                                               */
+otsdb_status otsdb_agg_run_device(otsdb_ctx* ctx, const otsdb_query_spec* spec,
+                                  const otsdb_batch* batch, otsdb_result* out,
+                                  void* hip_stream);
+
+/* ---- multi-GPU (series-sharded) ----------------------------------------- */
+/* Partial per-(group, bucket) reduction state, the unit exchanged between
+ * ranks over RCCL.  32 bytes, see DESIGN.md §Multi-GPU.                     */
+typedef struct {
+  double x, y, z;
+  int64_t w;
+} otsdb_partial;
+
+/* Runs the local shard (downsample/rate/interpolate + chunked group reduce)
+ * and writes one partial per (group, bucket) plus the emit mask into DEVICE
+ * buffers partials[G*n_buckets], emit[G*n_buckets].  n_buckets from plan.   */
+otsdb_status otsdb_agg_partials_device(otsdb_ctx* ctx,
+                                       const otsdb_query_spec* spec,
+                                       const otsdb_batch* batch,
+                                       otsdb_partial* partials,
+                                       uint8_t* emit, void* hip_stream);
+/* Combines `n_ranks` partial sets laid out rank-major in DEVICE memory
+ * ([n_ranks][G*n_buckets], combined in rank order = series order) and
+ * writes the final result (DEVICE pointers).                                */
+otsdb_status otsdb_agg_finalize_device(otsdb_ctx* ctx,
+                                       const otsdb_query_spec* spec,
+                                       int64_t n_groups, int64_t n_buckets,
+                                       int32_t n_ranks,
+                                       const otsdb_partial* partials,
+                                       const uint8_t* emit,
+                                       otsdb_result* out, void* hip_stream);
+
+/* ---- synthetic workload generator (bench / tests) ----------- */
+/* Generates the columnar batch of `n_series` series starting at global
+ * series index `series0` directly in HBM.  Pass offsets=NULL first to get
+ * the per-series point counts (written to `counts`, DEVICE [S]).            */
+typedef struct {
+  uint64_t seed;          /* 42                                              */
+  int64_t t0_ms;          /* 1356998400000                                   */
+  int64_t duration_ms;    /* 86400000 / 604800000                            */
+  int64_t cadence_ms;     /* 10000                                           */
+  int32_t kind;           /* 0 = gauge f64, 1 = gauge int64, 2 = counter int64 */
+  int32_t _pad;
+} otsdb_gen_spec;
+
+otsdb_status otsdb_gen_counts_device(otsdb_ctx* ctx, const otsdb_gen_spec* g,
+                                     int64_t series0, int64_t n_series,
+                                     int64_t* counts, void* hip_stream);
+otsdb_status otsdb_gen_fill_device(otsdb_ctx* ctx, const otsdb_gen_spec* g,
+                                   int64_t series0, int64_t n_series,
+                                   const int64_t* offsets, int64_t* ts_ms,
+                                   int64_t* val, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OTSDB_AGG_H */

@@ -1,0 +1,164 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes front-end of the CPU restatement
+(oracle/otsdb_oracle.c).  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg import this module; the product never does.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "_build", "liboracle.so")
+
+POINT = np.dtype([("ts", np.int64), ("bits", np.int64), ("is_int", np.int32),
+                  ("_pad", np.int32)])
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        l = C.CDLL(LIB)
+        vp, i64, i32, cp = C.c_void_p, C.c_int64, C.c_int32, C.c_char_p
+        l.or_group_by.argtypes = [vp, vp, vp, i64, vp, C.POINTER(i64), cp,
+                                  C.c_int]
+        l.or_view_stream.argtypes = [vp, C.c_int, i64, i64, vp, vp, vp, vp,
+                                     i64, C.POINTER(i64), cp, C.c_int]
+        l.or_run_double.argtypes = [i32, vp, i64, C.POINTER(C.c_double), cp,
+                                    C.c_int]
+        l.or_run_long.argtypes = [i32, vp, i64, C.POINTER(i64), cp, C.c_int]
+        l.or_decode_row.argtypes = [vp, i64, vp, i64, i64, vp, i64,
+                                    C.POINTER(i64), cp, C.c_int]
+        l.or_gen_count.argtypes = [vp, i64]
+        l.or_gen_count.restype = i64
+        l.or_gen_fill.argtypes = [vp, i64, vp, vp]
+        l.or_gen_fill.restype = i64
+        _lib = l
+    return _lib
+
+
+class OracleError(Exception):
+    def __init__(self, status, msg):
+        super().__init__("status %d: %s" % (status, msg))
+        self.status = status
+        self.msg = msg
+
+
+def group_by(spec, batch):
+    """Returns (status, list of per-group structured arrays of POINT)."""
+    l = lib()
+    b = batch.as_abi()
+    G = batch.n_groups
+    offs = np.zeros(G + 1, np.int64)
+    need = C.c_int64(0)
+    err = C.create_string_buffer(256)
+    cap = max(1024, 4 * int(batch.offsets[-1]) + 16)
+    while True:
+        out = np.zeros(cap, POINT)
+        st = l.or_group_by(C.byref(spec), C.byref(b), out.ctypes.data, cap,
+                           offs.ctypes.data, C.byref(need), err, 256)
+        if st == 7 and need.value > cap:
+            cap = need.value
+            continue
+        break
+    if st != 0:
+        raise OracleError(st, err.value.decode())
+    return [out[offs[g]:offs[g + 1]].copy() for g in range(G)]
+
+
+def view_stream(spec, ts, bits, is_float, seek=None):
+    l = lib()
+    ts = np.ascontiguousarray(ts, np.int64)
+    bits = np.ascontiguousarray(bits, np.int64)
+    isf = np.ascontiguousarray(is_float, np.uint8)
+    cap = 4 * len(ts) + 1024
+    out = np.zeros(cap, POINT)
+    need = C.c_int64(0)
+    err = C.create_string_buffer(256)
+    st = l.or_view_stream(C.byref(spec), 0 if seek is None else 1,
+                          0 if seek is None else int(seek), len(ts),
+                          ts.ctypes.data, bits.ctypes.data, isf.ctypes.data,
+                          out.ctypes.data, cap, C.byref(need), err, 256)
+    if st != 0:
+        raise OracleError(st, err.value.decode())
+    return out[:need.value].copy()
+
+
+def run_double(agg_id, values):
+    v = np.ascontiguousarray(values, np.float64)
+    out = C.c_double(0)
+    err = C.create_string_buffer(256)
+    st = lib().or_run_double(agg_id, v.ctypes.data, len(v), C.byref(out),
+                             err, 256)
+    if st != 0:
+        raise OracleError(st, err.value.decode())
+    return out.value
+
+
+def run_long(agg_id, values):
+    v = np.ascontiguousarray(values, np.int64)
+    out = C.c_int64(0)
+    err = C.create_string_buffer(256)
+    st = lib().or_run_long(agg_id, v.ctypes.data, len(v), C.byref(out), err,
+                           256)
+    if st != 0:
+        raise OracleError(st, err.value.decode())
+    return out.value
+
+
+def decode_row(qual, vals, base_time_s):
+    q = np.frombuffer(bytes(qual), np.uint8)
+    v = np.frombuffer(bytes(vals), np.uint8)
+    cap = len(q) + 4
+    out = np.zeros(cap, POINT)
+    need = C.c_int64(0)
+    err = C.create_string_buffer(256)
+    st = lib().or_decode_row(q.ctypes.data, len(q), v.ctypes.data, len(v),
+                             base_time_s, out.ctypes.data, cap, C.byref(need),
+                             err, 256)
+    if st != 0:
+        raise OracleError(st, err.value.decode())
+    return out[:need.value].copy()
+
+
+def gen_series(gspec, s):
+    """(ts, val) of global series s from the C restatement of the generator."""
+    l = lib()
+    n = l.or_gen_count(C.byref(gspec), s)
+    ts = np.zeros(max(n, 1), np.int64)
+    val = np.zeros(max(n, 1), np.int64)
+    l.or_gen_fill(C.byref(gspec), s, ts.ctypes.data, val.ctypes.data)
+    return ts[:n], val[:n]
+
+
+def gen_batch(gspec, series0, n_series, group_of=None):
+    """Host batch of series [series0, series0+n) with group ids from
+    group_of(global_s) (default: one group)."""
+    from opentsdb_amd.batch import HostBatch, groups_from_ids
+    tss, vals = [], []
+    offs = [0]
+    for s in range(series0, series0 + n_series):
+        t, v = gen_series(gspec, s)
+        tss.append(t)
+        vals.append(v)
+        offs.append(offs[-1] + len(t))
+    ts = np.concatenate(tss) if tss else np.zeros(0, np.int64)
+    val = np.concatenate(vals) if vals else np.zeros(0, np.int64)
+    sf = np.full(n_series, 1 if gspec.kind == 0 else 0, np.uint8)
+    if group_of is None:
+        gid = np.zeros(n_series, np.int64)
+    else:
+        gid = np.array([group_of(s) for s in
+                        range(series0, series0 + n_series)], np.int64)
+        gid -= gid.min() if n_series else 0
+    g_off, members = groups_from_ids(gid)
+    return HostBatch(np.array(offs, np.int64), ts, val, None, sf, g_off,
+                     members)
