@@ -244,6 +244,16 @@ otsdb_status otsdb_agg_finalize_device(otsdb_ctx* ctx,
                                        const uint8_t* emit,
                                        otsdb_result* out, void* hip_stream);
 
+/* ---- stage timing (bench roofline) ------------------------------------- */
+/* When enabled, every query records HIP events around its pipeline stages
+ * on the query's stream.  otsdb_prof_read returns, per stage, the summed
+ * milliseconds and the number of launches since the last reset:
+ * [0] k_bucketize  [1] k_transform  [2] k_group+k_combine  [3] k_prep
+ * [4] k_compact+k_scan.  Synchronises the stream.                           */
+otsdb_status otsdb_prof_enable(otsdb_ctx* ctx, int enable);
+otsdb_status otsdb_prof_read(otsdb_ctx* ctx, double* ms, int64_t* launches,
+                             int n, int reset);
+
 /* ---- synthetic workload generator (bench / tests) ----------- */
 /* Generates the columnar batch of `n_series` series starting at global
  * series index `series0` directly in HBM.  Pass offsets=NULL first to get

@@ -97,7 +97,7 @@ EXPORTS = [
     "otsdb_agg_interpolation", "otsdb_agg_plan", "otsdb_agg_run",
     "otsdb_agg_run_device", "otsdb_agg_partials_device",
     "otsdb_agg_finalize_device", "otsdb_gen_counts_device",
-    "otsdb_gen_fill_device",
+    "otsdb_gen_fill_device", "otsdb_prof_enable", "otsdb_prof_read",
 ]
 
 _lib = None
@@ -145,6 +145,10 @@ def load(path=None):
     lib.otsdb_gen_counts_device.restype = C.c_int
     lib.otsdb_gen_fill_device.argtypes = [vp, PG, i64, i64, vp, vp, vp, vp]
     lib.otsdb_gen_fill_device.restype = C.c_int
+    lib.otsdb_prof_enable.argtypes = [vp, C.c_int]
+    lib.otsdb_prof_enable.restype = C.c_int
+    lib.otsdb_prof_read.argtypes = [vp, vp, vp, C.c_int, C.c_int]
+    lib.otsdb_prof_read.restype = C.c_int
     if path is None:
         _lib = lib
     return lib

@@ -1,0 +1,938 @@
+// engine.hip — host side of libotsdb_agg.so: the C-ABI of include/otsdb_agg.h.
+//
+// Plans one query (bucket grid, series chunks), carves a reusable HBM
+// workspace, launches the kernel pipeline of kernels.hip on the context's
+// stream and maps the device error word back onto the reference's
+// exceptions.  No CPU fallback exists: every data point is produced on the
+// GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/otsdb_agg.h"
+#include "kernels.hip"
+
+using namespace otsdb;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+otsdb_status fail(otsdb_status st, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return st;
+}
+
+#define HIP_TRY(x)                                                        \
+  do {                                                                    \
+    hipError_t e_ = (x);                                                  \
+    if (e_ != hipSuccess)                                                 \
+      return fail(OTSDB_E_DEVICE, "%s: %s", #x, hipGetErrorString(e_));   \
+  } while (0)
+
+struct AggInfo {
+  const char* key;   // Aggregators.get() name
+  const char* name;  // toString()
+  int interp;
+};
+
+const AggInfo kAggs[OTSDB_AGG_COUNT_IDS] = {
+    {"sum", "sum", 0},          {"pfsum", "pfsum", 4},
+    {"min", "min", 0},          {"max", "max", 0},
+    {"avg", "avg", 0},          {"median", "median", 0},
+    {"none", "raw", 1},         {"mult", "multiply", 0},
+    {"dev", "dev", 0},          {"diff", "diff", 0},
+    {"zimsum", "zimsum", 1},    {"mimmin", "mimmin", 2},
+    {"mimmax", "mimmax", 3},    {"squareSum", "squareSum", 1},
+    {"count", "count", 1},      {"first", "first", 1},
+    {"last", "last", 1},        {"p999", "p999", 0},
+    {"p99", "p99", 0},          {"p95", "p95", 0},
+    {"p90", "p90", 0},          {"p75", "p75", 0},
+    {"p50", "p50", 0},          {"ep999r3", "ep999r3", 0},
+    {"ep99r3", "ep99r3", 0},    {"ep95r3", "ep95r3", 0},
+    {"ep90r3", "ep90r3", 0},    {"ep75r3", "ep75r3", 0},
+    {"ep50r3", "ep50r3", 0},    {"ep999r7", "ep999r7", 0},
+    {"ep99r7", "ep99r7", 0},    {"ep95r7", "ep95r7", 0},
+    {"ep90r7", "ep90r7", 0},    {"ep75r7", "ep75r7", 0},
+    {"ep50r7", "ep50r7", 0},
+};
+
+bool is_selection(int agg) {
+  return agg == OTSDB_AGG_MEDIAN || agg >= OTSDB_AGG_P999;
+}
+
+double pct_of(int agg) {  // PercentileAgg(percentile).evaluate(): p / 100d
+  static const double P[6] = {99.9, 99.0, 95.0, 90.0, 75.0, 50.0};
+  return P[(agg - OTSDB_AGG_P999) % 6] / 100.0;
+}
+
+// Calls f(M{}) with the reduction state type of aggregator `agg`.
+template <class F>
+bool with_monoid(int agg, F&& f) {
+  switch (agg) {
+    case OTSDB_AGG_SUM:
+    case OTSDB_AGG_PFSUM:
+    case OTSDB_AGG_ZIMSUM: f(MSum<0>{}); return true;
+    case OTSDB_AGG_AVG: f(MSum<1>{}); return true;
+    case OTSDB_AGG_SQUARESUM: f(MSum<2>{}); return true;
+    case OTSDB_AGG_COUNT: f(MSum<3>{}); return true;
+    case OTSDB_AGG_MIN:
+    case OTSDB_AGG_MIMMIN: f(MMinMax<false>{}); return true;
+    case OTSDB_AGG_MAX:
+    case OTSDB_AGG_MIMMAX: f(MMinMax<true>{}); return true;
+    case OTSDB_AGG_DEV: f(MDev{}); return true;
+    case OTSDB_AGG_FIRST: f(MFirstLast<false>{}); return true;
+    case OTSDB_AGG_LAST: f(MFirstLast<true>{}); return true;
+    case OTSDB_AGG_MULT: f(MMult{}); return true;
+    case OTSDB_AGG_DIFF: f(MDiff{}); return true;
+    case OTSDB_AGG_NONE: f(MNone{}); return true;
+    default: return false;
+  }
+}
+
+inline int64_t jmod(int64_t a, int64_t b) { return a % b; }
+inline int64_t align_down(int64_t t, int64_t iv) { return t - jmod(t, iv); }
+
+constexpr int64_t kChunk = 256;  // series per cross-series chunk
+
+struct Carve {
+  char* base;
+  size_t off = 0;
+  template <class T>
+  T* take(size_t n) {
+    off = (off + 255) & ~(size_t)255;
+    T* p = reinterpret_cast<T*>(base + off);
+    off += n * sizeof(T);
+    return p;
+  }
+};
+
+}  // namespace
+
+struct otsdb_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  void* ws = nullptr;
+  size_t ws_cap = 0;
+  void* stage = nullptr;
+  size_t stage_cap = 0;
+  int* d_err = nullptr;                 // device error word
+  unsigned long long* d_mm = nullptr;   // k_bounds min/max
+  int64_t* h_small = nullptr;           // pinned readback
+  // tile plan cache (keyed by the group offsets)
+  std::vector<int64_t> goff_cache;
+  int64_t* d_tiles = nullptr;
+  size_t d_tiles_cap = 0;
+  int64_t n_tiles = 0, n_multi = 0;
+  std::mutex mu;  // one query at a time per context
+  // stage timing (otsdb_prof_*)
+  bool prof = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_pending;
+  size_t ev_used = 0;
+  double prof_ms[8] = {0};
+  int64_t prof_n[8] = {0};
+};
+
+namespace {
+
+otsdb_status ensure(void** p, size_t* cap, size_t need) {
+  if (need <= *cap) return OTSDB_OK;
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  size_t n = std::max(need, (size_t)1 << 20);
+  hipError_t e = hipMalloc(p, n);
+  if (e != hipSuccess)
+    return fail(OTSDB_E_DEVICE, "hipMalloc(%zu): %s", n, hipGetErrorString(e));
+  *cap = n;
+  return OTSDB_OK;
+}
+
+// --------------------------------------------------------------- planning
+struct Plan {
+  Params P;
+  int64_t S, G, M, N;
+  bool sel;  // percentile/median across series
+};
+
+otsdb_status check_spec(const otsdb_query_spec* s) {
+  if (s->agg_id < 0 || s->agg_id >= OTSDB_AGG_COUNT_IDS)
+    return fail(OTSDB_E_NO_SUCH_ELEMENT, "No such aggregator: %d", s->agg_id);
+  const bool ds = s->ds_interval_ms > 0 || s->run_all;
+  if (!ds)
+    return fail(OTSDB_E_UNSUPPORTED,
+                "raw (non-downsampled) group-by is not offloaded yet");
+  if (s->ds_agg_id < 0 || s->ds_agg_id >= OTSDB_AGG_COUNT_IDS)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "No such downsampling function");
+  if (s->ds_agg_id == OTSDB_AGG_NONE)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT,
+                "cannot use the NONE aggregator for downsampling");
+  if (is_selection(s->ds_agg_id))
+    return fail(OTSDB_E_UNSUPPORTED,
+                "percentile/median downsampling is not offloaded yet");
+  if (s->use_calendar)
+    return fail(OTSDB_E_UNSUPPORTED, "calendar downsampling");
+  if (s->fill == OTSDB_FILL_SCALAR)
+    return fail(OTSDB_E_UNSUPPORTED, "unhandled fill policy");
+  if (s->fill < 0 || s->fill > OTSDB_FILL_SCALAR)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "bad fill policy %d", s->fill);
+  if (s->interp < -1 || s->interp > OTSDB_INTERP_PREV)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "bad interpolation %d", s->interp);
+  if (!s->run_all && s->start_ms < 0)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "negative start");
+  return OTSDB_OK;
+}
+
+// Grid of buckets every series row is laid out on.
+otsdb_status make_params(const otsdb_query_spec* s, Params* P) {
+  memset(P, 0, sizeof(*P));
+  P->start_ms = s->start_ms;
+  P->end_ms = s->end_ms;
+  P->run_all = s->run_all;
+  P->fill = s->run_all ? 0 : s->fill;
+  P->rate = s->rate;
+  P->counter = s->counter;
+  P->drop_resets = s->drop_resets;
+  P->counter_max = s->counter_max;
+  P->reset_value = s->reset_value;
+  P->interp = s->interp >= 0 ? s->interp : kAggs[s->agg_id].interp;
+  P->fill_value = (P->fill == OTSDB_FILL_ZERO) ? 0.0 : NAN;
+  P->pct = s->agg_id >= OTSDB_AGG_P999 ? pct_of(s->agg_id) : 0.0;
+  P->rate_origin_ts = 0;
+  P->rate_origin_val = 0.0;
+  if (s->run_all) {
+    // Downsampler "all": one point at query_start holding the points of
+    // [query_start, query_end) after seek(start) (Downsampler.java:354-379)
+    P->interval = 1;
+    P->inv_interval = 1.0;
+    P->gbase = s->query_start_ms;
+    P->out_ts0 = s->query_start_ms;
+    P->seek_ts = std::max(s->start_ms, s->query_start_ms);
+    P->stop_ts = s->query_end_ms;
+    P->nb = (s->query_start_ms >= s->start_ms &&
+             s->query_start_ms <= s->end_ms) ? 1 : 0;
+    return OTSDB_OK;
+  }
+  const int64_t iv = s->ds_interval_ms;
+  P->interval = iv;
+  P->inv_interval = 1.0 / (double)iv;
+  const int64_t grid0 = align_down(s->start_ms + iv - 1, iv);
+  P->gbase = grid0;
+  P->seek_ts = grid0;
+  if (P->fill) {
+    // FillingDownsampler: every bucket of [align(start), align(end)); the
+    // aggregation iterator skips those before start (FillingDownsampler.java
+    // :136-142, AggregationIterator.java:425-447)
+    const int64_t aend = align_down(s->end_ms, iv);
+    P->nb = aend > grid0 ? (aend - grid0) / iv : 0;
+    P->stop_ts = grid0 + P->nb * iv;
+    const int64_t astart = align_down(s->start_ms, iv);
+    if (astart < grid0) {
+      P->rate_origin_ts = astart;
+      P->rate_origin_val = P->fill_value;
+    }
+  } else {
+    P->nb = s->end_ms >= grid0 ? (s->end_ms - grid0) / iv + 1 : 0;
+    P->stop_ts = grid0 + P->nb * iv;
+  }
+  return OTSDB_OK;
+}
+
+otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff) {
+  if (c->d_tiles && goff == c->goff_cache) return OTSDB_OK;
+  const int64_t G = (int64_t)goff.size() - 1;
+  std::vector<int64_t> tg, tm0, tm1, mg, mt0, mt1, ag, at0, at1;
+  std::vector<uint8_t> single;
+  for (int64_t g = 0; g < G; ++g) {
+    const int64_t a = goff[g], b = goff[g + 1];
+    const int64_t t0 = (int64_t)tg.size();
+    for (int64_t m = a; m < b; m += kChunk) {
+      tg.push_back(g);
+      tm0.push_back(m);
+      tm1.push_back(std::min(b, m + kChunk));
+    }
+    const int64_t t1 = (int64_t)tg.size();
+    for (int64_t t = t0; t < t1; ++t) single.push_back(t1 - t0 == 1);
+    if (t1 - t0 > 1) {
+      mg.push_back(g);
+      mt0.push_back(t0);
+      mt1.push_back(t1);
+    }
+    ag.push_back(g);
+    at0.push_back(t0);
+    at1.push_back(t1);
+  }
+  const int64_t T = (int64_t)tg.size(), MG = (int64_t)mg.size();
+  // layout: tg tm0 tm1 [T] | mg mt0 mt1 [MG] | ag at0 at1 [G] | single [T]
+  const size_t n64 = 3 * T + 3 * MG + 3 * G;
+  const size_t bytes = n64 * 8 + T + 64;
+  void* p = c->d_tiles;
+  size_t cap = c->d_tiles_cap;
+  otsdb_status st = ensure(&p, &cap, bytes);
+  c->d_tiles = (int64_t*)p;
+  c->d_tiles_cap = cap;
+  if (st) return st;
+  std::vector<int64_t> h;
+  h.reserve(n64);
+  h.insert(h.end(), tg.begin(), tg.end());
+  h.insert(h.end(), tm0.begin(), tm0.end());
+  h.insert(h.end(), tm1.begin(), tm1.end());
+  h.insert(h.end(), mg.begin(), mg.end());
+  h.insert(h.end(), mt0.begin(), mt0.end());
+  h.insert(h.end(), mt1.begin(), mt1.end());
+  h.insert(h.end(), ag.begin(), ag.end());
+  h.insert(h.end(), at0.begin(), at0.end());
+  h.insert(h.end(), at1.begin(), at1.end());
+  if (!h.empty())
+    HIP_TRY(hipMemcpyAsync(c->d_tiles, h.data(), n64 * 8,
+                           hipMemcpyHostToDevice, c->stream));
+  if (T)
+    HIP_TRY(hipMemcpyAsync((char*)c->d_tiles + n64 * 8, single.data(), T,
+                           hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->goff_cache = goff;
+  c->n_tiles = T;
+  c->n_multi = MG;
+  return OTSDB_OK;
+}
+
+struct Tiles {
+  const int64_t *tg, *tm0, *tm1, *mg, *mt0, *mt1, *ag, *at0, *at1;
+  const uint8_t* single;
+  int64_t T, MG, G;
+};
+
+Tiles tiles_of(otsdb_ctx* c, int64_t G) {
+  Tiles t;
+  const int64_t T = c->n_tiles, MG = c->n_multi;
+  const int64_t* b = c->d_tiles;
+  t.tg = b;
+  t.tm0 = b + T;
+  t.tm1 = b + 2 * T;
+  t.mg = b + 3 * T;
+  t.mt0 = t.mg + MG;
+  t.mt1 = t.mg + 2 * MG;
+  t.ag = b + 3 * T + 3 * MG;
+  t.at0 = t.ag + G;
+  t.at1 = t.ag + 2 * G;
+  t.single = (const uint8_t*)(b + 3 * T + 3 * MG + 3 * G);
+  t.T = T;
+  t.MG = MG;
+  t.G = G;
+  return t;
+}
+
+// Brackets a pipeline stage with HIP events when profiling is enabled.
+struct StageTimer {
+  otsdb_ctx* c;
+  int stage;
+  hipEvent_t a = nullptr, b = nullptr;
+  hipEvent_t get() {
+    if (c->ev_used == c->ev_pool.size()) {
+      hipEvent_t e;
+      hipEventCreate(&e);
+      c->ev_pool.push_back(e);
+    }
+    return c->ev_pool[c->ev_used++];
+  }
+  StageTimer(otsdb_ctx* c_, int s_) : c(c_), stage(s_) {
+    if (c->prof) {
+      a = get();
+      hipEventRecord(a, c->stream);
+    }
+  }
+  ~StageTimer() {
+    if (c->prof) {
+      b = get();
+      hipEventRecord(b, c->stream);
+      c->ev_pending.push_back({stage, {a, b}});
+    }
+  }
+};
+
+inline unsigned blocks_for(int64_t n, int per) {
+  return (unsigned)((n + per - 1) / per);
+}
+
+struct Work {
+  SeriesMeta SM;
+  Rows R;
+  Packed* partial;
+  uint8_t* tile_emit;
+  double* out_val;
+  uint8_t* out_emit;
+  int64_t* counts;
+};
+
+// Everything up to dense (group, bucket) results / partials.
+// mode 0: final dense results; mode 1: per-group partials into `gpart/gemit`
+otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
+                          const BatchDev& B, const int64_t* d_members,
+                          std::vector<int64_t>& goff, Params& P, Work& W,
+                          int mode, Packed* gpart, uint8_t* gemit) {
+  hipStream_t st = c->stream;
+  const int64_t S = B.S;
+  const int64_t G = (int64_t)goff.size() - 1;
+  otsdb_status rc = build_tiles(c, goff);
+  if (rc) return rc;
+  const Tiles T = tiles_of(c, G);
+  const int64_t nb = P.nb;
+
+  // grid trimming for very wide windows (NONE fill only): the rows span only
+  // the buckets that hold data
+  if (!P.run_all && !P.fill && (double)S * (double)nb > 4.0e9) {
+    unsigned long long init[2] = {~0ULL, 0ULL};
+    HIP_TRY(hipMemcpyAsync(c->d_mm, init, 16, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_bounds, dim3(blocks_for(S, 256)), dim3(256), 0, st, P,
+                       B, c->d_mm);
+    unsigned long long mm[2];
+    HIP_TRY(hipMemcpyAsync(mm, c->d_mm, 16, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (mm[0] > mm[1]) {
+      P.nb = 0;
+    } else {
+      const int64_t b_lo = ((int64_t)mm[0] - P.gbase) / P.interval;
+      const int64_t b_hi = ((int64_t)mm[1] - P.gbase) / P.interval;
+      P.gbase += b_lo * P.interval;
+      P.nb = b_hi - b_lo + 1;
+    }
+    if ((double)S * (double)P.nb > 2.0e10)
+      return fail(OTSDB_E_UNSUPPORTED, "bucket grid too large (%lld x %lld)",
+                  (long long)S, (long long)P.nb);
+  } else if ((double)S * (double)nb > 2.0e10) {
+    return fail(OTSDB_E_UNSUPPORTED, "bucket grid too large (%lld x %lld)",
+                (long long)S, (long long)nb);
+  }
+  const int64_t NB = P.nb;
+
+  // workspace
+  auto carve = [&](char* base) {
+    Carve cv{base};
+    W.SM.lo = cv.take<int64_t>(S);
+    W.SM.hi = cv.take<int64_t>(S);
+    W.SM.of_ts = cv.take<int64_t>(S);
+    W.SM.of_val = cv.take<double>(S);
+    W.SM.keep = cv.take<uint8_t>(S);
+    W.SM.of_has = cv.take<uint8_t>(S);
+    W.R.val = cv.take<double>((size_t)S * NB);
+    W.R.state = cv.take<uint8_t>((size_t)S * NB);
+    W.partial = cv.take<Packed>((size_t)T.T * NB);
+    W.tile_emit = cv.take<uint8_t>((size_t)T.T * NB);
+    W.out_val = cv.take<double>((size_t)G * NB);
+    W.out_emit = cv.take<uint8_t>((size_t)G * NB);
+    W.counts = cv.take<int64_t>(G + 1);
+    return cv.off + 256;
+  };
+  const size_t need = carve(nullptr);
+  rc = ensure(&c->ws, &c->ws_cap, need);
+  if (rc) return rc;
+  carve((char*)c->ws);
+
+  HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), st));
+  if (G * NB > 0 && mode == 0)
+    HIP_TRY(hipMemsetAsync(W.out_emit, 0, (size_t)G * NB, st));
+  if (S > 0 && NB > 0)
+    HIP_TRY(hipMemsetAsync(W.R.state, 0, (size_t)S * NB, st));
+
+  bool ok = true;
+  if (S > 0 && NB > 0) {
+    ok = with_monoid(spec->ds_agg_id, [&](auto tag) {
+      using M = decltype(tag);
+      {
+        StageTimer tm(c, 3);
+        hipLaunchKernelGGL(k_prep<M>, dim3(blocks_for(S, 256)), dim3(256), 0,
+                           st, P, B, W.SM);
+      }
+      StageTimer tm(c, 0);
+      hipLaunchKernelGGL(k_bucketize<M>, dim3(blocks_for(S, 4)), dim3(256), 0,
+                         st, P, B, W.SM, W.R);
+    });
+    if (!ok) return fail(OTSDB_E_UNSUPPORTED, "downsampler %d", spec->ds_agg_id);
+    StageTimer tm(c, 1);
+    hipLaunchKernelGGL(k_transform, dim3(blocks_for(S, 4)), dim3(256), 0, st,
+                       P, S, W.SM, W.R, c->d_err);
+  } else if (S > 0) {
+    // still need the span filter for nothing: no buckets -> no output
+  }
+  if (G > 0 && NB > 0) {
+    StageTimer tm(c, 2);
+    if (is_selection(spec->agg_id)) {
+      if (mode != 0)
+        return fail(OTSDB_E_UNSUPPORTED,
+                    "percentiles across ranks are not offloaded yet");
+      hipLaunchKernelGGL(k_group_select,
+                         dim3(blocks_for(T.T * NB, SEL_THREADS)),
+                         dim3(SEL_THREADS), 0, st, NB, T.T, T.tg, T.tm0, T.tm1,
+                         T.single, d_members, W.R, W.out_val, W.out_emit,
+                         c->d_err, spec->agg_id == OTSDB_AGG_MEDIAN ? 1 : 0,
+                         P.pct);
+    } else {
+      ok = with_monoid(spec->agg_id, [&](auto tag) {
+        using M = decltype(tag);
+        if (T.T > 0)
+          hipLaunchKernelGGL(k_group<M>, dim3(blocks_for(T.T * NB, 256)),
+                             dim3(256), 0, st, NB, T.T, T.tg, T.tm0, T.tm1,
+                             T.single, d_members, W.R, W.partial, W.tile_emit,
+                             W.out_val, W.out_emit, c->d_err, mode);
+        if (mode == 0) {
+          if (T.MG > 0)
+            hipLaunchKernelGGL(k_combine<M>, dim3(blocks_for(T.MG * NB, 256)),
+                               dim3(256), 0, st, NB, T.MG, T.mg, T.mt0, T.mt1,
+                               W.partial, W.tile_emit, W.out_val, W.out_emit,
+                               (Packed*)nullptr, c->d_err);
+        } else {
+          hipLaunchKernelGGL(k_combine<M>, dim3(blocks_for(G * NB, 256)),
+                             dim3(256), 0, st, NB, G, T.ag, T.at0, T.at1,
+                             W.partial, W.tile_emit, W.out_val, gemit, gpart,
+                             c->d_err);
+        }
+      });
+      if (!ok) return fail(OTSDB_E_NO_SUCH_ELEMENT, "aggregator %d", spec->agg_id);
+    }
+  }
+  HIP_TRY(hipGetLastError());
+  return OTSDB_OK;
+}
+
+otsdb_status compact(otsdb_ctx* c, const Params& P, int64_t G,
+                     const double* out_val, const uint8_t* out_emit,
+                     int64_t* counts, otsdb_result* out) {
+  hipStream_t st = c->stream;
+  if (G == 0) {
+    HIP_TRY(hipMemsetAsync(out->offsets, 0, sizeof(int64_t), st));
+    return OTSDB_OK;
+  }
+  if (P.nb == 0) {
+    HIP_TRY(hipMemsetAsync(out->offsets, 0, sizeof(int64_t) * (G + 1), st));
+    return OTSDB_OK;
+  }
+  StageTimer tm(c, 4);
+  hipLaunchKernelGGL(k_compact, dim3(blocks_for(G, 4)), dim3(256), 0, st, P,
+                     G, out_val, out_emit, counts, (const int64_t*)nullptr,
+                     (int64_t)0, (int64_t*)nullptr, (int64_t*)nullptr,
+                     (uint8_t*)nullptr, 0);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, G,
+                     (const int64_t*)counts, out->offsets);
+  hipLaunchKernelGGL(k_compact, dim3(blocks_for(G, 4)), dim3(256), 0, st, P,
+                     G, out_val, out_emit, counts,
+                     (const int64_t*)out->offsets, out->capacity, out->ts,
+                     out->val, out->is_int, 1);
+  HIP_TRY(hipGetLastError());
+  return OTSDB_OK;
+}
+
+// reads the error word and the total point count; maps to a status
+otsdb_status finish(otsdb_ctx* c, int64_t G, otsdb_result* out) {
+  hipStream_t st = c->stream;
+  HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
+                         hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_small[1], out->offsets + G, sizeof(int64_t),
+                         hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const int err = (int)(c->h_small[0] & 0xFFFFFFFF);
+  const int64_t total = c->h_small[1];
+  if (err & ERR_NONE_MULTI)
+    return fail(OTSDB_E_ILLEGAL_DATA, "More than one value in aggregator raw");
+  if (err & ERR_RATE_TS)
+    return fail(OTSDB_E_ILLEGAL_STATE,
+                "Next timestamp is supposed to be strictly greater than the "
+                "previous one");
+  if (err & ERR_INFINITY)
+    return fail(OTSDB_E_ILLEGAL_STATE, "Got Infinity");
+  if (err & ERR_SEL_TOO_BIG)
+    return fail(OTSDB_E_UNSUPPORTED,
+                "percentile/median over groups of more than %d series is not "
+                "offloaded yet", SEL_K);
+  if (total > out->capacity)
+    return fail(OTSDB_E_CAPACITY, "result capacity %lld < %lld points",
+                (long long)out->capacity, (long long)total);
+  return OTSDB_OK;
+}
+
+otsdb_status read_goff(otsdb_ctx* c, const otsdb_batch* b, bool device,
+                       std::vector<int64_t>& goff) {
+  goff.resize(b->n_groups + 1);
+  if (b->n_groups < 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "n_groups < 0");
+  if (!b->group_offsets) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "no groups");
+  if (device) {
+    HIP_TRY(hipMemcpyAsync(goff.data(), b->group_offsets,
+                           sizeof(int64_t) * goff.size(),
+                           hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  } else {
+    memcpy(goff.data(), b->group_offsets, sizeof(int64_t) * goff.size());
+  }
+  for (size_t i = 1; i < goff.size(); ++i)
+    if (goff[i] < goff[i - 1])
+      return fail(OTSDB_E_ILLEGAL_ARGUMENT, "group_offsets not monotonic");
+  return OTSDB_OK;
+}
+
+otsdb_status run_device_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
+                             const otsdb_batch* b, otsdb_result* out,
+                             std::vector<int64_t>& goff) {
+  otsdb_status rc = check_spec(spec);
+  if (rc) return rc;
+  Params P;
+  rc = make_params(spec, &P);
+  if (rc) return rc;
+  BatchDev B{b->n_series, b->offsets, b->ts_ms, b->val, b->is_float,
+             b->series_float};
+  Work W;
+  rc = run_pipeline(c, spec, B, b->group_members, goff, P, W, 0, nullptr,
+                    nullptr);
+  if (rc) return rc;
+  const int64_t G = (int64_t)goff.size() - 1;
+  rc = compact(c, P, G, W.out_val, W.out_emit, W.counts, out);
+  if (rc) return rc;
+  return finish(c, G, out);
+}
+
+}  // namespace
+
+// =========================================================================
+// C-ABI
+// =========================================================================
+extern "C" {
+
+int otsdb_abi_version(void) { return OTSDB_ABI_VERSION; }
+
+const char* otsdb_last_error(void) { return g_last_error.c_str(); }
+
+otsdb_status otsdb_ctx_create(int device, otsdb_ctx** out) {
+  if (!out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null out");
+  *out = nullptr;
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n)
+    return fail(OTSDB_E_DEVICE, "no HIP device %d (have %d)", device, n);
+  HIP_TRY(hipSetDevice(device));
+  otsdb_ctx* c = new otsdb_ctx();
+  c->device = device;
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIP_TRY(hipMalloc(&c->d_err, 256));
+  c->d_mm = (unsigned long long*)((char*)c->d_err + 64);
+  HIP_TRY(hipHostMalloc(&c->h_small, 64));
+  *out = c;
+  return OTSDB_OK;
+}
+
+void otsdb_ctx_destroy(otsdb_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->ws) hipFree(c->ws);
+  if (c->stage) hipFree(c->stage);
+  if (c->d_tiles) hipFree(c->d_tiles);
+  if (c->d_err) hipFree(c->d_err);
+  for (auto e : c->ev_pool) hipEventDestroy(e);
+  if (c->h_small) hipHostFree(c->h_small);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+otsdb_status otsdb_agg_lookup(const char* name, int32_t* agg_id) {
+  if (!name || !agg_id) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  for (int i = 0; i < OTSDB_AGG_COUNT_IDS; ++i)
+    if (strcmp(kAggs[i].key, name) == 0) {
+      *agg_id = i;
+      return OTSDB_OK;
+    }
+  return fail(OTSDB_E_NO_SUCH_ELEMENT, "No such aggregator: %s", name);
+}
+
+const char* otsdb_agg_name(int32_t agg_id) {
+  if (agg_id < 0 || agg_id >= OTSDB_AGG_COUNT_IDS) return nullptr;
+  return kAggs[agg_id].name;
+}
+
+int32_t otsdb_agg_interpolation(int32_t agg_id) {
+  if (agg_id < 0 || agg_id >= OTSDB_AGG_COUNT_IDS) return -1;
+  return kAggs[agg_id].interp;
+}
+
+otsdb_status otsdb_agg_plan(otsdb_ctx* c, const otsdb_query_spec* spec,
+                            const otsdb_batch* b, otsdb_sizes* out) {
+  if (!spec || !b || !out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  otsdb_status rc = check_spec(spec);
+  if (rc) return rc;
+  Params P;
+  rc = make_params(spec, &P);
+  if (rc) return rc;
+  out->n_buckets = P.nb;
+  out->max_out_points = b->n_groups * P.nb;
+  out->workspace_bytes =
+      b->n_series * (P.nb * 9 + 48) + b->n_groups * (P.nb * 9 + 8);
+  return OTSDB_OK;
+}
+
+otsdb_status otsdb_agg_run_device(otsdb_ctx* c, const otsdb_query_spec* spec,
+                                  const otsdb_batch* b, otsdb_result* out,
+                                  void* hip_stream) {
+  if (!c || !spec || !b || !out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t saved = c->stream;
+  if (hip_stream) c->stream = (hipStream_t)hip_stream;
+  std::vector<int64_t> goff;
+  otsdb_status rc = read_goff(c, b, true, goff);
+  if (!rc) rc = run_device_impl(c, spec, b, out, goff);
+  c->stream = saved;
+  return rc;
+}
+
+otsdb_status otsdb_agg_run(otsdb_ctx* c, const otsdb_query_spec* spec,
+                           const otsdb_batch* b, otsdb_result* out) {
+  if (!c || !spec || !b || !out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  std::vector<int64_t> goff;
+  otsdb_status rc = read_goff(c, b, false, goff);
+  if (rc) return rc;
+  const int64_t S = b->n_series, N = b->n_points, G = b->n_groups;
+  const int64_t M = goff.back();
+  if (S < 0 || N < 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
+  if (S > 0 && b->offsets[S] != N)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "offsets[S] != n_points");
+  for (int64_t m = 0; m < M; ++m)
+    if (b->group_members[m] < 0 || b->group_members[m] >= S)
+      return fail(OTSDB_E_ILLEGAL_ARGUMENT, "group member out of range");
+  const int64_t cap = out->capacity;
+  // staging layout in HBM
+  auto carve = [&](char* base) {
+    Carve cv{base};
+    void* p[11];
+    p[0] = cv.take<int64_t>(S + 1);
+    p[1] = cv.take<int64_t>(N + 1);
+    p[2] = cv.take<int64_t>(N + 1);
+    p[3] = b->is_float ? cv.take<uint8_t>(N + 1) : nullptr;
+    p[4] = b->series_float ? cv.take<uint8_t>(S + 1) : nullptr;
+    p[5] = cv.take<int64_t>(G + 1);
+    p[6] = cv.take<int64_t>(M + 1);
+    p[7] = cv.take<int64_t>(G + 1);
+    p[8] = cv.take<int64_t>(cap + 1);
+    p[9] = cv.take<int64_t>(cap + 1);
+    p[10] = cv.take<uint8_t>(cap + 1);
+    return std::make_pair(cv.off + 256, std::vector<void*>(p, p + 11));
+  };
+  const size_t need = carve(nullptr).first;
+  rc = ensure(&c->stage, &c->stage_cap, need);
+  if (rc) return rc;
+  auto pp = carve((char*)c->stage).second;
+  hipStream_t st = c->stream;
+  auto h2d = [&](void* d, const void* h, size_t n) -> otsdb_status {
+    if (n && h) HIP_TRY(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, st));
+    return OTSDB_OK;
+  };
+  if ((rc = h2d(pp[0], b->offsets, 8 * (S + 1)))) return rc;
+  if ((rc = h2d(pp[1], b->ts_ms, 8 * N))) return rc;
+  if ((rc = h2d(pp[2], b->val, 8 * N))) return rc;
+  if (b->is_float && (rc = h2d(pp[3], b->is_float, N))) return rc;
+  if (b->series_float && (rc = h2d(pp[4], b->series_float, S))) return rc;
+  if ((rc = h2d(pp[5], b->group_offsets, 8 * (G + 1)))) return rc;
+  if ((rc = h2d(pp[6], b->group_members, 8 * M))) return rc;
+  otsdb_batch db = *b;
+  db.offsets = (const int64_t*)pp[0];
+  db.ts_ms = (const int64_t*)pp[1];
+  db.val = (const int64_t*)pp[2];
+  db.is_float = (const uint8_t*)pp[3];
+  db.series_float = (const uint8_t*)pp[4];
+  db.group_offsets = (const int64_t*)pp[5];
+  db.group_members = (const int64_t*)pp[6];
+  otsdb_result dr;
+  dr.capacity = cap;
+  dr.offsets = (int64_t*)pp[7];
+  dr.ts = (int64_t*)pp[8];
+  dr.val = (int64_t*)pp[9];
+  dr.is_int = (uint8_t*)pp[10];
+  rc = run_device_impl(c, spec, &db, &dr, goff);
+  if (rc) return rc;
+  const int64_t total = c->h_small[1];
+  HIP_TRY(hipMemcpyAsync(out->offsets, dr.offsets, 8 * (G + 1),
+                         hipMemcpyDeviceToHost, st));
+  if (total > 0) {
+    HIP_TRY(hipMemcpyAsync(out->ts, dr.ts, 8 * total, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(out->val, dr.val, 8 * total, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(out->is_int, dr.is_int, total, hipMemcpyDeviceToHost, st));
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  return OTSDB_OK;
+}
+
+otsdb_status otsdb_agg_partials_device(otsdb_ctx* c,
+                                       const otsdb_query_spec* spec,
+                                       const otsdb_batch* b,
+                                       otsdb_partial* partials, uint8_t* emit,
+                                       void* hip_stream) {
+  if (!c || !spec || !b || !partials || !emit)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t saved = c->stream;
+  if (hip_stream) c->stream = (hipStream_t)hip_stream;
+  std::vector<int64_t> goff;
+  otsdb_status rc = read_goff(c, b, true, goff);
+  Params P;
+  if (!rc) rc = check_spec(spec);
+  if (!rc) rc = make_params(spec, &P);
+  if (!rc && !P.run_all && !P.fill && (double)b->n_series * (double)P.nb > 4.0e9)
+    rc = fail(OTSDB_E_UNSUPPORTED, "grid trimming is not supported across ranks");
+  if (!rc) {
+    BatchDev B{b->n_series, b->offsets, b->ts_ms, b->val, b->is_float,
+               b->series_float};
+    Work W;
+    const int64_t G = (int64_t)goff.size() - 1;
+    if (G * P.nb > 0) {
+      hipMemsetAsync(emit, 0, (size_t)G * P.nb, c->stream);
+      hipMemsetAsync(partials, 0, sizeof(otsdb_partial) * (size_t)G * P.nb,
+                     c->stream);
+    }
+    rc = run_pipeline(c, spec, B, b->group_members, goff, P, W, 1,
+                      (Packed*)partials, emit);
+    if (!rc) {
+      HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
+                             hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      const int err = (int)(c->h_small[0] & 0xFFFFFFFF);
+      if (err & ERR_RATE_TS)
+        rc = fail(OTSDB_E_ILLEGAL_STATE,
+                  "Next timestamp is supposed to be strictly greater");
+    }
+  }
+  c->stream = saved;
+  return rc;
+}
+
+otsdb_status otsdb_agg_finalize_device(otsdb_ctx* c,
+                                       const otsdb_query_spec* spec,
+                                       int64_t n_groups, int64_t n_buckets,
+                                       int32_t n_ranks,
+                                       const otsdb_partial* partials,
+                                       const uint8_t* emit, otsdb_result* out,
+                                       void* hip_stream) {
+  if (!c || !spec || !out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t saved = c->stream;
+  if (hip_stream) c->stream = (hipStream_t)hip_stream;
+  otsdb_status rc = check_spec(spec);
+  Params P;
+  if (!rc) rc = make_params(spec, &P);
+  if (!rc && P.nb != n_buckets)
+    rc = fail(OTSDB_E_ILLEGAL_ARGUMENT, "n_buckets %lld != plan %lld",
+              (long long)n_buckets, (long long)P.nb);
+  if (!rc) {
+    const int64_t G = n_groups, GB = G * P.nb;
+    auto carve = [&](char* base) {
+      Carve cv{base};
+      double* v = cv.take<double>(GB + 1);
+      uint8_t* e = cv.take<uint8_t>(GB + 1);
+      int64_t* cnt = cv.take<int64_t>(G + 1);
+      return std::make_tuple(cv.off + 256, v, e, cnt);
+    };
+    rc = ensure(&c->ws, &c->ws_cap, std::get<0>(carve(nullptr)));
+    if (!rc) {
+      auto t = carve((char*)c->ws);
+      double* ov = std::get<1>(t);
+      uint8_t* oe = std::get<2>(t);
+      int64_t* cnt = std::get<3>(t);
+      hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream);
+      bool ok = true;
+      if (GB > 0)
+        ok = with_monoid(spec->agg_id, [&](auto tag) {
+          using M = decltype(tag);
+          hipLaunchKernelGGL(k_finalize_ranks<M>, dim3(blocks_for(GB, 256)),
+                             dim3(256), 0, c->stream, GB, n_ranks,
+                             (const Packed*)partials, emit, ov, oe, c->d_err);
+        });
+      if (!ok) rc = fail(OTSDB_E_UNSUPPORTED, "aggregator %d across ranks",
+                         spec->agg_id);
+      if (!rc) rc = compact(c, P, G, ov, oe, cnt, out);
+      if (!rc) rc = finish(c, G, out);
+    }
+  }
+  c->stream = saved;
+  return rc;
+}
+
+otsdb_status otsdb_prof_enable(otsdb_ctx* c, int enable) {
+  if (!c) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->prof = enable != 0;
+  return OTSDB_OK;
+}
+
+otsdb_status otsdb_prof_read(otsdb_ctx* c, double* ms, int64_t* launches,
+                             int n, int reset) {
+  if (!c) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (auto& p : c->ev_pending) {
+    float t = 0.f;
+    HIP_TRY(hipEventSynchronize(p.second.second));
+    HIP_TRY(hipEventElapsedTime(&t, p.second.first, p.second.second));
+    c->prof_ms[p.first] += t;
+    c->prof_n[p.first] += 1;
+  }
+  c->ev_pending.clear();
+  c->ev_used = 0;
+  for (int i = 0; i < n && i < 8; ++i) {
+    if (ms) ms[i] = c->prof_ms[i];
+    if (launches) launches[i] = c->prof_n[i];
+  }
+  if (reset)
+    for (int i = 0; i < 8; ++i) {
+      c->prof_ms[i] = 0;
+      c->prof_n[i] = 0;
+    }
+  return OTSDB_OK;
+}
+
+otsdb_status otsdb_gen_counts_device(otsdb_ctx* c, const otsdb_gen_spec* g,
+                                     int64_t series0, int64_t n_series,
+                                     int64_t* counts, void* hip_stream) {
+  if (!c || !g || !counts) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  if (g->cadence_ms <= 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "cadence");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  GenP gp{g->seed, g->t0_ms, g->duration_ms, g->cadence_ms, g->kind};
+  if (n_series > 0)
+    hipLaunchKernelGGL(k_gen_counts, dim3(blocks_for(n_series, 4)), dim3(256),
+                       0, st, gp, series0, n_series, counts);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(st));
+  return OTSDB_OK;
+}
+
+otsdb_status otsdb_gen_fill_device(otsdb_ctx* c, const otsdb_gen_spec* g,
+                                   int64_t series0, int64_t n_series,
+                                   const int64_t* offsets, int64_t* ts_ms,
+                                   int64_t* val, void* hip_stream) {
+  if (!c || !g || !offsets || !ts_ms || !val)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  GenP gp{g->seed, g->t0_ms, g->duration_ms, g->cadence_ms, g->kind};
+  if (n_series > 0)
+    hipLaunchKernelGGL(k_gen_fill, dim3(blocks_for(n_series, 4)), dim3(256),
+                       0, st, gp, series0, n_series, offsets, ts_ms, val);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(st));
+  return OTSDB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,84 @@
+// kernels.h — HIP kernels of the aggregation engine (gfx950, wave64).
+//
+// Pipeline for one downsampled query:
+//   k_prep        per series: SpanGroup.add filter, seek/stop point bounds
+//                 (binary search), first bucket beyond the window
+//   k_bucketize   one wavefront per series streams its points from HBM
+//                 (16-B loads, 2 points per lane) and reduces them into epoch
+//                 aligned buckets with a segmented wave scan — Downsampler /
+//                 ValuesInInterval semantics
+//   k_transform   one wavefront per series sweeps its bucket row: fill policy
+//                 (FillingDownsampler), RateSpan, and the per-series
+//                 interpolation AggregationIterator applies (LERP/ZIM/MAX/
+//                 MIN/PREV), marking each bucket real / interpolated / absent
+//   k_group       one thread per (series chunk, bucket): the cross-series
+//                 aggregator, sequential in SpanCmp order inside a chunk
+//   k_combine     merges chunk partials in order, finalises, flags Infinity
+//   k_compact     per group: emitted buckets -> (ts, value) arrays
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "monoids.h"
+
+namespace otsdb {
+
+// row state of one (series, bucket)
+enum : uint8_t {
+  ST_ABSENT = 0,  // series does not contribute at this timestamp
+  ST_INTERP = 1,  // contributes an interpolated / held value
+  ST_REAL = 2,    // series has a real point here (emits the timestamp)
+  ST_KEPT = 3     // transient: kept rate point (k_transform pass 1)
+};
+
+// device error word bits
+enum : int {
+  ERR_NONE_MULTI = 1,   // `none` fed >1 value  -> E_ILLEGAL_DATA
+  ERR_INFINITY = 2,     // "Got Infinity"       -> E_ILLEGAL_STATE
+  ERR_RATE_TS = 4,      // non-increasing ts    -> E_ILLEGAL_STATE
+  ERR_SEL_TOO_BIG = 8,  // percentile group over the select limit
+};
+
+struct Params {
+  int64_t gbase;         // timestamp of bucket 0
+  int64_t interval;      // ms
+  double inv_interval;   // 1.0 / interval
+  int64_t nb;            // buckets per series row
+  int64_t seek_ts;       // first point considered: ts >= seek_ts
+  int64_t stop_ts;       // points with ts >= stop_ts are beyond the grid
+  int64_t start_ms, end_ms;
+  int64_t out_ts0;       // run_all: the single bucket's timestamp
+  int64_t counter_max, reset_value;
+  double fill_value;
+  // previous point of RateSpan's first rate: (0, 0) normally; the
+  // FillingDownsampler bucket align(start) when start is not aligned
+  int64_t rate_origin_ts;
+  double rate_origin_val;
+  int32_t run_all, fill, rate, counter, drop_resets, interp;
+  double pct;            // percentile / 100.0 (PercentileAgg)
+};
+
+struct BatchDev {
+  int64_t S;
+  const int64_t* offsets;
+  const int64_t* ts;
+  const int64_t* val;
+  const uint8_t* is_float;
+  const uint8_t* series_float;
+};
+
+struct SeriesMeta {
+  int64_t* lo;
+  int64_t* hi;
+  uint8_t* keep;
+  uint8_t* of_has;
+  int64_t* of_ts;
+  double* of_val;
+};
+
+struct Rows {
+  double* val;     // [S * nb]
+  uint8_t* state;  // [S * nb]
+};
+
+}  // namespace otsdb

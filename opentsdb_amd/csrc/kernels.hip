@@ -1,0 +1,812 @@
+// kernels.hip — device code of the aggregation engine (gfx950, wave64).
+// See kernels.h for the pipeline.  Reference semantics cited per kernel
+// (paths under /root/reference).
+//
+// Compiled with -ffp-contract=off: Java evaluates `y0 + (x-x0)*(y1-y0)/(x1-x0)`
+// and every aggregator loop with separate roundings, so no FMA may be formed.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace otsdb {
+
+#define LANE (threadIdx.x & 63)
+
+DEV double bits_to_double(int64_t b) { return __longlong_as_double(b); }
+
+// Java `t - t % interval` (Downsampler.alignTimestamp, Downsampler.java:452)
+DEV int64_t align_ts(int64_t t, int64_t iv) { return t - t % iv; }
+
+// floor(rel / interval) for rel >= 0 without a 64-bit divide: double
+// reciprocal estimate + one correction step each way.
+DEV int64_t bucket_of(const Params& P, int64_t ts) {
+  if (P.run_all) return 0;
+  const int64_t rel = ts - P.gbase;
+  int64_t q = (int64_t)((double)rel * P.inv_interval);
+  int64_t r = rel - q * P.interval;
+  if (r < 0) { --q; r += P.interval; }
+  if (r < 0) { --q; r += P.interval; }
+  if (r >= P.interval) { ++q; r -= P.interval; }
+  if (r >= P.interval) { ++q; }
+  return q;
+}
+
+DEV int64_t bucket_ts(const Params& P, int64_t b) {
+  return P.run_all ? P.out_ts0 : P.gbase + b * P.interval;
+}
+
+DEV double point_value(const BatchDev& B, int64_t i, int64_t bits, int sf) {
+  const int f = B.is_float ? (int)B.is_float[i] : sf;
+  return f ? bits_to_double(bits) : (double)bits;
+}
+
+// first index in [a, b) with ts >= t (the seek of Span.Iterator /
+// MockSeekableView on sorted points)
+DEV int64_t lower_bound(const int64_t* ts, int64_t a, int64_t b, int64_t t) {
+  while (a < b) {
+    const int64_t m = a + ((b - a) >> 1);
+    if (ts[m] < t) a = m + 1;
+    else b = m;
+  }
+  return a;
+}
+
+DEV int64_t wave_incl_max(int64_t x) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t y = __shfl_up(x, d);
+    if (LANE >= d) x = x > y ? x : y;
+  }
+  return x;
+}
+
+// ------------------------------------------------------------------------
+// k_prep: SpanGroup.add filter (SpanGroup.java:321-338), the Downsampler
+// seek (ValuesInInterval.seekInterval rounds up, Downsampler.java:431) or
+// the "all" bounds (Downsampler.java:354-379), and the first bucket past the
+// window (the point AggregationIterator keeps in its "next" slot, used to
+// interpolate up to end_time, AggregationIterator.java:760-775).
+// One thread per series.
+// ------------------------------------------------------------------------
+template <class M>
+__global__ void k_prep(Params P, BatchDev B, SeriesMeta SM) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= B.S) return;
+  const int64_t p0 = B.offsets[s], p1 = B.offsets[s + 1];
+  const bool keep = p1 > p0 && B.ts[p0] <= P.end_ms && B.ts[p1 - 1] >= P.start_ms;
+  SM.keep[s] = keep;
+  int64_t lo = p1, hi = p1;
+  uint8_t of_has = 0;
+  int64_t of_ts = 0;
+  double of_val = 0.0;
+  if (keep) {
+    lo = lower_bound(B.ts, p0, p1, P.seek_ts);
+    hi = lower_bound(B.ts, lo, p1, P.stop_ts);
+    if (!P.run_all && P.fill == 0 && hi < p1) {
+      const int sf = B.series_float ? (int)B.series_float[s] : 1;
+      const int64_t t = B.ts[hi];
+      of_ts = align_ts(t, P.interval);
+      const int64_t e = of_ts + P.interval;
+      M st = M::init();
+      for (int64_t i = hi; i < p1 && B.ts[i] < e; ++i)
+        st.push(point_value(B, i, B.val[i], sf));
+      int err = 0;
+      of_val = st.finish(&err);
+      of_has = 1;
+    }
+  }
+  SM.lo[s] = lo;
+  SM.hi[s] = hi;
+  SM.of_has[s] = of_has;
+  SM.of_ts[s] = of_ts;
+  SM.of_val[s] = of_val;
+}
+
+// ------------------------------------------------------------------------
+// k_bucketize: Downsampler.next / ValuesInInterval (Downsampler.java:162-228,
+// :461-479) for every series at once.  One wavefront per series; each lane
+// takes 2 consecutive points per step (16-byte loads of ts and value, fully
+// coalesced 1 KiB per wave instruction), computes their epoch-aligned bucket
+// and the wave reduces equal-bucket runs with a segmented inclusive scan.
+// Buckets that close inside the step are written to the series' row; the
+// open one is carried to the next step.
+// ------------------------------------------------------------------------
+template <class M>
+__global__ __launch_bounds__(256) void k_bucketize(Params P, BatchDev B,
+                                                   SeriesMeta SM, Rows R) {
+  const int lane = LANE;
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= B.S) return;
+  if (!SM.keep[s]) return;
+  const int64_t lo = SM.lo[s], hi = SM.hi[s];
+  if (lo >= hi) return;
+  const int sf = B.series_float ? (int)B.series_float[s] : 1;
+  double* rowv = R.val + s * P.nb;
+  uint8_t* rows = R.state + s * P.nb;
+
+  int carry_key = INT32_MIN;
+  M carry = M::init();
+
+  const int64_t base0 = lo & ~(int64_t)1;
+  // software pipeline: loads of step k+1 are issued before step k reduces
+  int64_t i0 = base0 + 2 * lane;
+  int64_t ta = 0, tb = 0, va = 0, vb = 0;
+  auto load = [&](int64_t i, int64_t& t0, int64_t& t1, int64_t& v0,
+                  int64_t& v1) {
+    if (i + 1 < hi) {
+      const longlong2 tt = *reinterpret_cast<const longlong2*>(B.ts + i);
+      const longlong2 vv = *reinterpret_cast<const longlong2*>(B.val + i);
+      t0 = tt.x; t1 = tt.y; v0 = vv.x; v1 = vv.y;
+    } else if (i < hi) {
+      t0 = B.ts[i]; v0 = B.val[i];
+    }
+  };
+  load(i0, ta, tb, va, vb);
+  for (int64_t base = base0; base < hi; base += 128) {
+    const int64_t ia = base + 2 * lane, ib = ia + 1;
+    const int64_t cta = ta, ctb = tb, cva = va, cvb = vb;
+    if (base + 128 < hi) load(ia + 128, ta, tb, va, vb);
+
+    const bool inA = ia >= lo && ia < hi;
+    const bool inB = ib >= lo && ib < hi;
+    const int kA = inA ? (int)bucket_of(P, cta) : (ia < lo ? -1 : INT32_MAX);
+    const int kB = inB ? (int)bucket_of(P, ctb) : (ib < lo ? -1 : INT32_MAX);
+    M sA = inA ? M::from(point_value(B, ia, cva, sf)) : M::init();
+    const M sB = inB ? M::from(point_value(B, ib, cvb, sf)) : M::init();
+    if (lane == 0 && carry_key == kA) sA = M::combine(carry, sA);
+    // inclusive segmented scan keyed by each lane's last bucket
+    int key = kB;
+    M st = (kA == kB) ? M::combine(sA, sB) : sB;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int k2 = __shfl_up(key, d);
+      M o = st;
+      o.shfl_up(d);
+      if (lane >= d && k2 == key) st = M::combine(o, st);
+    }
+    // bucket of element A closes inside this lane
+    const int pkey = __shfl_up(key, 1);
+    M pst = st;
+    pst.shfl_up(1);
+    const int next_kA = __shfl_down(kA, 1);
+    int err = 0;
+    if (inA && kA != kB) {
+      const M full = (lane > 0 && pkey == kA) ? M::combine(pst, sA) : sA;
+      rowv[kA] = full.finish(&err);
+      rows[kA] = ST_REAL;
+    }
+    if (inB && lane < 63 && next_kA != kB) {
+      rowv[kB] = st.finish(&err);
+      rows[kB] = ST_REAL;
+    }
+    // carry the bucket still open at lane 63 (broadcast lane 63's state)
+    carry_key = __shfl(key, 63);
+    {
+      Packed p = st.pack();
+      p.x = __shfl(p.x, 63);
+      p.y = __shfl(p.y, 63);
+      p.z = __shfl(p.z, 63);
+      p.w = __shfl(p.w, 63);
+      carry = M::unpack(p);
+    }
+  }
+  if (lane == 0 && carry_key >= 0 && carry_key < P.nb) {
+    int err = 0;
+    rowv[carry_key] = carry.finish(&err);
+    rows[carry_key] = ST_REAL;
+  }
+}
+
+// ------------------------------------------------------------------------
+// interpolation of a series between two of its points, exactly as
+// AggregationIterator.nextDoubleValue (AggregationIterator.java:772-793)
+// ------------------------------------------------------------------------
+DEV double interp_value(int method, int64_t x, int64_t x0, double y0,
+                        int64_t x1, double y1) {
+  switch (method) {
+    case 0: return y0 + (double)(x - x0) * (y1 - y0) / (double)(x1 - x0);
+    case 1: return 0.0;
+    case 2: return kDoubleMax;
+    case 3: return -kDoubleMax;
+    default: return y0;
+  }
+}
+
+// ------------------------------------------------------------------------
+// k_transform: per-series bucket row -> what the series contributes at each
+// union timestamp of AggregationIterator (one wavefront per series):
+//  * FillingDownsampler (FillingDownsampler.java:172-298): every grid bucket
+//    is a point; missing ones take the fill value;
+//  * RateSpan (RateSpan.java:121-180) over the bucket points, incl. the junk
+//    first rate vs (0, 0) and the hold-previous-rate rule of
+//    AggregationIterator (:448-459, :744-753);
+//  * otherwise interpolation between the series' own points (:754-793),
+//    contributing iff first <= x <= last (or a point exists past the window).
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_transform(Params P, int64_t S,
+                                                   SeriesMeta SM, Rows R,
+                                                   int* err_word) {
+  const int lane = LANE;
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= S) return;
+  if (!SM.keep[s]) return;
+  const int64_t nb = P.nb;
+  double* rowv = R.val + s * nb;
+  uint8_t* rows = R.state + s * nb;
+  const bool fill = P.fill != 0 && !P.run_all;
+
+  if (!P.rate) {
+    if (fill) {
+      for (int64_t c0 = 0; c0 < nb; c0 += 64) {
+        const int64_t b = c0 + lane;
+        if (b < nb && rows[b] != ST_REAL) {
+          rowv[b] = P.fill_value;
+          rows[b] = ST_REAL;
+        }
+      }
+      return;
+    }
+    // NONE fill: interpolate inside gaps, and toward the point past the
+    // window when there is one.
+    int64_t carry_idx = -1;
+    double carry_val = 0.0;
+    for (int64_t c0 = 0; c0 < nb; c0 += 64) {
+      const int64_t b = c0 + lane;
+      const bool p = b < nb && rows[b] == ST_REAL;
+      const double v = p ? rowv[b] : 0.0;
+      const int64_t incl = wave_incl_max(p ? b : -1);
+      int64_t prev = __shfl_up(incl, 1);
+      if (lane == 0) prev = -1;
+      prev = prev > carry_idx ? prev : carry_idx;
+      const double yp = __shfl(v, (int)((prev - c0) & 63));
+      const double yprev = prev >= c0 ? yp : carry_val;
+      uint64_t gaps = __ballot(p && prev >= 0 && prev < b - 1);
+      while (gaps) {
+        const int g = __builtin_ctzll(gaps);
+        gaps &= gaps - 1;
+        const int64_t k0 = __shfl(prev, g), k1 = c0 + g;
+        const double y0 = __shfl(yprev, g), y1 = __shfl(v, g);
+        const int64_t x0 = bucket_ts(P, k0), x1 = bucket_ts(P, k1);
+        for (int64_t j = k0 + 1 + lane; j < k1; j += 64) {
+          rowv[j] = interp_value(P.interp, bucket_ts(P, j), x0, y0, x1, y1);
+          rows[j] = ST_INTERP;
+        }
+      }
+      const int64_t last = __shfl(incl, 63);
+      if (last >= 0) {
+        carry_val = __shfl(v, (int)((last - c0) & 63));
+        carry_idx = last;
+      }
+    }
+    if (SM.of_has[s] && carry_idx >= 0) {
+      const int64_t x0 = bucket_ts(P, carry_idx), x1 = SM.of_ts[s];
+      const double y1 = SM.of_val[s];
+      for (int64_t j = carry_idx + 1 + lane; j < nb; j += 64) {
+        rowv[j] = interp_value(P.interp, bucket_ts(P, j), x0, carry_val, x1, y1);
+        rows[j] = ST_INTERP;
+      }
+    }
+    return;
+  }
+
+  // ---------------- rate: pass 1 computes the rate points ----------------
+  const double cmax_d = (double)P.counter_max;
+  // previous source point: the (0, 0) origin of RateSpan's first rate, or the
+  // FillingDownsampler bucket before the grid when start is unaligned
+  int64_t carry_pts = P.rate_origin_ts;
+  double carry_pv = P.rate_origin_val;
+  int64_t r0_idx = -1, last_kept = -1;
+  double r0_val = 0.0;
+  int kept_count = 0;
+  int bad_ts = 0;
+  for (int64_t c0 = 0; c0 < nb; c0 += 64) {
+    const int64_t b = c0 + lane;
+    const bool inb = b < nb;
+    const uint8_t st = inb ? rows[b] : 0;
+    const bool pt = inb && (fill || st == ST_REAL);
+    const double pv = (st == ST_REAL) ? rowv[b] : P.fill_value;
+    const int64_t t = bucket_ts(P, b);
+    const int64_t incl = wave_incl_max(pt ? b : -1);
+    int64_t prev = __shfl_up(incl, 1);
+    if (lane == 0) prev = -1;
+    const double vp = __shfl(pv, (int)((prev - c0) & 63));
+    int64_t tprev;
+    double vprev;
+    if (prev >= c0) {
+      tprev = bucket_ts(P, prev);
+      vprev = vp;
+    } else {
+      tprev = carry_pts;
+      vprev = carry_pv;
+    }
+    bool kept = false;
+    double rate = 0.0;
+    if (pt) {
+      if (t <= tprev) bad_ts = 1;
+      const double dt = (double)(t - tprev) / 1000.0;
+      double diff = pv - vprev;
+      if (P.counter && diff < 0) {
+        if (!P.drop_resets) {
+          kept = true;
+          diff = cmax_d - vprev + pv;
+          const double r = diff / dt;
+          rate = (P.reset_value > 0 && r > (double)P.reset_value) ? 0.0 : r;
+        }
+      } else {
+        kept = true;
+        rate = diff / dt;
+      }
+    }
+    if (inb) {
+      if (pt && kept) {
+        rowv[b] = rate;
+        rows[b] = ST_KEPT;
+      } else {
+        rows[b] = ST_ABSENT;
+      }
+    }
+    const uint64_t km = __ballot(pt && kept);
+    if (km) {
+      const int f = __builtin_ctzll(km);
+      if (r0_idx < 0) {
+        r0_idx = c0 + f;
+        r0_val = __shfl(rate, f);
+      }
+      kept_count += __popcll(km);
+      if (kept_count > 2) kept_count = 2;
+      last_kept = c0 + 63 - __builtin_clzll(km);
+    }
+    const int64_t lp = __shfl(incl, 63);
+    if (lp >= 0) {
+      carry_pts = bucket_ts(P, lp);
+      carry_pv = __shfl(pv, (int)((lp - c0) & 63));
+    }
+  }
+  if (__ballot(bad_ts) && lane == 0) atomicOr(err_word, ERR_RATE_TS);
+  // a rate point past the window keeps the series contributing to the end
+  bool of_kept = false;
+  if (!fill && SM.of_has[s]) {
+    const double diff = SM.of_val[s] - carry_pv;
+    of_kept = !(P.counter && diff < 0 && P.drop_resets);
+  }
+  const int total = kept_count + (of_kept ? 1 : 0);
+
+  // ---------------- rate: pass 2 writes contributions --------------------
+  int64_t carry_k = -1;
+  double carry_kv = 0.0;
+  for (int64_t c0 = 0; c0 < nb; c0 += 64) {
+    const int64_t b = c0 + lane;
+    const bool inb = b < nb;
+    const uint8_t st = inb ? rows[b] : 0;
+    const bool k = st == ST_KEPT;
+    const double kv = k ? rowv[b] : 0.0;
+    const int64_t incl = wave_incl_max(k ? b : -1);
+    const int64_t lk = incl > carry_k ? incl : carry_k;
+    const double lv = __shfl(kv, (int)((incl - c0) & 63));
+    const double held = incl >= c0 ? lv : (lk >= 0 ? carry_kv : r0_val);
+    if (inb) {
+      if (total < 2 || (b > last_kept && !of_kept)) {
+        rows[b] = ST_ABSENT;
+      } else if (k && b != r0_idx) {
+        rows[b] = ST_REAL;
+      } else {
+        rowv[b] = held;
+        rows[b] = ST_INTERP;
+      }
+    }
+    const int64_t lk63 = __shfl(incl, 63);
+    if (lk63 >= 0) {
+      carry_k = lk63;
+      carry_kv = __shfl(kv, (int)((lk63 - c0) & 63));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------
+// k_group: cross-series aggregation (AggregationIterator.next + the
+// aggregator's runDouble over the contributing spans in span order,
+// AggregationIterator.java:514-567, :635-647, :735-797).  One thread per
+// (chunk of a group's members, bucket); the members of a chunk are pushed in
+// SpanCmp order, so a group of <= CHUNK series reproduces the Java sum
+// bit for bit.  Single-chunk groups finish here; others leave partials.
+// ------------------------------------------------------------------------
+template <class M>
+__global__ __launch_bounds__(256) void k_group(
+    int64_t nb, int64_t n_tiles, const int64_t* __restrict__ tile_g,
+    const int64_t* __restrict__ tile_m0, const int64_t* __restrict__ tile_m1,
+    const uint8_t* __restrict__ tile_single, const int64_t* __restrict__ members,
+    Rows R, Packed* __restrict__ partial, uint8_t* __restrict__ tile_emit,
+    double* __restrict__ out_val, uint8_t* __restrict__ out_emit,
+    int* err_word, int always_partial) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t t = idx / nb;
+  if (t >= n_tiles) return;
+  const int64_t b = idx - t * nb;
+  const int64_t m0 = tile_m0[t], m1 = tile_m1[t];
+  M st = M::init();
+  int emit = 0;
+  int64_t m = m0;
+  for (; m + 4 <= m1; m += 4) {
+    int64_t off[4];
+    uint8_t sv[4];
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) off[u] = members[m + u] * nb + b;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sv[u] = R.state[off[u]];
+      v[u] = R.val[off[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (sv[u]) {
+        st.push(v[u]);
+        emit |= sv[u] == ST_REAL;
+      }
+    }
+  }
+  for (; m < m1; ++m) {
+    const int64_t off = members[m] * nb + b;
+    const uint8_t sv = R.state[off];
+    if (sv) {
+      st.push(R.val[off]);
+      emit |= sv == ST_REAL;
+    }
+  }
+  if (tile_single[t] && !always_partial) {
+    const int64_t o = tile_g[t] * nb + b;
+    double r = 0.0;
+    if (emit) {
+      int e = 0;
+      r = st.finish(&e);
+      if (is_inf(r)) e |= ERR_INFINITY;
+      if (e) atomicOr(err_word, e);
+    }
+    out_val[o] = r;
+    out_emit[o] = (uint8_t)emit;
+  } else {
+    partial[t * nb + b] = st.pack();
+    tile_emit[t * nb + b] = (uint8_t)emit;
+  }
+}
+
+// merge the chunk partials of multi-chunk groups in chunk order
+template <class M>
+__global__ __launch_bounds__(256) void k_combine(
+    int64_t nb, int64_t n_groups, const int64_t* __restrict__ grp_g,
+    const int64_t* __restrict__ grp_t0, const int64_t* __restrict__ grp_t1,
+    const Packed* __restrict__ partial, const uint8_t* __restrict__ tile_emit,
+    double* __restrict__ out_val, uint8_t* __restrict__ out_emit,
+    Packed* __restrict__ out_partial, int* err_word) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = idx / nb;
+  if (i >= n_groups) return;
+  const int64_t b = idx - i * nb;
+  const int64_t g = grp_g[i];
+  M st = M::init();
+  int emit = 0;
+  for (int64_t t = grp_t0[i]; t < grp_t1[i]; ++t) {
+    st = M::combine(st, M::unpack(partial[t * nb + b]));
+    emit |= tile_emit[t * nb + b];
+  }
+  const int64_t o = g * nb + b;
+  if (out_partial) {
+    out_partial[o] = st.pack();
+    out_emit[o] = (uint8_t)emit;
+    return;
+  }
+  double r = 0.0;
+  if (emit) {
+    int e = 0;
+    r = st.finish(&e);
+    if (is_inf(r)) e |= ERR_INFINITY;
+    if (e) atomicOr(err_word, e);
+  }
+  out_val[o] = r;
+  out_emit[o] = (uint8_t)emit;
+}
+
+// multi-GPU: merge per-rank partials in rank (= series) order, finalise
+template <class M>
+__global__ __launch_bounds__(256) void k_finalize_ranks(
+    int64_t GB, int n_ranks, const Packed* __restrict__ partials,
+    const uint8_t* __restrict__ emits, double* __restrict__ out_val,
+    uint8_t* __restrict__ out_emit, int* err_word) {
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= GB) return;
+  M st = M::init();
+  int emit = 0;
+  for (int r = 0; r < n_ranks; ++r) {
+    st = M::combine(st, M::unpack(partials[(int64_t)r * GB + o]));
+    emit |= emits[(int64_t)r * GB + o];
+  }
+  double v = 0.0;
+  if (emit) {
+    int e = 0;
+    v = st.finish(&e);
+    if (is_inf(v)) e |= ERR_INFINITY;
+    if (e) atomicOr(err_word, e);
+  }
+  out_val[o] = v;
+  out_emit[o] = (uint8_t)emit;
+}
+
+// ------------------------------------------------------------------------
+// Percentile / median across series (PercentileAgg.runDouble,
+// Aggregators.java:687-706 — LEGACY estimation whatever the name says; and
+// Median.runDouble, :412-431).  One thread per (group, bucket) for groups of
+// up to SEL_K series: non-NaN contributions sorted in LDS, then selected.
+// ------------------------------------------------------------------------
+constexpr int SEL_K = 32;
+constexpr int SEL_THREADS = 128;
+
+DEV uint64_t order_key(double v) {  // total order, -0.0 < 0.0 (compareTo)
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
+}
+
+__global__ __launch_bounds__(SEL_THREADS) void k_group_select(
+    int64_t nb, int64_t n_tiles, const int64_t* __restrict__ tile_g,
+    const int64_t* __restrict__ tile_m0, const int64_t* __restrict__ tile_m1,
+    const uint8_t* __restrict__ tile_single,
+    const int64_t* __restrict__ members, Rows R, double* __restrict__ out_val,
+    uint8_t* __restrict__ out_emit, int* err_word, int median, double p) {
+  __shared__ uint64_t buf[SEL_K * SEL_THREADS];
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t t = idx / nb;
+  if (t >= n_tiles) return;
+  const int64_t b = idx - t * nb;
+  if (!tile_single[t]) {
+    atomicOr(err_word, ERR_SEL_TOO_BIG);
+    return;
+  }
+  const int64_t m0 = tile_m0[t], m1 = tile_m1[t];
+  if (m1 - m0 > SEL_K) {
+    atomicOr(err_word, ERR_SEL_TOO_BIG);
+    return;
+  }
+  int n = 0, emit = 0;
+  for (int64_t m = m0; m < m1; ++m) {
+    const int64_t off = members[m] * nb + b;
+    const uint8_t sv = R.state[off];
+    if (!sv) continue;
+    emit |= sv == ST_REAL;
+    const double v = R.val[off];
+    if (is_nan(v)) continue;
+    // insertion sort by total order
+    const uint64_t k = order_key(v);
+    int j = n++;
+    while (j > 0 && buf[(j - 1) * SEL_THREADS + threadIdx.x] > k) {
+      buf[j * SEL_THREADS + threadIdx.x] = buf[(j - 1) * SEL_THREADS + threadIdx.x];
+      --j;
+    }
+    buf[j * SEL_THREADS + threadIdx.x] = k;
+  }
+  auto val_at = [&](int i) {
+    const uint64_t k = buf[i * SEL_THREADS + threadIdx.x];
+    const uint64_t u = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFULL) : ~k;
+    return __longlong_as_double((long long)u);
+  };
+  double r = 0.0;
+  if (emit) {
+    if (n == 0) {
+      r = qnan();
+    } else if (median) {
+      r = val_at(n / 2);
+    } else if (n == 1) {
+      r = val_at(0);
+    } else {
+      const double pos = p * (double)(n + 1);
+      const double fpos = __builtin_floor(pos);
+      const int ip = (int)fpos;
+      const double dif = pos - fpos;
+      if (pos < 1) r = val_at(0);
+      else if (pos >= (double)n) r = val_at(n - 1);
+      else {
+        const double lower = val_at(ip - 1), upper = val_at(ip);
+        r = lower + dif * (upper - lower);
+      }
+    }
+    if (is_inf(r)) atomicOr(err_word, ERR_INFINITY);
+  }
+  const int64_t o = tile_g[t] * nb + b;
+  out_val[o] = r;
+  out_emit[o] = (uint8_t)emit;
+}
+
+// ------------------------------------------------------------------------
+// k_compact: dense (group, bucket) results -> per-group (ts, value) arrays.
+// One wavefront per group.  mode 0 counts, mode 1 scatters.
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_compact(
+    Params P, int64_t G, const double* __restrict__ out_val,
+    const uint8_t* __restrict__ out_emit, int64_t* __restrict__ counts,
+    const int64_t* __restrict__ offsets, int64_t cap, int64_t* __restrict__ r_ts,
+    int64_t* __restrict__ r_val, uint8_t* __restrict__ r_isint, int mode) {
+  const int lane = LANE;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= G) return;
+  const int64_t nb = P.nb;
+  int64_t pos = mode ? offsets[g] : 0;
+  for (int64_t c0 = 0; c0 < nb; c0 += 64) {
+    const int64_t b = c0 + lane;
+    const bool e = b < nb && out_emit[g * nb + b];
+    const uint64_t m = __ballot(e);
+    if (mode && e) {
+      const int64_t p = pos + __popcll(m & ((1ULL << lane) - 1));
+      if (p < cap) {
+        r_ts[p] = bucket_ts(P, b);
+        r_val[p] = __double_as_longlong(out_val[g * nb + b]);
+        r_isint[p] = 0;
+      }
+    }
+    pos += __popcll(m);
+  }
+  if (!mode && lane == 0) counts[g] = pos;
+}
+
+// exclusive scan of counts[G] -> offsets[G+1] (single workgroup; G is the
+// number of output groups, small next to the point stream)
+__global__ __launch_bounds__(1024) void k_scan(int64_t G,
+                                               const int64_t* __restrict__ in,
+                                               int64_t* __restrict__ out) {
+  __shared__ int64_t part[1024];
+  const int tid = threadIdx.x;
+  const int64_t per = (G + 1023) / 1024;
+  const int64_t a = tid * per, e = (a + per < G) ? a + per : G;
+  int64_t sum = 0;
+  for (int64_t i = a; i < e; ++i) sum += in[i];
+  part[tid] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const int64_t x = tid >= d ? part[tid - d] : 0;
+    __syncthreads();
+    part[tid] += x;
+    __syncthreads();
+  }
+  int64_t run = part[tid] - sum;
+  for (int64_t i = a; i < e; ++i) {
+    out[i] = run;
+    run += in[i];
+  }
+  if (tid == 1023) out[G] = part[1023];
+}
+
+// bounds of the data inside [seek_ts, stop_ts) (grid trimming for very wide
+// windows)
+__global__ void k_bounds(Params P, BatchDev B, unsigned long long* mm) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= B.S) return;
+  const int64_t p0 = B.offsets[s], p1 = B.offsets[s + 1];
+  if (p1 <= p0) return;
+  const int64_t lo = lower_bound(B.ts, p0, p1, P.seek_ts);
+  const int64_t hi = lower_bound(B.ts, lo, p1, P.stop_ts);
+  if (lo >= hi) return;
+  atomicMin(&mm[0], (unsigned long long)B.ts[lo]);
+  atomicMax(&mm[1], (unsigned long long)B.ts[hi - 1]);
+}
+
+// ------------------------------------------------------------------------
+// Synthetic workload generator (bit-identical to
+// or_gen_fill in oracle/otsdb_oracle.c).  One wavefront per series.
+// ------------------------------------------------------------------------
+constexpr uint64_t GOLDEN = 0x9E3779B97F4A7C15ULL;
+DEV uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+struct GenSeries {
+  uint64_t key;
+  int64_t n, first, last, phase;
+  int n_out;
+  int64_t out_lo[2], out_hi[2];
+  int64_t counter0;
+};
+
+struct GenP {
+  uint64_t seed;
+  int64_t t0_ms, duration_ms, cadence_ms;
+  int kind;
+};
+
+DEV GenSeries gen_params(const GenP& g, int64_t s) {
+  GenSeries p;
+  const uint64_t key = mix64((g.seed ^ (uint64_t)s) + GOLDEN);
+  uint64_t r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = mix64(key + GOLDEN * (uint64_t)(j + 1));
+  p.key = key;
+  p.n = g.duration_ms / g.cadence_ms;
+  p.phase = (int64_t)(r[0] % (uint64_t)g.cadence_ms);
+  p.first = 0;
+  p.last = p.n;
+  if (p.n > 1 && (r[1] % 100) < 5) {
+    const int64_t cut = (int64_t)(r[3] % (uint64_t)(p.n / 2));
+    if (r[2] & 1) p.first = cut;
+    else p.last = p.n - cut;
+  }
+  p.n_out = (int)(r[4] % 3);
+  const int64_t pph = 3600000 / g.cadence_ms;
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    const uint64_t x = r[5 + o];
+    const int64_t lo = (int64_t)(x % (uint64_t)(p.n > 0 ? p.n : 1));
+    p.out_lo[o] = lo;
+    p.out_hi[o] = lo + (int64_t)(1 + ((x >> 32) % 6)) * pph;
+  }
+  p.counter0 = (int64_t)(r[7] & 0xFFFFFFFFULL);
+  return p;
+}
+
+DEV bool gen_present(const GenSeries& p, int64_t i) {
+  if (i < p.first || i >= p.last) return false;
+  for (int o = 0; o < p.n_out; ++o)
+    if (i >= p.out_lo[o] && i < p.out_hi[o]) return false;
+  const uint64_t h = mix64(p.key ^ ((uint64_t)(i + 1) * 0xD1B54A32D192ED03ULL));
+  return (h >> 11) >= 180143985094819ULL;
+}
+
+__global__ __launch_bounds__(256) void k_gen_counts(GenP g, int64_t series0,
+                                                    int64_t n_series,
+                                                    int64_t* counts) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= n_series) return;
+  const GenSeries p = gen_params(g, series0 + w);
+  int64_t c = 0;
+  for (int64_t c0 = 0; c0 < p.n; c0 += 64) {
+    const int64_t i = c0 + LANE;
+    c += __popcll(__ballot(i < p.n && gen_present(p, i)));
+  }
+  if (LANE == 0) counts[w] = c;
+}
+
+__global__ __launch_bounds__(256) void k_gen_fill(GenP g, int64_t series0,
+                                                  int64_t n_series,
+                                                  const int64_t* offsets,
+                                                  int64_t* ts, int64_t* val) {
+  const int lane = LANE;
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= n_series) return;
+  const GenSeries p = gen_params(g, series0 + w);
+  int64_t pos = offsets[w];
+  int64_t counter = p.counter0;
+  for (int64_t c0 = 0; c0 < p.n; c0 += 64) {
+    const int64_t i = c0 + lane;
+    const bool inr = i < p.n;
+    const uint64_t hv = mix64(p.key + (uint64_t)(i + 1) * 0x8CB92BA72F3D8DD7ULL);
+    int64_t v = 0;
+    if (g.kind == 2) {
+      // counter: running sum of increments, reset to 0 (segmented scan)
+      int rst = inr && ((hv >> 40) % 10000) == 0;
+      int64_t x = (!inr || rst) ? 0 : (int64_t)(500 + (hv % 1001));
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int r2 = __shfl_up(rst, d);
+        const int64_t x2 = __shfl_up(x, d);
+        if (lane >= d && !rst) {
+          x += x2;
+          rst |= r2;
+        }
+      }
+      v = rst ? x : counter + x;
+      counter = __shfl(v, 63);
+    } else if (g.kind == 0) {
+      v = __double_as_longlong((double)(hv >> 11) * 0x1p-53 * 100.0);
+    } else {
+      v = (int64_t)((hv >> 11) % 100);
+    }
+    const bool pr = inr && gen_present(p, i);
+    const uint64_t m = __ballot(pr);
+    if (pr) {
+      const int64_t q = pos + __popcll(m & ((1ULL << lane) - 1));
+      ts[q] = g.t0_ms + p.phase + i * g.cadence_ms;
+      val[q] = v;
+    }
+    pos += __popcll(m);
+  }
+}
+
+}  // namespace otsdb

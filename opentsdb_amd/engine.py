@@ -1,0 +1,205 @@
+"""The aggregation engine as the reference's callers see it.
+
+`Engine.run(spec, batch)` is the batched replacement of
+`for each SpanGroup: SpanGroup.iterator()` (SpanGroup.java:525-530) — one
+native call evaluates every group of a query on the GPU.  Results come back as
+`DataPoints` (array-backed SeekableView, DataPoints.java:29-240 /
+SeekableView.java:37-71), so code written against the reference's iterator
+contract keeps working.
+
+The native library is mandatory: there is no CPU fallback.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .core import (IllegalStateException, NoSuchElementException,
+                   raise_for_status)
+
+
+class DataPoint:
+    """One aggregated point (DataPoint.java:20)."""
+    __slots__ = ("_ts", "_bits", "_is_int")
+
+    def __init__(self, ts, bits, is_int):
+        self._ts, self._bits, self._is_int = int(ts), int(bits), bool(is_int)
+
+    def timestamp(self):
+        return self._ts
+
+    def isInteger(self):
+        return self._is_int
+
+    def longValue(self):
+        if not self._is_int:
+            raise TypeError("value is a double")
+        return self._bits
+
+    def doubleValue(self):
+        if self._is_int:
+            raise TypeError("value is a long")
+        return float(np.int64(self._bits).view(np.float64))
+
+    def toDouble(self):
+        return float(self._bits) if self._is_int else self.doubleValue()
+
+
+class DataPoints:
+    """The output series of one group, array-backed."""
+
+    def __init__(self, ts, bits, is_int):
+        self.ts = ts
+        self.bits = bits
+        self.is_int = is_int
+
+    def size(self):
+        return len(self.ts)
+
+    __len__ = size
+
+    def timestamp(self, i):
+        return int(self.ts[i])
+
+    def values(self):
+        """Values as float64 (longs converted)."""
+        out = self.bits.view(np.float64).copy()
+        ints = self.is_int.astype(bool)
+        out[ints] = self.bits[ints].astype(np.float64)
+        return out
+
+    def iterator(self):
+        return SeekableView(self)
+
+    def __iter__(self):
+        it = self.iterator()
+        while it.hasNext():
+            yield it.next()
+
+
+class SeekableView:
+    """hasNext/next/seek over a DataPoints (SeekableView.java:37-71)."""
+
+    def __init__(self, dps):
+        self.dps = dps
+        self.i = 0
+
+    def hasNext(self):
+        return self.i < len(self.dps.ts)
+
+    def next(self):
+        if not self.hasNext():
+            raise NoSuchElementException("no more elements")
+        i = self.i
+        self.i += 1
+        return DataPoint(self.dps.ts[i], self.dps.bits[i], self.dps.is_int[i])
+
+    def seek(self, timestamp):
+        self.i = int(np.searchsorted(self.dps.ts, timestamp, side="left"))
+
+
+class Engine:
+    """One context per GPU (one process per GPU)."""
+
+    def __init__(self, device=0):
+        self.lib = abi.load()
+        self.ctx = C.c_void_p()
+        self._check(self.lib.otsdb_ctx_create(int(device), C.byref(self.ctx)))
+        self.device = device
+
+    def close(self):
+        if self.ctx:
+            self.lib.otsdb_ctx_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st):
+        if st != 0:
+            raise_for_status(st, self.lib.otsdb_last_error().decode())
+
+    def plan(self, spec, batch):
+        sz = abi.Sizes()
+        self._check(self.lib.otsdb_agg_plan(self.ctx, C.byref(spec),
+                                            C.byref(batch.as_abi()),
+                                            C.byref(sz)))
+        return sz
+
+    def run(self, spec, batch):
+        """Host-array path (what a JNI shim calls).  Returns one DataPoints
+        per group, in group order."""
+        sz = self.plan(spec, batch)
+        cap = max(1, int(sz.max_out_points))
+        G = batch.n_groups
+        offs = np.zeros(G + 1, np.int64)
+        ts = np.zeros(cap, np.int64)
+        bits = np.zeros(cap, np.int64)
+        isint = np.zeros(cap, np.uint8)
+        r = abi.Result(cap, offs.ctypes.data, ts.ctypes.data,
+                       bits.ctypes.data, isint.ctypes.data)
+        b = batch.as_abi()
+        self._check(self.lib.otsdb_agg_run(self.ctx, C.byref(spec), C.byref(b),
+                                           C.byref(r)))
+        return [DataPoints(ts[offs[g]:offs[g + 1]], bits[offs[g]:offs[g + 1]],
+                           isint[offs[g]:offs[g + 1]]) for g in range(G)]
+
+
+class DeviceBatch:
+    """A batch whose arrays are torch tensors resident in HBM (the bench and
+    multi-GPU path).  Tensors are kept alive by this object."""
+
+    def __init__(self, offsets, ts, val, group_offsets, group_members,
+                 is_float=None, series_float=None):
+        self.offsets, self.ts, self.val = offsets, ts, val
+        self.group_offsets, self.group_members = group_offsets, group_members
+        self.is_float, self.series_float = is_float, series_float
+
+    @property
+    def n_series(self):
+        return self.offsets.numel() - 1
+
+    @property
+    def n_groups(self):
+        return self.group_offsets.numel() - 1
+
+    def as_abi(self):
+        def p(t):
+            return None if t is None else t.data_ptr()
+        b = abi.Batch()
+        b.n_series = self.n_series
+        b.n_points = self.ts.numel()
+        b.offsets = p(self.offsets)
+        b.ts_ms = p(self.ts)
+        b.val = p(self.val)
+        b.is_float = p(self.is_float)
+        b.series_float = p(self.series_float)
+        b.n_groups = self.n_groups
+        b.group_offsets = p(self.group_offsets)
+        b.group_members = p(self.group_members)
+        return b
+
+
+class DeviceResult:
+    def __init__(self, torch, G, cap, device):
+        self.offsets = torch.zeros(G + 1, dtype=torch.int64, device=device)
+        self.ts = torch.empty(max(cap, 1), dtype=torch.int64, device=device)
+        self.val = torch.empty(max(cap, 1), dtype=torch.int64, device=device)
+        self.is_int = torch.empty(max(cap, 1), dtype=torch.uint8, device=device)
+        self.cap = cap
+
+    def as_abi(self):
+        return abi.Result(self.cap, self.offsets.data_ptr(), self.ts.data_ptr(),
+                          self.val.data_ptr(), self.is_int.data_ptr())
+
+
+def run_device(engine, spec, dbatch, dresult, stream=None):
+    """Device-resident path: no host copies of points in or out."""
+    b = dbatch.as_abi()
+    r = dresult.as_abi()
+    engine._check(engine.lib.otsdb_agg_run_device(
+        engine.ctx, C.byref(spec), C.byref(b), C.byref(r),
+        None if stream is None else C.c_void_p(stream)))

@@ -1,0 +1,127 @@
+"""BASELINE.json workloads and their synthetic data.
+
+Series s of the synthetic dataset has tags host = s // 10, cpu = s % 10,
+dc = host % 16; series are numbered in SpanCmp order (host, cpu UIDs are
+assigned in that order).  The per-series generator (seed 42, T0 =
+1356998400 s, 10 s cadence, 2 % dropped points, 0-2 outages of 1-6 h, 5 %
+late-start/early-end series) runs on the GPU through the C-ABI
+(otsdb_gen_*_device) and is restated bit for bit by the oracle
+(or_gen_fill) for parity tests.
+"""
+import numpy as np
+
+from . import abi, core
+
+T0_S = 1356998400
+DAY_MS = 86400 * 1000
+
+# name -> (n_series, days, value kind, query) ; query = (agg, ds, rate opts,
+# group-by tag)
+CONFIGS = {
+    # configs[0]: CPU reference
+    "C1": dict(n_series=1000, days=1, kind=0, agg="sum", ds="1m-avg",
+               rate=None, group="host"),
+    # configs[1]: the single-GPU bench workload
+    "C2": dict(n_series=100000, days=7, kind=0, agg="zimsum", ds="5m-avg",
+               rate=None, group="host"),
+    # configs[2]: 8 GPU, LERP, cross-rank partial all-reduce
+    "C3": dict(n_series=1000000, days=1, kind=0, agg="avg", ds="1h-max",
+               rate=None, group="dc"),
+    # configs[3]: counters
+    "C4": dict(n_series=500000, days=1, kind=2, agg="dev", ds="1m-sum",
+               rate=(True, 2**63 - 1, 1000000), group=None),
+    # configs[4]: percentiles with fill=nan
+    "C5": dict(n_series=1000000, days=1, kind=0, agg="p99", ds="1m-avg-nan",
+               rate=None, group=None),
+}
+
+
+def gen_spec(name):
+    c = CONFIGS[name]
+    return abi.GenSpec(42, T0_S * 1000, c["days"] * DAY_MS, 10000, c["kind"],
+                       0)
+
+
+def group_of(name, s):
+    g = CONFIGS[name]["group"]
+    if g == "host":
+        return s // 10
+    if g == "dc":
+        return (s // 10) % 16
+    return 0
+
+
+def group_ids(name, series0, n):
+    s = np.arange(series0, series0 + n, dtype=np.int64)
+    g = CONFIGS[name]["group"]
+    if g == "host":
+        return s // 10
+    if g == "dc":
+        return (s // 10) % 16
+    return np.zeros(n, np.int64)
+
+
+def query_spec(name, series0=0):
+    """The TsdbQuery a user would send: [T0, T0 + days - 1 s]; the SpanGroup
+    window comes from getScanStart/EndTimeSeconds (TsdbQuery.java:1573-1675)
+    normalised to ms (SpanGroup.java:267-270)."""
+    c = CONFIGS[name]
+    ds = core.DownsamplingSpecification(c["ds"])
+    q_start = T0_S
+    q_end = T0_S + c["days"] * 86400 - 1
+    start_s = core.get_scan_start_time_seconds(q_start, ds)
+    end_s = core.get_scan_end_time_seconds(q_end, ds)
+    ro = core.RateOptions(*c["rate"]) if c["rate"] else None
+    return core.make_spec(start_s, end_s, core.Aggregators.get(c["agg"]), ds,
+                          q_start * 1000, q_end * 1000, c["rate"] is not None,
+                          ro, normalize=True)
+
+
+def local_groups(name, series0, n):
+    """Group CSR for series [series0, series0+n) with group ids made dense
+    and kept in ByteMap (= numeric) order; returns (g_off, members,
+    global_group_ids)."""
+    gid = group_ids(name, series0, n)
+    uniq, dense = np.unique(gid, return_inverse=True)
+    order = np.argsort(dense, kind="stable").astype(np.int64)
+    counts = np.bincount(dense, minlength=len(uniq))
+    g_off = np.zeros(len(uniq) + 1, np.int64)
+    np.cumsum(counts, out=g_off[1:])
+    return g_off, order, uniq
+
+
+def generate_device(engine, gspec, series0, n_series, group_size=None,
+                    config=None, device="cuda"):
+    """Generates series [series0, series0+n) straight into HBM and returns a
+    DeviceBatch (torch tensors)."""
+    import ctypes as C
+    import torch
+    from .engine import DeviceBatch
+    counts = torch.zeros(n_series, dtype=torch.int64, device=device)
+    engine._check(engine.lib.otsdb_gen_counts_device(
+        engine.ctx, C.byref(gspec), series0, n_series, counts.data_ptr(),
+        None))
+    offsets = torch.zeros(n_series + 1, dtype=torch.int64, device=device)
+    torch.cumsum(counts, 0, out=offsets[1:])
+    N = int(offsets[-1].item())
+    ts = torch.empty(max(N, 2), dtype=torch.int64, device=device)
+    val = torch.empty(max(N, 2), dtype=torch.int64, device=device)
+    engine._check(engine.lib.otsdb_gen_fill_device(
+        engine.ctx, C.byref(gspec), series0, n_series, offsets.data_ptr(),
+        ts.data_ptr(), val.data_ptr(), None))
+    torch.cuda.synchronize()
+    if config is not None:
+        g_off, members, _ = local_groups(config, series0, n_series)
+    else:
+        gs = group_size or n_series
+        gid = (np.arange(series0, series0 + n_series) // gs)
+        gid = gid - gid[0] if n_series else gid
+        from .batch import groups_from_ids
+        g_off, members = groups_from_ids(gid)
+    sf = torch.full((n_series,), 1 if gspec.kind == 0 else 0,
+                    dtype=torch.uint8, device=device)
+    db = DeviceBatch(offsets, ts[:N] if N else ts[:0], val[:N] if N else val[:0],
+                     torch.from_numpy(g_off).to(device),
+                     torch.from_numpy(members).to(device), None, sf)
+    db.n_points_total = N
+    return db

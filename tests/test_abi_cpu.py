@@ -1,0 +1,105 @@
+"""CPU-side checks of the boundary and of the host mirror: the C-ABI library
+loads and exports every entry point include/otsdb_agg.h declares, the
+registry matches the reference's, spec parsing follows the reference."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from opentsdb_amd import abi, core
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    with open(os.path.join(ROOT, "include", "otsdb_agg.h")) as f:
+        src = f.read()
+    # function declarations: return type, name, '('
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(otsdb_[a-z_0-9]+)\(",
+                       src, re.M)
+    return sorted(set(names))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from opentsdb_amd import build
+    build.build()
+    return abi.load()
+
+
+def test_library_exports_every_declared_symbol(lib):
+    syms = header_symbols()
+    assert len(syms) >= 14, syms
+    assert sorted(syms) == sorted(abi.EXPORTS)
+    for s in syms:
+        assert hasattr(lib, s), "missing export " + s
+
+
+def test_abi_version(lib):
+    assert lib.otsdb_abi_version() == 1
+
+
+def test_struct_sizes_match_header():
+    assert C.sizeof(abi.QuerySpec) == 4 * 8 + 4 * 2 + 8 + 4 * 8 + 8 * 2
+    assert C.sizeof(abi.Batch) == 10 * 8
+    assert C.sizeof(abi.Result) == 5 * 8
+    assert C.sizeof(abi.Partial) == 32
+
+
+def test_registry_matches_reference(lib):
+    """Aggregators.get / toString / interpolationMethod
+    (Aggregators.java:47-203) through the C-ABI and the Python mirror."""
+    for key in core.Aggregators.set():
+        a = core.Aggregators.get(key)
+        out = C.c_int32(-1)
+        assert lib.otsdb_agg_lookup(key.encode(), C.byref(out)) == 0
+        assert out.value == a.id
+        assert lib.otsdb_agg_name(a.id).decode() == a.name
+        assert lib.otsdb_agg_interpolation(a.id) == int(a.interpolationMethod())
+    assert lib.otsdb_agg_lookup(b"nosuch", C.byref(C.c_int32())) == 4
+    assert len(core.Aggregators.set()) == 35
+    assert str(core.Aggregators.get("none")) == "raw"
+    assert str(core.Aggregators.get("mult")) == "multiply"
+    with pytest.raises(core.NoSuchElementException):
+        core.Aggregators.get("Sum")  # case sensitive
+
+
+def test_parse_duration():
+    """DateTime.parseDuration (DateTime.java:187-231)."""
+    P = core.DateTime.parseDuration
+    assert P("1s") == 1000
+    assert P("1m") == 60000
+    assert P("1h") == 3600000
+    assert P("1d") == 86400000
+    assert P("1w") == 604800000
+    assert P("1n") == 2592000000
+    assert P("1y") == 31536000000
+    assert P("500ms") == 500
+    for bad in ("", "1", "s", "0s", "-1s", "1x"):
+        with pytest.raises(core.IllegalArgumentException):
+            P(bad)
+
+
+def test_downsampling_specification():
+    """DownsamplingSpecification(String) (DownsamplingSpecification.java:116-191)."""
+    d = core.DownsamplingSpecification("1m-avg")
+    assert d.getInterval() == 60000 and d.getFunction().name == "avg"
+    assert d.getFillPolicy() == core.FillPolicy.NONE and not d.useCalendar()
+    d = core.DownsamplingSpecification("10s-sum-NaN")
+    assert d.getFillPolicy() == core.FillPolicy.NOT_A_NUMBER
+    d = core.DownsamplingSpecification("1h-max-zero")
+    assert d.getFillPolicy() == core.FillPolicy.ZERO
+    d = core.DownsamplingSpecification("1dc-sum")
+    assert d.useCalendar() and d.getInterval() == 86400000
+    d = core.DownsamplingSpecification("0all-sum")
+    assert d.run_all and d.getInterval() == 0
+    for bad in ("1m", "1m-avg-nan-x", "1m-nosuch", "1m-none", "1m-avg-bogus"):
+        with pytest.raises(core.IllegalArgumentException):
+            core.DownsamplingSpecification(bad)
+
+
+def test_rate_options_defaults():
+    r = core.RateOptions()
+    assert not r.isCounter() and r.getCounterMax() == 2**63 - 1
+    assert r.getResetValue() == 0 and not r.getDropResets()

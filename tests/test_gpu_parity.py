@@ -1,0 +1,283 @@
+"""Parity of the HIP engine (through the C-ABI) with the CPU oracle and with
+the reference's transcribed known answers.  Needs an MI355X.
+
+Bar (north star): timestamps, emission, counts, min/max/first/last and
+anything computed from order-insensitive inputs are bit-exact; double
+sum/avg/dev/mult/squareSum within 1e-12 relative where the reduction order
+differs (downsample buckets are reduced in a wavefront tree; cross-series
+reduction keeps the reference's order inside each 256-series chunk).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from opentsdb_amd import core
+from opentsdb_amd.engine import Engine
+from oracle import pyoracle
+from tests import datasets, kat
+
+pytestmark = pytest.mark.gpu
+
+ORDER_FREE = {"min", "max", "mimmin", "mimmax", "first", "last", "count",
+              "diff"}
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from opentsdb_amd import build
+    build.build()
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def _vals(bits, is_int):
+    b = np.asarray(bits, np.int64)
+    f = b.view(np.float64).copy()
+    ii = np.asarray(is_int).astype(bool)
+    f[ii] = b[ii].astype(np.float64)
+    return f
+
+
+def compare(got, ref, exact, scale=1.0, where=""):
+    assert len(got) == len(ref), "%s: %d groups vs %d" % (where, len(got), len(ref))
+    for g, (a, r) in enumerate(zip(got, ref)):
+        w = "%s/g%d" % (where, g)
+        assert len(a.ts) == len(r), "%s: %d points vs oracle %d" % (w, len(a.ts), len(r))
+        if len(r) == 0:
+            continue
+        assert np.array_equal(np.asarray(a.ts), r["ts"]), w + ": timestamps"
+        assert np.array_equal(np.asarray(a.is_int).astype(bool),
+                              r["is_int"].astype(bool)), w + ": is_int"
+        va, vr = _vals(a.bits, a.is_int), _vals(r["bits"], r["is_int"])
+        na, nr = np.isnan(va), np.isnan(vr)
+        assert np.array_equal(na, nr), w + ": NaN pattern %s vs %s" % (
+            va[na != nr][:4], vr[na != nr][:4])
+        if exact:
+            bad = (np.asarray(a.bits) != r["bits"]) & ~na
+            assert not bad.any(), "%s: not bit-exact at %s: %r vs %r" % (
+                w, np.nonzero(bad)[0][:5], va[bad][:5], vr[bad][:5])
+        else:
+            d = np.abs(va - vr)[~na]
+            tol = 1e-12 * np.maximum(np.maximum(np.abs(va), np.abs(vr)), scale)[~na]
+            assert (d <= tol).all(), "%s: max rel err %g" % (
+                w, (d / tol * 1e-12).max())
+
+
+def run_both(engine, spec, batch):
+    try:
+        ref = pyoracle.group_by(spec, batch)
+        ref_err = None
+    except pyoracle.OracleError as e:
+        ref, ref_err = None, e.status
+    try:
+        got = engine.run(spec, batch)
+        got_err = None
+    except core.OpenTSDBException as e:
+        got, got_err = None, e.status
+    assert got_err == ref_err, "engine status %s vs oracle %s" % (got_err, ref_err)
+    return got, ref
+
+
+# ------------------------------------------------------------------ KATs
+@pytest.mark.parametrize("c", kat.load_cases("group_by"), ids=lambda c: c["name"])
+def test_reference_kat(engine, c):
+    spec = kat.spec_from_case(c["spec"])
+    batch = kat.batch_from_case(c)
+    if not c["spec"].get("ds_interval_ms"):
+        with pytest.raises(core.UnsupportedOperationException):
+            engine.run(spec, batch)
+        pytest.skip("raw group-by not offloaded yet (SURVEY §8f rank 2)")
+    got = engine.run(spec, batch)
+    for g, exp in enumerate(c["expect"]):
+        pts = np.zeros(len(got[g].ts), pyoracle.POINT)
+        pts["ts"], pts["bits"], pts["is_int"] = got[g].ts, got[g].bits, got[g].is_int
+        kat.check_points(pts, exp, c["tol"], "%s/g%d" % (c["name"], g))
+
+
+# ------------------------------------------------------- parity matrix
+def _spec(agg, ds, fill="none", start=None, end=None, rate=False, ro=None,
+          interp=None, interval="1m"):
+    d = core.DownsamplingSpecification("%s-%s-%s" % (interval, ds, fill))
+    s0 = datasets.T0 if start is None else start
+    e0 = datasets.T0 + 3 * 3600 * 1000 if end is None else end
+    return core.make_spec(s0, e0, core.Aggregators.get(agg), d, s0, e0, rate,
+                          ro, interp)
+
+
+AGGS = ["sum", "zimsum", "pfsum", "avg", "min", "max", "mimmin", "mimmax",
+        "dev", "count", "first", "last", "diff", "mult", "squareSum",
+        "median", "p50", "p90", "p99", "p999", "ep95r3", "ep75r7"]
+DS = ["avg", "sum", "min", "max", "count", "first", "last", "dev", "diff",
+      "mult", "squareSum", "zimsum", "mimmax"]
+
+
+@pytest.mark.parametrize("agg", AGGS)
+def test_cross_series_aggregators(engine, agg):
+    b = datasets.random_batch(11, n_series=60, n_groups=6)
+    for ds in ("avg", "max"):
+        spec = _spec(agg, ds)
+        got, ref = run_both(engine, spec, b)
+        compare(got, ref, ds == "max", scale=100.0, where="%s:%s" % (agg, ds))
+
+
+@pytest.mark.parametrize("ds", DS)
+def test_downsample_functions(engine, ds):
+    for kind in ("float", "int", "mixed"):
+        b = datasets.random_batch(23, n_series=30, n_groups=3, value_kind=kind,
+                                  nan_frac=0.05 if kind == "float" else 0)
+        for agg in ("sum", "min"):
+            spec = _spec(agg, ds, interval="5m")
+            got, ref = run_both(engine, spec, b)
+            exact = ds in ORDER_FREE or (kind == "int" and ds not in (
+                "dev", "mult"))
+            compare(got, ref, exact, scale=1e4, where="%s/%s/%s" % (ds, agg, kind))
+
+
+@pytest.mark.parametrize("fill", ["none", "nan", "zero", "null"])
+@pytest.mark.parametrize("aligned", [True, False])
+def test_fill_policies_and_window(engine, fill, aligned):
+    b = datasets.random_batch(31, n_series=25, n_groups=4, nan_frac=0.02)
+    start = datasets.T0 + (0 if aligned else 37000)
+    end = datasets.T0 + 2 * 3600 * 1000 + (0 if aligned else 11000)
+    for agg in ("sum", "avg", "count", "last", "mimmin"):
+        spec = _spec(agg, "max", fill, start, end)
+        got, ref = run_both(engine, spec, b)
+        compare(got, ref, True, where="%s/%s/%s" % (fill, agg, aligned))
+
+
+@pytest.mark.parametrize("interp", list(core.Interpolation))
+def test_interpolation_methods(engine, interp):
+    b = datasets.random_batch(41, n_series=30, n_groups=3)
+    for agg in ("sum", "max", "first"):
+        spec = _spec(agg, "min", interp=interp, interval="10s")
+        got, ref = run_both(engine, spec, b)
+        compare(got, ref, True, where="%s/%s" % (interp.name, agg))
+
+
+RATES = [
+    core.RateOptions(),
+    core.RateOptions(True, 2**63 - 1, 0),
+    core.RateOptions(True, 2**63 - 1, 50),
+    core.RateOptions(True, 10**12, 0, True),
+]
+
+
+@pytest.mark.parametrize("ri", range(len(RATES)))
+@pytest.mark.parametrize("fill", ["none", "nan", "zero"])
+def test_rate(engine, ri, fill):
+    b = datasets.random_batch(51 + ri, n_series=30, n_groups=3, counter=True)
+    for agg, ds in (("sum", "max"), ("dev", "sum"), ("avg", "last"),
+                    ("count", "min")):
+        for aligned in (True, False):
+            start = datasets.T0 + (0 if aligned else 61000)
+            spec = _spec(agg, ds, fill, start=start, rate=True, ro=RATES[ri])
+            got, ref = run_both(engine, spec, b)
+            exact = agg != "dev"
+            compare(got, ref, exact, scale=1.0,
+                    where="rate%d/%s/%s/%s" % (ri, fill, agg, aligned))
+
+
+def test_run_all(engine):
+    b = datasets.random_batch(61, n_series=20, n_groups=4)
+    qs, qe = datasets.T0 + 600000, datasets.T0 + 7200000
+    for agg in ("sum", "max", "count"):
+        d = core.DownsamplingSpecification("0all-max")
+        spec = core.make_spec(datasets.T0, datasets.T0 + 4 * 3600 * 1000,
+                              core.Aggregators.get(agg), d, qs, qe)
+        got, ref = run_both(engine, spec, b)
+        compare(got, ref, True, where="all/" + agg)
+
+
+def test_big_groups_chunked(engine):
+    """Groups larger than one 256-series chunk: chunk partials merged in
+    order (exact for order-free aggregators, 1e-12 otherwise)."""
+    b = datasets.random_batch(71, n_series=700, big_group=True,
+                              span_ms=3600 * 1000, cadence_ms=30000)
+    for agg in ("sum", "avg", "dev", "min", "count", "first", "last", "diff"):
+        spec = _spec(agg, "max", end=datasets.T0 + 3600 * 1000)
+        got, ref = run_both(engine, spec, b)
+        compare(got, ref, agg in ORDER_FREE, scale=100.0, where="big/" + agg)
+
+
+def test_got_infinity(engine):
+    """AggregationIterator.doubleValue throws on +-Infinity
+    (AggregationIterator.java:640-643)."""
+    from opentsdb_amd.batch import HostBatch
+    big = 1.5e308
+    groups = [[[(datasets.T0 + 1000 * i, big, 1) for i in range(5)]] * 3]
+    b = HostBatch.from_groups(groups)
+    spec = _spec("sum", "max", end=datasets.T0 + 60000)
+    run_both(engine, spec, b)
+    with pytest.raises(core.IllegalStateException):
+        engine.run(spec, b)
+
+
+def test_none_more_than_one_value(engine):
+    """`none` fed by more than one span -> IllegalDataException
+    (Aggregators.java:446-449)."""
+    b = datasets.random_batch(81, n_series=6, n_groups=2, outside=False,
+                              empty_frac=0)
+    spec = _spec("none", "avg")
+    run_both(engine, spec, b)
+    with pytest.raises(core.IllegalDataException):
+        engine.run(spec, b)
+
+
+def test_empty_and_degenerate(engine):
+    from opentsdb_amd.batch import HostBatch
+    # no series at all / empty spans only / window before all data
+    b = HostBatch.from_groups([[[], []], []])
+    got, ref = run_both(engine, _spec("sum", "avg"), b)
+    compare(got, ref, True, where="empty")
+    b = datasets.random_batch(91, n_series=10, n_groups=2)
+    spec = _spec("sum", "avg", start=datasets.T0 - 10 * 3600 * 1000,
+                 end=datasets.T0 - 9 * 3600 * 1000)
+    got, ref = run_both(engine, spec, b)
+    compare(got, ref, True, where="before")
+
+
+# ------------------------------------------------------------ generator
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_device_generator_matches_oracle(engine, kind):
+    import torch
+    from opentsdb_amd import abi, workload
+    g = abi.GenSpec(42, 1356998400000, 86400000, 10000, kind, 0)
+    db = workload.generate_device(engine, g, series0=1000, n_series=64,
+                                  group_size=10)
+    offs = db.offsets.cpu().numpy()
+    ts = db.ts.cpu().numpy()
+    val = db.val.cpu().numpy()
+    for i in range(64):
+        t, v = pyoracle.gen_series(g, 1000 + i)
+        assert np.array_equal(ts[offs[i]:offs[i + 1]], t), i
+        assert np.array_equal(val[offs[i]:offs[i + 1]], v), i
+
+
+def test_device_path_matches_host_path(engine):
+    """otsdb_agg_run_device on HBM-resident tensors == otsdb_agg_run."""
+    import torch
+    from opentsdb_amd import abi, workload
+    from opentsdb_amd.engine import DeviceResult, run_device
+    g = abi.GenSpec(42, 1356998400000, 86400000, 10000, 0, 0)
+    db = workload.generate_device(engine, g, series0=0, n_series=200,
+                                  group_size=10)
+    spec = workload.query_spec("C1", 0)
+    sz = engine.plan(spec, db)
+    res = DeviceResult(torch, db.n_groups, int(sz.max_out_points), "cuda")
+    run_device(engine, spec, db, res)
+    torch.cuda.synchronize()
+    hb = pyoracle.gen_batch(g, 0, 200, lambda s: s // 10)
+    ref = pyoracle.group_by(spec, hb)
+    host = engine.run(spec, hb)
+    offs = res.offsets.cpu().numpy()
+    from opentsdb_amd.engine import DataPoints
+    got = [DataPoints(res.ts[offs[i]:offs[i + 1]].cpu().numpy(),
+                      res.val[offs[i]:offs[i + 1]].cpu().numpy(),
+                      res.is_int[offs[i]:offs[i + 1]].cpu().numpy())
+           for i in range(db.n_groups)]
+    compare(got, ref, False, scale=100.0, where="device")
+    compare(host, ref, False, scale=100.0, where="host")
+    for a, h in zip(got, host):
+        assert np.array_equal(a.bits, h.bits)
