@@ -114,6 +114,13 @@ def load(path=None):
         raise RuntimeError(
             "libotsdb_agg.so not built (%s): run __graft_entry__.build(); the "
             "aggregation path has no CPU fallback" % p)
+    try:
+        # torch ships its own HIP runtime under the same SONAME; loading it
+        # first makes libotsdb_agg.so bind to that one copy instead of
+        # starting a second runtime in the process.
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(p)
     vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int32
     lib.otsdb_abi_version.restype = C.c_int

@@ -589,6 +589,9 @@ otsdb_status run_device_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
   Params P;
   rc = make_params(spec, &P);
   if (rc) return rc;
+  if ((((uintptr_t)b->ts_ms) | ((uintptr_t)b->val)) & 15)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT,
+                "ts_ms/val must be 16-byte aligned (16-B streaming loads)");
   BatchDev B{b->n_series, b->offsets, b->ts_ms, b->val, b->is_float,
              b->series_float};
   Work W;

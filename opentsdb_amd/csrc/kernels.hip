@@ -154,7 +154,16 @@ __global__ __launch_bounds__(256) void k_bucketize(Params P, BatchDev B,
     const int kB = inB ? (int)bucket_of(P, ctb) : (ib < lo ? -1 : INT32_MAX);
     M sA = inA ? M::from(point_value(B, ia, cva, sf)) : M::init();
     const M sB = inB ? M::from(point_value(B, ib, cvb, sf)) : M::init();
-    if (lane == 0 && carry_key == kA) sA = M::combine(carry, sA);
+    if (lane == 0) {
+      if (carry_key == kA) {
+        sA = M::combine(carry, sA);
+      } else if (carry_key >= 0 && carry_key < P.nb) {
+        // the bucket carried from the previous step closed on its boundary
+        int err = 0;
+        rowv[carry_key] = carry.finish(&err);
+        rows[carry_key] = ST_REAL;
+      }
+    }
     // inclusive segmented scan keyed by each lane's last bucket
     int key = kB;
     M st = (kA == kB) ? M::combine(sA, sB) : sB;

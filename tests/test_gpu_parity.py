@@ -80,6 +80,14 @@ def run_both(engine, spec, batch):
     return got, ref
 
 
+def check(engine, spec, batch, exact, scale=1.0, where=""):
+    """run_both + compare; a query both sides reject is parity too."""
+    got, ref = run_both(engine, spec, batch)
+    if ref is not None:
+        compare(got, ref, exact, scale, where)
+    return got, ref
+
+
 # ------------------------------------------------------------------ KATs
 @pytest.mark.parametrize("c", kat.load_cases("group_by"), ids=lambda c: c["name"])
 def test_reference_kat(engine, c):
@@ -118,8 +126,7 @@ def test_cross_series_aggregators(engine, agg):
     b = datasets.random_batch(11, n_series=60, n_groups=6)
     for ds in ("avg", "max"):
         spec = _spec(agg, ds)
-        got, ref = run_both(engine, spec, b)
-        compare(got, ref, ds == "max", scale=100.0, where="%s:%s" % (agg, ds))
+        check(engine, spec, b, ds == "max", scale=100.0, where="%s:%s" % (agg, ds))
 
 
 @pytest.mark.parametrize("ds", DS)
@@ -129,10 +136,10 @@ def test_downsample_functions(engine, ds):
                                   nan_frac=0.05 if kind == "float" else 0)
         for agg in ("sum", "min"):
             spec = _spec(agg, ds, interval="5m")
-            got, ref = run_both(engine, spec, b)
             exact = ds in ORDER_FREE or (kind == "int" and ds not in (
                 "dev", "mult"))
-            compare(got, ref, exact, scale=1e4, where="%s/%s/%s" % (ds, agg, kind))
+            check(engine, spec, b, exact, scale=1e4,
+                  where="%s/%s/%s" % (ds, agg, kind))
 
 
 @pytest.mark.parametrize("fill", ["none", "nan", "zero", "null"])
@@ -143,8 +150,7 @@ def test_fill_policies_and_window(engine, fill, aligned):
     end = datasets.T0 + 2 * 3600 * 1000 + (0 if aligned else 11000)
     for agg in ("sum", "avg", "count", "last", "mimmin"):
         spec = _spec(agg, "max", fill, start, end)
-        got, ref = run_both(engine, spec, b)
-        compare(got, ref, True, where="%s/%s/%s" % (fill, agg, aligned))
+        check(engine, spec, b, True, where="%s/%s/%s" % (fill, agg, aligned))
 
 
 @pytest.mark.parametrize("interp", list(core.Interpolation))
@@ -152,8 +158,7 @@ def test_interpolation_methods(engine, interp):
     b = datasets.random_batch(41, n_series=30, n_groups=3)
     for agg in ("sum", "max", "first"):
         spec = _spec(agg, "min", interp=interp, interval="10s")
-        got, ref = run_both(engine, spec, b)
-        compare(got, ref, True, where="%s/%s" % (interp.name, agg))
+        check(engine, spec, b, True, where="%s/%s" % (interp.name, agg))
 
 
 RATES = [
@@ -173,10 +178,9 @@ def test_rate(engine, ri, fill):
         for aligned in (True, False):
             start = datasets.T0 + (0 if aligned else 61000)
             spec = _spec(agg, ds, fill, start=start, rate=True, ro=RATES[ri])
-            got, ref = run_both(engine, spec, b)
             exact = agg != "dev"
-            compare(got, ref, exact, scale=1.0,
-                    where="rate%d/%s/%s/%s" % (ri, fill, agg, aligned))
+            check(engine, spec, b, exact, scale=1.0,
+                  where="rate%d/%s/%s/%s" % (ri, fill, agg, aligned))
 
 
 def test_run_all(engine):
@@ -186,8 +190,7 @@ def test_run_all(engine):
         d = core.DownsamplingSpecification("0all-max")
         spec = core.make_spec(datasets.T0, datasets.T0 + 4 * 3600 * 1000,
                               core.Aggregators.get(agg), d, qs, qe)
-        got, ref = run_both(engine, spec, b)
-        compare(got, ref, True, where="all/" + agg)
+        check(engine, spec, b, True, where="all/" + agg)
 
 
 def test_big_groups_chunked(engine):
@@ -197,8 +200,7 @@ def test_big_groups_chunked(engine):
                               span_ms=3600 * 1000, cadence_ms=30000)
     for agg in ("sum", "avg", "dev", "min", "count", "first", "last", "diff"):
         spec = _spec(agg, "max", end=datasets.T0 + 3600 * 1000)
-        got, ref = run_both(engine, spec, b)
-        compare(got, ref, agg in ORDER_FREE, scale=100.0, where="big/" + agg)
+        check(engine, spec, b, agg in ORDER_FREE, scale=100.0, where="big/" + agg)
 
 
 def test_got_infinity(engine):
@@ -234,8 +236,7 @@ def test_empty_and_degenerate(engine):
     b = datasets.random_batch(91, n_series=10, n_groups=2)
     spec = _spec("sum", "avg", start=datasets.T0 - 10 * 3600 * 1000,
                  end=datasets.T0 - 9 * 3600 * 1000)
-    got, ref = run_both(engine, spec, b)
-    compare(got, ref, True, where="before")
+    check(engine, spec, b, True, where="before")
 
 
 # ------------------------------------------------------------ generator
