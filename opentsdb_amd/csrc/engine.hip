@@ -144,6 +144,7 @@ struct otsdb_ctx {
   size_t ev_used = 0;
   double prof_ms[8] = {0};
   int64_t prof_n[8] = {0};
+  int bucketize_k = 8;  // points per lane in k_bucketize (OTSDB_BUCKETIZE_K)
 };
 
 namespace {
@@ -457,8 +458,20 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
                            st, P, B, W.SM);
       }
       StageTimer tm(c, 0);
-      hipLaunchKernelGGL(k_bucketize<M>, dim3(blocks_for(S, 4)), dim3(256), 0,
-                         st, P, B, W.SM, W.R);
+      const dim3 grid(blocks_for(S, 4)), blk(256);
+      switch (c->bucketize_k) {
+        case 2:
+          hipLaunchKernelGGL(k_bucketize<M>, grid, blk, 0, st, P, B, W.SM,
+                             W.R);
+          break;
+        case 4:
+          hipLaunchKernelGGL((k_bucketize_k<M, 4>), grid, blk, 0, st, P, B,
+                             W.SM, W.R);
+          break;
+        default:
+          hipLaunchKernelGGL((k_bucketize_k<M, 8>), grid, blk, 0, st, P, B,
+                             W.SM, W.R);
+      }
     });
     if (!ok) return fail(OTSDB_E_UNSUPPORTED, "downsampler %d", spec->ds_agg_id);
     StageTimer tm(c, 1);
@@ -625,6 +638,7 @@ otsdb_status otsdb_ctx_create(int device, otsdb_ctx** out) {
   HIP_TRY(hipSetDevice(device));
   otsdb_ctx* c = new otsdb_ctx();
   c->device = device;
+  if (const char* k = getenv("OTSDB_BUCKETIZE_K")) c->bucketize_k = atoi(k);
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIP_TRY(hipMalloc(&c->d_err, 256));
   c->d_mm = (unsigned long long*)((char*)c->d_err + 64);

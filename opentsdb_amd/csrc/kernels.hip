@@ -208,6 +208,136 @@ __global__ __launch_bounds__(256) void k_bucketize(Params P, BatchDev B,
 }
 
 // ------------------------------------------------------------------------
+// k_bucketize_k: the same reduction with K consecutive points per lane
+// (K/2 16-byte loads per column per lane; a step covers 64*K points).  Each
+// lane folds its points sequentially (Java order inside the lane), closes
+// the buckets that start and end inside it, and hands its first ("head")
+// and last ("tail") runs to a segmented wave scan over the tails — so the
+// cross-lane scan is paid once per 64*K points instead of once per 128.
+// ------------------------------------------------------------------------
+template <class M, int K>
+__global__ __launch_bounds__(256) void k_bucketize_k(Params P, BatchDev B,
+                                                     SeriesMeta SM, Rows R) {
+  static_assert(K % 2 == 0, "K must be even (16-byte loads)");
+  const int lane = LANE;
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= B.S) return;
+  if (!SM.keep[s]) return;
+  const int64_t lo = SM.lo[s], hi = SM.hi[s];
+  if (lo >= hi) return;
+  const int sf = B.series_float ? (int)B.series_float[s] : 1;
+  double* rowv = R.val + s * P.nb;
+  uint8_t* rows = R.state + s * P.nb;
+  int err = 0;
+
+  int carry_key = INT32_MIN;
+  M carry = M::init();
+  constexpr int PTS = 64 * K;
+  for (int64_t base = lo & ~(int64_t)1; base < hi; base += PTS) {
+    const int64_t i0 = base + (int64_t)K * lane;
+    int64_t t[K], v[K];
+    if (i0 + K <= hi) {
+#pragma unroll
+      for (int j = 0; j < K; j += 2) {
+        const longlong2 tt = *reinterpret_cast<const longlong2*>(B.ts + i0 + j);
+        const longlong2 vv = *reinterpret_cast<const longlong2*>(B.val + i0 + j);
+        t[j] = tt.x; t[j + 1] = tt.y;
+        v[j] = vv.x; v[j + 1] = vv.y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        t[j] = (i0 + j < hi) ? B.ts[i0 + j] : 0;
+        v[j] = (i0 + j < hi) ? B.val[i0 + j] : 0;
+      }
+    }
+    // ---- lane-local sequential fold
+    int nseg = 0, cur_key = 0, head_key = 0;
+    M cur = M::init(), head = M::init();
+    int64_t bnd = INT64_MIN;  // first timestamp past cur_key's bucket
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int64_t i = i0 + j;
+      if (i < lo || i >= hi) continue;
+      int k = cur_key;
+      if (nseg == 0 || t[j] >= bnd) {
+        k = (int)bucket_of(P, t[j]);
+        bnd = P.run_all ? INT64_MAX : P.gbase + ((int64_t)k + 1) * P.interval;
+      }
+      const double x = point_value(B, i, v[j], sf);
+      if (nseg == 0) {
+        cur_key = k;
+        cur = M::from(x);
+        nseg = 1;
+      } else if (k == cur_key) {
+        cur.push(x);
+      } else {
+        if (nseg == 1) {
+          head_key = cur_key;
+          head = cur;
+        } else {  // a bucket wholly inside this lane
+          rowv[cur_key] = cur.finish(&err);
+          rows[cur_key] = ST_REAL;
+        }
+        cur_key = k;
+        cur = M::from(x);
+        ++nseg;
+      }
+    }
+    if (nseg == 0) {  // lane wholly before lo (first step) or past hi
+      cur_key = (i0 < lo) ? -1 : INT32_MAX;
+      head_key = cur_key;
+    } else if (nseg == 1) {
+      head_key = cur_key;
+    }
+    // ---- previous step's open bucket
+    if (lane == 0) {
+      if (nseg >= 1 && carry_key == head_key) {
+        if (nseg == 1) cur = M::combine(carry, cur);
+        else head = M::combine(carry, head);
+      } else if (carry_key >= 0 && carry_key < P.nb) {
+        rowv[carry_key] = carry.finish(&err);
+        rows[carry_key] = ST_REAL;
+      }
+    }
+    // ---- segmented inclusive scan over the lanes' tail runs
+    int key = cur_key;
+    M st = cur;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int k2 = __shfl_up(key, d);
+      M o = st;
+      o.shfl_up(d);
+      if (lane >= d && k2 == key) st = M::combine(o, st);
+    }
+    const int pkey = __shfl_up(key, 1);
+    M pst = st;
+    pst.shfl_up(1);
+    const int next_head = __shfl_down(head_key, 1);
+    if (nseg >= 2) {  // head run closes inside this lane
+      const M full = (lane > 0 && pkey == head_key) ? M::combine(pst, head) : head;
+      rowv[head_key] = full.finish(&err);
+      rows[head_key] = ST_REAL;
+    }
+    if (nseg >= 1 && lane < 63 && next_head != key) {
+      rowv[key] = st.finish(&err);
+      rows[key] = ST_REAL;
+    }
+    carry_key = __shfl(key, 63);
+    Packed p = st.pack();
+    p.x = __shfl(p.x, 63);
+    p.y = __shfl(p.y, 63);
+    p.z = __shfl(p.z, 63);
+    p.w = __shfl(p.w, 63);
+    carry = M::unpack(p);
+  }
+  if (lane == 0 && carry_key >= 0 && carry_key < P.nb) {
+    rowv[carry_key] = carry.finish(&err);
+    rows[carry_key] = ST_REAL;
+  }
+}
+
+// ------------------------------------------------------------------------
 // interpolation of a series between two of its points, exactly as
 // AggregationIterator.nextDoubleValue (AggregationIterator.java:772-793)
 // ------------------------------------------------------------------------

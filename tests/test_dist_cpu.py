@@ -1,0 +1,91 @@
+"""Multi-rank path on CPU (gloo, world size 2): sharding, cross-rank group
+detection and the partial exchange protocol (all-gather, rank-major layout,
+merge in rank = series order)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from opentsdb_amd import dist as odist
+from opentsdb_amd import workload
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_ranges_cover_series_in_order():
+    for n in (0, 1, 7, 100, 1001):
+        for w in (1, 2, 3, 8):
+            rs = [odist.shard_range(n, w, r) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            for (a, b), (c, d) in zip(rs, rs[1:]):
+                assert b == c and a <= b
+            sizes = [b - a for a, b in rs]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_shared_groups_by_config():
+    n = 1000
+    host = workload.group_ids("C2", 0, n)
+    assert len(odist.shared_groups(host, 2)) == 0      # {host=*}: rank-local
+    assert len(odist.shared_groups(host, 8)) <= 7      # at most one per cut
+    dc = workload.group_ids("C3", 0, n)
+    assert len(odist.shared_groups(dc, 2)) == 16       # {dc=*}: spans ranks
+    one = workload.group_ids("C5", 0, n)
+    assert list(odist.shared_groups(one, 4)) == [0]
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(100 + rank)
+    GB = 37
+    s = rng.random(GB) * 10
+    n = rng.integers(0, 5, GB)
+    parts = np.zeros((GB, 4), np.int64)
+    parts[:, 0] = s.view(np.int64)
+    parts[:, 3] = n
+    emit = (n > 0).astype(np.uint8)
+    gp, ge = odist.all_gather_partials(torch.from_numpy(parts),
+                                       torch.from_numpy(emit))
+    if rank == 0:
+        q.put((gp.numpy(), ge.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_partial_exchange_gloo_world2():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    gp, ge = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert gp.shape == (2, 37, 4) and ge.shape == (2, 37)
+    # rank-major: slice r is exactly what rank r contributed
+    for r in range(world):
+        rng = np.random.default_rng(100 + r)
+        s = rng.random(37) * 10
+        n = rng.integers(0, 5, 37)
+        assert np.array_equal(gp[r, :, 0].view(np.float64), s)
+        assert np.array_equal(gp[r, :, 3], n)
+        assert np.array_equal(ge[r], (n > 0).astype(np.uint8))
+    s, n = odist.merge_partials_reference(gp)
+    exp_s = gp[0, :, 0].view(np.float64) + gp[1, :, 0].view(np.float64)
+    assert np.array_equal(s, exp_s)
