@@ -18,6 +18,7 @@
 
 #include "../../include/otsdb_agg.h"
 #include "kernels.hip"
+#include "select.hip"
 
 using namespace otsdb;
 
@@ -135,7 +136,7 @@ struct otsdb_ctx {
   std::vector<int64_t> goff_cache;
   int64_t* d_tiles = nullptr;
   size_t d_tiles_cap = 0;
-  int64_t n_tiles = 0, n_multi = 0;
+  int64_t n_tiles = 0, n_multi = 0, n_large = 0, n_large_chunks = 0;
   std::mutex mu;  // one query at a time per context
   // stage timing (otsdb_prof_*)
   bool prof = false;
@@ -256,6 +257,7 @@ otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff) {
   if (c->d_tiles && goff == c->goff_cache) return OTSDB_OK;
   const int64_t G = (int64_t)goff.size() - 1;
   std::vector<int64_t> tg, tm0, tm1, mg, mt0, mt1, ag, at0, at1;
+  std::vector<int64_t> lgg, lgo, lgk, lgc{0};  // groups for radix select
   std::vector<uint8_t> single;
   for (int64_t g = 0; g < G; ++g) {
     const int64_t a = goff[g], b = goff[g + 1];
@@ -275,10 +277,18 @@ otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff) {
     ag.push_back(g);
     at0.push_back(t0);
     at1.push_back(t1);
+    if (b - a > SEL_K) {
+      lgg.push_back(g);
+      lgo.push_back(a);
+      lgk.push_back(b - a);
+      lgc.push_back(lgc.back() + (b - a + SEL_CHUNK - 1) / SEL_CHUNK);
+    }
   }
+  const int64_t LG = (int64_t)lgg.size();
   const int64_t T = (int64_t)tg.size(), MG = (int64_t)mg.size();
-  // layout: tg tm0 tm1 [T] | mg mt0 mt1 [MG] | ag at0 at1 [G] | single [T]
-  const size_t n64 = 3 * T + 3 * MG + 3 * G;
+  // layout: tg tm0 tm1 [T] | mg mt0 mt1 [MG] | ag at0 at1 [G] |
+  //         lg_g lg_off lg_k [LG] | lg_ch0 [LG+1] | single [T]
+  const size_t n64 = 3 * T + 3 * MG + 3 * G + 4 * LG + 1;
   const size_t bytes = n64 * 8 + T + 64;
   void* p = c->d_tiles;
   size_t cap = c->d_tiles_cap;
@@ -297,6 +307,10 @@ otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff) {
   h.insert(h.end(), ag.begin(), ag.end());
   h.insert(h.end(), at0.begin(), at0.end());
   h.insert(h.end(), at1.begin(), at1.end());
+  h.insert(h.end(), lgg.begin(), lgg.end());
+  h.insert(h.end(), lgo.begin(), lgo.end());
+  h.insert(h.end(), lgk.begin(), lgk.end());
+  h.insert(h.end(), lgc.begin(), lgc.end());
   if (!h.empty())
     HIP_TRY(hipMemcpyAsync(c->d_tiles, h.data(), n64 * 8,
                            hipMemcpyHostToDevice, c->stream));
@@ -307,13 +321,16 @@ otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff) {
   c->goff_cache = goff;
   c->n_tiles = T;
   c->n_multi = MG;
+  c->n_large = LG;
+  c->n_large_chunks = lgc.back();
   return OTSDB_OK;
 }
 
 struct Tiles {
   const int64_t *tg, *tm0, *tm1, *mg, *mt0, *mt1, *ag, *at0, *at1;
+  const int64_t *lg_g, *lg_off, *lg_k, *lg_ch0;
   const uint8_t* single;
-  int64_t T, MG, G;
+  int64_t T, MG, G, LG, LGCH;
 };
 
 Tiles tiles_of(otsdb_ctx* c, int64_t G) {
@@ -329,7 +346,14 @@ Tiles tiles_of(otsdb_ctx* c, int64_t G) {
   t.ag = b + 3 * T + 3 * MG;
   t.at0 = t.ag + G;
   t.at1 = t.ag + 2 * G;
-  t.single = (const uint8_t*)(b + 3 * T + 3 * MG + 3 * G);
+  const int64_t LG = c->n_large;
+  t.lg_g = b + 3 * T + 3 * MG + 3 * G;
+  t.lg_off = t.lg_g + LG;
+  t.lg_k = t.lg_g + 2 * LG;
+  t.lg_ch0 = t.lg_g + 3 * LG;
+  t.single = (const uint8_t*)(b + 3 * T + 3 * MG + 3 * G + 4 * LG + 1);
+  t.LG = LG;
+  t.LGCH = c->n_large_chunks;
   t.T = T;
   t.MG = MG;
   t.G = G;
@@ -376,6 +400,9 @@ struct Work {
   double* out_val;
   uint8_t* out_emit;
   int64_t* counts;
+  uint64_t* keys = nullptr;
+  SelState* sel = nullptr;
+  uint32_t* hist = nullptr;
 };
 
 // Everything up to dense (group, bucket) results / partials.
@@ -420,6 +447,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   const int64_t NB = P.nb;
 
   // workspace
+  const bool sel_large = is_selection(spec->agg_id) && T.LG > 0;
   auto carve = [&](char* base) {
     Carve cv{base};
     W.SM.lo = cv.take<int64_t>(S);
@@ -435,6 +463,11 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     W.out_val = cv.take<double>((size_t)G * NB);
     W.out_emit = cv.take<uint8_t>((size_t)G * NB);
     W.counts = cv.take<int64_t>(G + 1);
+    if (sel_large) {
+      W.keys = cv.take<uint64_t>((size_t)goff.back() * NB);
+      W.sel = cv.take<SelState>((size_t)T.LG * NB);
+      W.hist = cv.take<uint32_t>((size_t)T.LG * NB * 512);
+    }
     return cv.off + 256;
   };
   const size_t need = carve(nullptr);
@@ -486,12 +519,49 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       if (mode != 0)
         return fail(OTSDB_E_UNSUPPORTED,
                     "percentiles across ranks are not offloaded yet");
+      const int median = spec->agg_id == OTSDB_AGG_MEDIAN ? 1 : 0;
+      // n (non-NaN contributions) and the emit mask of every group
+      using MC = MSum<3>;
+      if (T.T > 0)
+        hipLaunchKernelGGL(k_group<MC>, dim3(blocks_for(T.T * NB, 256)),
+                           dim3(256), 0, st, NB, T.T, T.tg, T.tm0, T.tm1,
+                           T.single, d_members, W.R, W.partial, W.tile_emit,
+                           W.out_val, W.out_emit, c->d_err, 0);
+      if (T.MG > 0)
+        hipLaunchKernelGGL(k_combine<MC>, dim3(blocks_for(T.MG * NB, 256)),
+                           dim3(256), 0, st, NB, T.MG, T.mg, T.mt0, T.mt1,
+                           W.partial, W.tile_emit, W.out_val, W.out_emit,
+                           (Packed*)nullptr, c->d_err);
+      // groups of <= SEL_K series: sort in LDS
       hipLaunchKernelGGL(k_group_select,
                          dim3(blocks_for(T.T * NB, SEL_THREADS)),
                          dim3(SEL_THREADS), 0, st, NB, T.T, T.tg, T.tm0, T.tm1,
                          T.single, d_members, W.R, W.out_val, W.out_emit,
-                         c->d_err, spec->agg_id == OTSDB_AGG_MEDIAN ? 1 : 0,
-                         P.pct);
+                         c->d_err, median, P.pct);
+      // larger groups: radix select over transposed keys
+      if (T.LG > 0) {
+        const int64_t M = goff.back();
+        const int64_t NSEG = T.LG * NB;
+        hipLaunchKernelGGL(k_keys_transpose,
+                           dim3(blocks_for(M, 64), blocks_for(NB, 64)),
+                           dim3(256), 0, st, NB, M, d_members, W.R, W.keys);
+        hipLaunchKernelGGL(k_sel_init, dim3(blocks_for(NSEG, 256)), dim3(256),
+                           0, st, NB, T.LG, T.lg_g, (const double*)W.out_val,
+                           (const uint8_t*)W.out_emit, W.sel, median, P.pct);
+        HIP_TRY(hipMemsetAsync(W.hist, 0, (size_t)NSEG * 512 * 4, st));
+        for (int pass = 0; pass < 8; ++pass) {
+          hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)(T.LGCH * NB)),
+                             dim3(256), 0, st, pass, NB, M, T.LG, T.lg_off,
+                             T.lg_k, T.lg_ch0, (const uint64_t*)W.keys,
+                             (const SelState*)W.sel, W.hist);
+          hipLaunchKernelGGL(k_radix_select, dim3(blocks_for(NSEG * 2, 256)),
+                             dim3(256), 0, st, pass, NSEG, W.hist, W.sel);
+        }
+        hipLaunchKernelGGL(k_sel_finish, dim3(blocks_for(NSEG, 256)),
+                           dim3(256), 0, st, NB, T.LG, T.lg_g,
+                           (const SelState*)W.sel, (const uint8_t*)W.out_emit,
+                           W.out_val, c->d_err, median, P.pct);
+      }
     } else {
       ok = with_monoid(spec->agg_id, [&](auto tag) {
         using M = decltype(tag);

@@ -696,15 +696,10 @@ __global__ __launch_bounds__(SEL_THREADS) void k_group_select(
   const int64_t t = idx / nb;
   if (t >= n_tiles) return;
   const int64_t b = idx - t * nb;
-  if (!tile_single[t]) {
-    atomicOr(err_word, ERR_SEL_TOO_BIG);
-    return;
-  }
+  // groups above SEL_K series go through the radix-select path (select.hip)
+  if (!tile_single[t]) return;
   const int64_t m0 = tile_m0[t], m1 = tile_m1[t];
-  if (m1 - m0 > SEL_K) {
-    atomicOr(err_word, ERR_SEL_TOO_BIG);
-    return;
-  }
+  if (m1 - m0 > SEL_K) return;
   int n = 0, emit = 0;
   for (int64_t m = m0; m < m1; ++m) {
     const int64_t off = members[m] * nb + b;

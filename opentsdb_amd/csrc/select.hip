@@ -1,0 +1,220 @@
+// select.hip — median / percentile across the series of large groups
+// (PercentileAgg.runDouble, Aggregators.java:687-706, commons-math3 3.4.1
+// LEGACY estimator; Median.runDouble, :412-431) by MSB radix select over
+// order-preserving 64-bit keys.
+//
+//  k_keys_transpose  bucket rows [S][B] -> key columns [B][M] (members in
+//                    group order; non-contributing / NaN -> KEY_NONE), via
+//                    64x64 LDS tiles so both the read and the write coalesce
+//  k_sel_init        per (group, bucket): n (non-NaN contributions) -> the
+//                    one or two target ranks the estimator needs
+//  k_radix_hist      per pass (8 bits of key): LDS histograms of the keys
+//                    that still match each target's prefix, flushed with one
+//                    global atomic per non-empty bin
+//  k_radix_select    per (segment, target): picks the digit holding the rank
+//  k_sel_finish      keys -> doubles -> estimator, "Got Infinity" check
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace otsdb {
+
+constexpr uint64_t KEY_NONE = ~0ULL;
+constexpr int SEL_CHUNK = 8192;  // keys per histogram block
+
+DEV uint64_t dkey(double v) {  // total order, -0.0 < 0.0 (Double.compareTo)
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
+}
+DEV double key_value(uint64_t k) {
+  const uint64_t u = (k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFULL) : ~k;
+  return __longlong_as_double((long long)u);
+}
+
+__global__ __launch_bounds__(256) void k_keys_transpose(
+    int64_t nb, int64_t M, const int64_t* __restrict__ members, Rows R,
+    uint64_t* __restrict__ keys) {
+  __shared__ uint64_t tile[64][65];
+  const int tid = threadIdx.x;
+  const int64_t m0 = (int64_t)blockIdx.x * 64, b0 = (int64_t)blockIdx.y * 64;
+  const int bi = tid & 63;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int mi = r * 4 + (tid >> 6);
+    const int64_t m = m0 + mi, b = b0 + bi;
+    uint64_t k = KEY_NONE;
+    if (m < M && b < nb) {
+      const int64_t off = members[m] * nb + b;
+      const uint8_t st = R.state[off];
+      if (st) {
+        const double v = R.val[off];
+        if (!is_nan(v)) k = dkey(v);
+      }
+    }
+    tile[mi][bi] = k;
+  }
+  __syncthreads();
+  const int mi = tid & 63;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int bj = r * 4 + (tid >> 6);
+    const int64_t m = m0 + mi, b = b0 + bj;
+    if (m < M && b < nb) keys[b * M + m] = tile[mi][bj];
+  }
+}
+
+struct SelState {
+  uint64_t prefix[2];
+  int64_t rank[2];
+  int64_t n;
+  int32_t ntarget;
+  int32_t _pad;
+};
+
+// segments: seg = lg * nb + b for large group lg (group id lg_g[lg])
+__global__ void k_sel_init(int64_t nb, int64_t n_lg,
+                           const int64_t* __restrict__ lg_g,
+                           const double* __restrict__ count_val,
+                           const uint8_t* __restrict__ count_emit,
+                           SelState* __restrict__ sel, int median, double p) {
+  const int64_t seg = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (seg >= n_lg * nb) return;
+  const int64_t lg = seg / nb, b = seg - lg * nb;
+  const int64_t o = lg_g[lg] * nb + b;
+  SelState s;
+  s.prefix[0] = s.prefix[1] = 0;
+  s.n = count_emit[o] ? (int64_t)count_val[o] : 0;
+  s.ntarget = 0;
+  s.rank[0] = s.rank[1] = 0;
+  if (s.n > 0) {
+    if (median) {
+      s.rank[0] = s.rank[1] = s.n / 2;
+    } else if (s.n == 1) {
+      s.rank[0] = s.rank[1] = 0;
+    } else {
+      const double pos = p * (double)(s.n + 1);
+      if (pos < 1) {
+        s.rank[0] = s.rank[1] = 0;
+      } else if (pos >= (double)s.n) {
+        s.rank[0] = s.rank[1] = s.n - 1;
+      } else {
+        const int64_t ip = (int64_t)__builtin_floor(pos);
+        s.rank[0] = ip - 1;
+        s.rank[1] = ip;
+      }
+    }
+    s.ntarget = (s.rank[0] == s.rank[1]) ? 1 : 2;
+  }
+  sel[seg] = s;
+}
+
+__global__ __launch_bounds__(256) void k_radix_hist(
+    int pass, int64_t nb, int64_t M, int64_t n_lg,
+    const int64_t* __restrict__ lg_off, const int64_t* __restrict__ lg_k,
+    const int64_t* __restrict__ lg_ch0, const uint64_t* __restrict__ keys,
+    const SelState* __restrict__ sel, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[2][256];
+  const int tid = threadIdx.x;
+  h[0][tid] = 0;
+  h[1][tid] = 0;
+  // block -> (large group, bucket, chunk)
+  const int64_t bid = blockIdx.x;
+  int64_t a = 0, z = n_lg;
+  while (z - a > 1) {
+    const int64_t mid = (a + z) >> 1;
+    if (lg_ch0[mid] * nb <= bid) a = mid;
+    else z = mid;
+  }
+  const int64_t lg = a;
+  const int64_t k = lg_k[lg];
+  const int64_t nch = (k + SEL_CHUNK - 1) / SEL_CHUNK;
+  const int64_t local = bid - lg_ch0[lg] * nb;
+  const int64_t b = local / nch, c = local - b * nch;
+  const int64_t seg = lg * nb + b;
+  const SelState s = sel[seg];
+  __syncthreads();
+  if (s.ntarget == 0) return;
+  const int shift = 56 - 8 * pass;
+  const uint64_t* col = keys + b * M + lg_off[lg];
+  const int64_t i1 = (c + 1) * SEL_CHUNK < k ? (c + 1) * SEL_CHUNK : k;
+  for (int64_t i = c * SEL_CHUNK + tid; i < i1; i += 256) {
+    const uint64_t key = col[i];
+    if (key == KEY_NONE) continue;
+    const unsigned d = (unsigned)(key >> shift) & 255u;
+    for (int t = 0; t < s.ntarget; ++t) {
+      if (pass == 0 || (key >> (shift + 8)) == (s.prefix[t] >> (shift + 8)))
+        atomicAdd(&h[t][d], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t* g = hist + seg * 512;
+  for (int t = 0; t < s.ntarget; ++t)
+    if (h[t][tid]) atomicAdd(&g[t * 256 + tid], h[t][tid]);
+}
+
+__global__ void k_radix_select(int pass, int64_t n_seg,
+                               uint32_t* __restrict__ hist,
+                               SelState* __restrict__ sel) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_seg * 2) return;
+  const int64_t seg = i >> 1;
+  const int t = (int)(i & 1);
+  SelState& s = sel[seg];
+  uint32_t* h = hist + seg * 512;
+  if (t >= s.ntarget) {
+    if (t == 1 && s.ntarget == 1) {
+      // keep target 1 in step with target 0 (same rank)
+    }
+    for (int d = 0; d < 256; ++d) h[t * 256 + d] = 0;
+    return;
+  }
+  const int shift = 56 - 8 * pass;
+  int64_t r = s.rank[t];
+  int64_t cum = 0;
+  int d = 0;
+  for (; d < 255; ++d) {
+    const int64_t c = h[t * 256 + d];
+    if (cum + c > r) break;
+    cum += c;
+  }
+  s.prefix[t] |= (uint64_t)d << shift;
+  s.rank[t] = r - cum;
+  for (int e = 0; e < 256; ++e) h[t * 256 + e] = 0;
+}
+
+__global__ void k_sel_finish(int64_t nb, int64_t n_lg,
+                             const int64_t* __restrict__ lg_g,
+                             const SelState* __restrict__ sel,
+                             const uint8_t* __restrict__ emit,
+                             double* __restrict__ out_val, int* err_word,
+                             int median, double p) {
+  const int64_t seg = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (seg >= n_lg * nb) return;
+  const int64_t lg = seg / nb, b = seg - lg * nb;
+  const int64_t o = lg_g[lg] * nb + b;
+  if (!emit[o]) return;
+  const SelState s = sel[seg];
+  double r;
+  if (s.n == 0) {
+    r = qnan();
+  } else if (median || s.n == 1) {
+    r = key_value(s.prefix[0]);
+  } else {
+    const double pos = p * (double)(s.n + 1);
+    if (pos < 1 || pos >= (double)s.n) {
+      r = key_value(s.prefix[0]);
+    } else {
+      const double fpos = __builtin_floor(pos);
+      const double dif = pos - fpos;
+      const double lower = key_value(s.prefix[0]);
+      const double upper = key_value(s.ntarget == 2 ? s.prefix[1] : s.prefix[0]);
+      r = lower + dif * (upper - lower);
+    }
+  }
+  if (is_inf(r)) atomicOr(err_word, ERR_INFINITY);
+  out_val[o] = r;
+}
+
+}  // namespace otsdb

@@ -203,6 +203,21 @@ def test_big_groups_chunked(engine):
         check(engine, spec, b, agg in ORDER_FREE, scale=100.0, where="big/" + agg)
 
 
+@pytest.mark.parametrize("n_series", [45, 300])
+def test_percentiles_large_groups(engine, n_series):
+    """median / percentiles over groups above the LDS-sort limit: radix
+    select over transposed keys (exact: selection + the reference's
+    estimator arithmetic)."""
+    b = datasets.random_batch(77, n_series=n_series, big_group=True,
+                              span_ms=3600 * 1000, cadence_ms=30000,
+                              nan_frac=0.05)
+    for agg in ("median", "p50", "p75", "p99", "p999", "ep95r3", "ep50r7"):
+        for fill in ("none", "nan"):
+            spec = _spec(agg, "max", fill, end=datasets.T0 + 3600 * 1000)
+            check(engine, spec, b, True, where="sel%d/%s/%s" % (
+                n_series, agg, fill))
+
+
 def test_got_infinity(engine):
     """AggregationIterator.doubleValue throws on +-Infinity
     (AggregationIterator.java:640-643)."""
