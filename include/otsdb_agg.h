@@ -244,6 +244,34 @@ otsdb_status otsdb_agg_finalize_device(otsdb_ctx* ctx,
                                        const uint8_t* emit,
                                        otsdb_result* out, void* hip_stream);
 
+/* ---- compacted-cell decode (RowSeq) ------------------- */
+/* The storage rows of a query as the scanner hands them to Span.addRow
+ * (Span.java:177-220): one compacted column per (series, hour) row —
+ * concatenated 2-byte (seconds) / 4-byte (ms) qualifiers and concatenated
+ * big-endian values, plus the trailing meta byte of multi-value columns
+ * (CompactionQueue.buildCompactedColumn, CompactionQueue.java:594-616).
+ * Rows sorted by (series, base time).  DEVICE pointers.                     */
+typedef struct {
+  int64_t n_rows;            /* R                                          */
+  const int64_t* row_series; /* [R] series index, nondecreasing            */
+  const int64_t* row_base_s; /* [R] row base time, seconds                 */
+  const int64_t* qual_off;   /* [R+1] offsets into qual                    */
+  const uint8_t* qual;       /* qualifier bytes                            */
+  const int64_t* val_off;    /* [R+1] offsets into val                     */
+  const uint8_t* val;        /* value bytes                                */
+} otsdb_cells;
+
+/* Decodes the rows into a columnar batch (RowSeq.Iterator semantics,
+ * RowSeq.java:552-643): offsets[S+1] (series point CSR), ts_ms/val/is_float
+ * [capacity].  Pass ts_ms=NULL to only count (offsets filled, offsets[S] =
+ * points).  A column whose value bytes do not match its qualifiers is
+ * OTSDB_E_ILLEGAL_DATA (Internal.extractDataPoints, Internal.java:307-321). */
+otsdb_status otsdb_decode_cells_device(otsdb_ctx* ctx, const otsdb_cells* cells,
+                                       int64_t n_series, int64_t* offsets,
+                                       int64_t* ts_ms, int64_t* val,
+                                       uint8_t* is_float, int64_t capacity,
+                                       void* hip_stream);
+
 /* ---- stage timing (bench roofline) ------------------------------------- */
 /* When enabled, every query records HIP events around its pipeline stages
  * on the query's stream.  otsdb_prof_read returns, per stage, the summed

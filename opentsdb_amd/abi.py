@@ -80,6 +80,18 @@ class Partial(C.Structure):
                 ("w", C.c_int64)]
 
 
+class Cells(C.Structure):
+    _fields_ = [
+        ("n_rows", C.c_int64),
+        ("row_series", C.c_void_p),
+        ("row_base_s", C.c_void_p),
+        ("qual_off", C.c_void_p),
+        ("qual", C.c_void_p),
+        ("val_off", C.c_void_p),
+        ("val", C.c_void_p),
+    ]
+
+
 class GenSpec(C.Structure):
     _fields_ = [
         ("seed", C.c_uint64),
@@ -98,6 +110,7 @@ EXPORTS = [
     "otsdb_agg_run_device", "otsdb_agg_partials_device",
     "otsdb_agg_finalize_device", "otsdb_gen_counts_device",
     "otsdb_gen_fill_device", "otsdb_prof_enable", "otsdb_prof_read",
+    "otsdb_decode_cells_device",
 ]
 
 _lib = None
@@ -152,6 +165,9 @@ def load(path=None):
     lib.otsdb_gen_counts_device.restype = C.c_int
     lib.otsdb_gen_fill_device.argtypes = [vp, PG, i64, i64, vp, vp, vp, vp]
     lib.otsdb_gen_fill_device.restype = C.c_int
+    lib.otsdb_decode_cells_device.argtypes = [vp, C.POINTER(Cells), i64, vp,
+                                              vp, vp, vp, i64, vp]
+    lib.otsdb_decode_cells_device.restype = C.c_int
     lib.otsdb_prof_enable.argtypes = [vp, C.c_int]
     lib.otsdb_prof_enable.restype = C.c_int
     lib.otsdb_prof_read.argtypes = [vp, vp, vp, C.c_int, C.c_int]

@@ -19,6 +19,7 @@
 #include "../../include/otsdb_agg.h"
 #include "kernels.hip"
 #include "select.hip"
+#include "decode.hip"
 
 using namespace otsdb;
 
@@ -146,6 +147,8 @@ struct otsdb_ctx {
   double prof_ms[8] = {0};
   int64_t prof_n[8] = {0};
   int bucketize_k = 8;  // points per lane in k_bucketize (OTSDB_BUCKETIZE_K)
+  void* dec_ws = nullptr;  // decode workspace
+  size_t dec_ws_cap = 0;
 };
 
 namespace {
@@ -723,6 +726,7 @@ void otsdb_ctx_destroy(otsdb_ctx* c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->ws) hipFree(c->ws);
   if (c->stage) hipFree(c->stage);
+  if (c->dec_ws) hipFree(c->dec_ws);
   if (c->d_tiles) hipFree(c->d_tiles);
   if (c->d_err) hipFree(c->d_err);
   for (auto e : c->ev_pool) hipEventDestroy(e);
@@ -953,6 +957,62 @@ otsdb_status otsdb_agg_finalize_device(otsdb_ctx* c,
   }
   c->stream = saved;
   return rc;
+}
+
+otsdb_status otsdb_decode_cells_device(otsdb_ctx* c, const otsdb_cells* cells,
+                                       int64_t n_series, int64_t* offsets,
+                                       int64_t* ts_ms, int64_t* val,
+                                       uint8_t* is_float, int64_t capacity,
+                                       void* hip_stream) {
+  if (!c || !cells || !offsets) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  if (ts_ms && (!val || !is_float))
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null output column");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  const int64_t R = cells->n_rows, S = n_series;
+  if (R < 0 || S < 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
+  // workspace: row counts + row output offsets
+  otsdb_status rc = ensure(&c->dec_ws, &c->dec_ws_cap, (size_t)(2 * R + 2) * 8);
+  if (rc) return rc;
+  int64_t* row_count = (int64_t*)c->dec_ws;
+  int64_t* row_out = row_count + (R + 1);
+  CellsDev C{R, cells->row_series, cells->row_base_s, cells->qual_off,
+             cells->qual, cells->val_off, cells->val};
+  HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), st));
+  if (R > 0) {
+    hipLaunchKernelGGL(k_decode, dim3(blocks_for(R, 4)), dim3(256), 0, st, C,
+                       0, row_count, (const int64_t*)nullptr, (int64_t)0,
+                       (int64_t*)nullptr, (int64_t*)nullptr,
+                       (uint8_t*)nullptr, c->d_err);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, R,
+                       (const int64_t*)row_count, row_out);
+  } else {
+    HIP_TRY(hipMemsetAsync(row_out, 0, 8, st));
+  }
+  hipLaunchKernelGGL(k_series_offsets, dim3(blocks_for(R + 1, 256)), dim3(256),
+                     0, st, R, S, cells->row_series, (const int64_t*)row_out,
+                     offsets);
+  HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
+                         hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_small[1], row_out + R, 8, hipMemcpyDeviceToHost,
+                         st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (c->h_small[0] & ERR_CORRUPT_CELL)
+    return fail(OTSDB_E_ILLEGAL_DATA,
+                "Corrupted value: couldn't break down into individual values");
+  const int64_t total = c->h_small[1];
+  if (!ts_ms) return OTSDB_OK;
+  if (total > capacity)
+    return fail(OTSDB_E_CAPACITY, "decode capacity %lld < %lld points",
+                (long long)capacity, (long long)total);
+  if (R > 0)
+    hipLaunchKernelGGL(k_decode, dim3(blocks_for(R, 4)), dim3(256), 0, st, C,
+                       1, row_count, (const int64_t*)row_out, capacity, ts_ms,
+                       val, is_float, c->d_err);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(st));
+  return OTSDB_OK;
 }
 
 otsdb_status otsdb_prof_enable(otsdb_ctx* c, int enable) {
