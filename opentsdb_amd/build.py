@@ -36,8 +36,11 @@ def up_to_date():
 def build(force=False, verbose=False):
     if not force and up_to_date():
         return OUT
+    flags = list(FLAGS)
+    if os.environ.get("OTSDB_BUCKETIZE_VARIANTS"):
+        flags.append("-DOTSDB_BUCKETIZE_VARIANTS=1")
     os.makedirs(OUT_DIR, exist_ok=True)
-    cmd = ["/opt/rocm/bin/hipcc"] + FLAGS + ["-o", OUT + ".tmp", SRC]
+    cmd = ["/opt/rocm/bin/hipcc"] + flags + ["-o", OUT + ".tmp", SRC]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

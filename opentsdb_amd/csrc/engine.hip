@@ -14,6 +14,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/otsdb_agg.h"
@@ -229,6 +230,7 @@ otsdb_status make_params(const otsdb_query_spec* s, Params* P) {
     P->stop_ts = s->query_end_ms;
     P->nb = (s->query_start_ms >= s->start_ms &&
              s->query_start_ms <= s->end_ms) ? 1 : 0;
+    P->narrow = 1;  // every point is bucket 0
     return OTSDB_OK;
   }
   const int64_t iv = s->ds_interval_ms;
@@ -253,6 +255,8 @@ otsdb_status make_params(const otsdb_query_spec* s, Params* P) {
     P->nb = s->end_ms >= grid0 ? (s->end_ms - grid0) / iv + 1 : 0;
     P->stop_ts = grid0 + P->nb * iv;
   }
+  // points fed to the bucket fold lie in [gbase, stop_ts): 32-bit offsets
+  P->narrow = iv < (int64_t(1) << 31) && P->nb < (int64_t(1) << 32) / iv;
   return OTSDB_OK;
 }
 
@@ -504,6 +508,71 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
           hipLaunchKernelGGL((k_bucketize_k<M, 4>), grid, blk, 0, st, P, B,
                              W.SM, W.R);
           break;
+#ifdef OTSDB_BUCKETIZE_VARIANTS
+        // tuning variants (K, prefetch, non-temporal), avg downsampler only
+        case 16: case 41: case 81: case 86: case 88: case 46: case 48: case 99:
+        case 80: case 40: case 97: case 85: case 89: case 49: case 82: case 42: case 96:
+          if constexpr (std::is_same<M, MSum<1>>::value) {
+            const int v = c->bucketize_k;
+            Params P0 = P;  // 80/40: the generic (branchy) fold only
+            P0.narrow = 0;
+            if (v == 80)
+              hipLaunchKernelGGL((k_bucketize_k<M, 8>), grid, blk, 0, st, P0,
+                                 B, W.SM, W.R);
+            else if (v == 40)
+              hipLaunchKernelGGL((k_bucketize_k<M, 4>), grid, blk, 0, st, P0,
+                                 B, W.SM, W.R);
+            else if (v == 97)  // loads-only at 4 waves/SIMD (LDS-limited)
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 1>), grid, blk,
+                                 36 * 1024, st, P, B, W.SM, W.R);
+            else if (v == 89)
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1>), grid, blk,
+                                 0, st, P, B, W.SM, W.R);
+            else if (v == 49)
+              hipLaunchKernelGGL((k_bucketize_k<M, 4, 0, 0, 1, 0, 1>), grid, blk,
+                                 0, st, P, B, W.SM, W.R);
+            else if (v == 96) {  // timing only: every series writes one row
+              Params P1 = P;
+              P1.nb = 0;
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1>), grid, blk,
+                                 0, st, P1, B, W.SM, W.R);
+            } else if (v == 82)
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 1, 0, 1, 0, 1>), grid, blk,
+                                 0, st, P, B, W.SM, W.R);
+            else if (v == 42)
+              hipLaunchKernelGGL((k_bucketize_k<M, 4, 1, 0, 1, 0, 1>), grid, blk,
+                                 0, st, P, B, W.SM, W.R);
+            else if (v == 85)
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 5>), grid, blk, 0,
+                                 st, P, B, W.SM, W.R);
+            else if (v == 16)
+              hipLaunchKernelGGL((k_bucketize_k<M, 16>), grid, blk, 0, st, P,
+                                 B, W.SM, W.R);
+            else if (v == 41)
+              hipLaunchKernelGGL((k_bucketize_k<M, 4, 1, 0>), grid, blk, 0, st,
+                                 P, B, W.SM, W.R);
+            else if (v == 81)
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 1, 0>), grid, blk, 0, st,
+                                 P, B, W.SM, W.R);
+            else if (v == 99)
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 1>), grid, blk, 0,
+                                 st, P, B, W.SM, W.R);
+            else if (v == 86)
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 6>), grid, blk, 0,
+                                 st, P, B, W.SM, W.R);
+            else if (v == 88)
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 8>), grid, blk, 0,
+                                 st, P, B, W.SM, W.R);
+            else if (v == 46)
+              hipLaunchKernelGGL((k_bucketize_k<M, 4, 0, 0, 6>), grid, blk, 0,
+                                 st, P, B, W.SM, W.R);
+            else
+              hipLaunchKernelGGL((k_bucketize_k<M, 4, 0, 0, 8>), grid, blk, 0,
+                                 st, P, B, W.SM, W.R);
+            break;
+          }
+          [[fallthrough]];
+#endif
         default:
           hipLaunchKernelGGL((k_bucketize_k<M, 8>), grid, blk, 0, st, P, B,
                              W.SM, W.R);

@@ -55,6 +55,7 @@ struct Params {
   int64_t rate_origin_ts;
   double rate_origin_val;
   int32_t run_all, fill, rate, counter, drop_resets, interp;
+  int32_t narrow;        // grid spans < 2^32 ms and interval < 2^31 ms
   double pct;            // percentile / 100.0 (PercentileAgg)
 };
 

@@ -215,9 +215,136 @@ __global__ __launch_bounds__(256) void k_bucketize(Params P, BatchDev B,
 // and last ("tail") runs to a segmented wave scan over the tails — so the
 // cross-lane scan is paid once per 64*K points instead of once per 128.
 // ------------------------------------------------------------------------
-template <class M, int K>
-__global__ __launch_bounds__(256) void k_bucketize_k(Params P, BatchDev B,
-                                                     SeriesMeta SM, Rows R) {
+typedef long long ll2_t __attribute__((ext_vector_type(2)));
+
+// Bucket index when the grid spans < 2^32 ms (P.narrow): a 32-bit relative
+// time, a double-reciprocal estimate and one exact correction — branch free.
+DEV int bucket_narrow(const Params& P, int64_t ts) {
+  if (P.run_all) return 0;
+  const uint32_t rel = (uint32_t)(ts - P.gbase);
+  const uint32_t iv = (uint32_t)P.interval;
+  uint32_t q = (uint32_t)((double)rel * P.inv_interval);
+  const uint32_t r = rel - q * iv;
+  q = ((int32_t)r < 0) ? q - 1 : (r >= iv ? q + 1 : q);
+  return (int)q;
+}
+
+// Fast lane fold for lanes whose K points fall into at most two buckets
+// (the common case when buckets hold more than K points): both runs are
+// accumulated branch free with masked pushes, in point order.  Returns false
+// (nothing changed) when the lane spans three or more buckets.
+template <class M, int K, bool FLOATONLY>
+DEV bool fold_fast(const Params& P, const BatchDev& B, int sf, int64_t i0,
+                   const int64_t* t, const int64_t* v, int& nseg, int& cur_key,
+                   int& head_key, M& cur, M& head) {
+  int k[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) k[j] = bucket_narrow(P, t[j]);
+  const int k0 = k[0], k1 = k[K - 1];
+  bool ok = true;
+#pragma unroll
+  for (int j = 1; j < K - 1; ++j) ok &= (k[j] == k0) | (k[j] == k1);
+  if (!ok) return false;
+  M h = M::init(), c = M::init();
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const double x =
+        FLOATONLY ? bits_to_double(v[j]) : point_value(B, i0 + j, v[j], sf);
+    const bool inh = k[j] == k0;
+    h.push_if(inh, x);
+    c.push_if(!inh, x);
+  }
+  head_key = k0;
+  if (k0 == k1) {
+    nseg = 1;
+    cur_key = k0;
+    cur = h;
+  } else {
+    nseg = 2;
+    cur_key = k1;
+    head = h;
+    cur = c;
+  }
+  return true;
+}
+
+// Folds the K points of one lane in order: the first run (which may continue
+// from the previous lane) goes to `head`, the last run (which may continue
+// into the next lane) stays in `cur`, runs in between close here.
+template <class M, int K, bool FLOATONLY, bool CHECKED>
+DEV void fold_lane(const Params& P, const BatchDev& B, int sf, int64_t i0,
+                   int64_t lo, int64_t hi, const int64_t* t, const int64_t* v,
+                   double* rowv, uint8_t* rows, int& err, int& nseg,
+                   int& cur_key, int& head_key, M& cur, M& head) {
+  int64_t bnd = INT64_MIN;  // first timestamp past cur_key's bucket
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const int64_t i = i0 + j;
+    if (CHECKED && (i < lo || i >= hi)) continue;
+    int k = cur_key;
+    if (nseg == 0 || t[j] >= bnd) {
+      k = (int)bucket_of(P, t[j]);
+      bnd = P.run_all ? INT64_MAX : P.gbase + ((int64_t)k + 1) * P.interval;
+    }
+    const double x = FLOATONLY ? bits_to_double(v[j]) : point_value(B, i, v[j], sf);
+    if (nseg == 0) {
+      cur_key = k;
+      cur = M::from(x);
+      nseg = 1;
+    } else if (k == cur_key) {
+      cur.push(x);
+    } else {
+      if (nseg == 1) {
+        head_key = cur_key;
+        head = cur;
+      } else {  // a bucket wholly inside this lane
+        rowv[cur_key] = cur.finish(&err);
+        rows[cur_key] = ST_REAL;
+      }
+      cur_key = k;
+      cur = M::from(x);
+      ++nseg;
+    }
+  }
+}
+
+// Segmented inclusive scan step over DPP: lanes combine the state DPP brings
+// from an earlier lane when it belongs to the same bucket (keys are
+// non-decreasing over the lanes, so equal keys mean one contiguous run).
+template <int CTRL, int RM, class M>
+DEV void seg_step_dpp(int key, M& st) {
+  const int k2 = dpp32<CTRL, RM>(INT32_MIN, key);
+  M o = st;
+  o.template dpp<CTRL, RM>();
+  if (k2 == key) st = M::combine(o, st);
+}
+template <class M>
+DEV void seg_scan_dpp(int key, M& st) {
+  seg_step_dpp<0x111, 0xF>(key, st);  // row_shr:1
+  seg_step_dpp<0x112, 0xF>(key, st);  // row_shr:2
+  seg_step_dpp<0x114, 0xF>(key, st);  // row_shr:4
+  seg_step_dpp<0x118, 0xF>(key, st);  // row_shr:8
+  seg_step_dpp<0x142, 0xA>(key, st);  // row_bcast:15 -> rows 1, 3
+  seg_step_dpp<0x143, 0xC>(key, st);  // row_bcast:31 -> rows 2, 3
+}
+DEV double readlane_d(double x, int l) {
+  const int64_t b = __builtin_bit_cast(int64_t, x);
+  const int32_t lo = __builtin_amdgcn_readlane((int32_t)(uint32_t)b, l);
+  const int32_t hi = __builtin_amdgcn_readlane((int32_t)(b >> 32), l);
+  return __builtin_bit_cast(double, (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+DEV int64_t readlane_l(int64_t b, int l) {
+  const int32_t lo = __builtin_amdgcn_readlane((int32_t)(uint32_t)b, l);
+  const int32_t hi = __builtin_amdgcn_readlane((int32_t)(b >> 32), l);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+template <class M, int K, int PF = 0, int NT = 0, int WAVES = 1, int ABL = 0,
+          int DPP = 0>
+__global__ __launch_bounds__(256, WAVES) void k_bucketize_k(Params P,
+                                                            BatchDev B,
+                                                            SeriesMeta SM,
+                                                            Rows R) {
   static_assert(K % 2 == 0, "K must be even (16-byte loads)");
   const int lane = LANE;
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -233,14 +360,21 @@ __global__ __launch_bounds__(256) void k_bucketize_k(Params P, BatchDev B,
   int carry_key = INT32_MIN;
   M carry = M::init();
   constexpr int PTS = 64 * K;
-  for (int64_t base = lo & ~(int64_t)1; base < hi; base += PTS) {
-    const int64_t i0 = base + (int64_t)K * lane;
-    int64_t t[K], v[K];
+  // K consecutive points of this lane: K/2 16-byte loads per column
+  auto load_step = [&](int64_t i0, int64_t* t, int64_t* v) {
     if (i0 + K <= hi) {
 #pragma unroll
       for (int j = 0; j < K; j += 2) {
-        const longlong2 tt = *reinterpret_cast<const longlong2*>(B.ts + i0 + j);
-        const longlong2 vv = *reinterpret_cast<const longlong2*>(B.val + i0 + j);
+        const ll2_t* pt = reinterpret_cast<const ll2_t*>(B.ts + i0 + j);
+        const ll2_t* pv = reinterpret_cast<const ll2_t*>(B.val + i0 + j);
+        ll2_t tt, vv;
+        if (NT) {
+          tt = __builtin_nontemporal_load(pt);
+          vv = __builtin_nontemporal_load(pv);
+        } else {
+          tt = *pt;
+          vv = *pv;
+        }
         t[j] = tt.x; t[j + 1] = tt.y;
         v[j] = vv.x; v[j + 1] = vv.y;
       }
@@ -251,38 +385,52 @@ __global__ __launch_bounds__(256) void k_bucketize_k(Params P, BatchDev B,
         v[j] = (i0 + j < hi) ? B.val[i0 + j] : 0;
       }
     }
-    // ---- lane-local sequential fold
+  };
+  int64_t tn[K], vn[K];
+  const int64_t base0 = lo & ~(int64_t)1;
+  if (PF) load_step(base0 + (int64_t)K * lane, tn, vn);
+  for (int64_t base = base0; base < hi; base += PTS) {
+    const int64_t i0 = base + (int64_t)K * lane;
+    int64_t t[K], v[K];
+    if (PF) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) { t[j] = tn[j]; v[j] = vn[j]; }
+      if (base + PTS < hi) load_step(i0 + PTS, tn, vn);
+    } else {
+      load_step(i0, t, v);
+    }
+    if (ABL == 1) {  // tuning ablation: stream only
+      int64_t x = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) x ^= t[j] + v[j];
+      if (x == 42) rows[0] = 1;
+      continue;
+    }
+    // ---- lane-local sequential fold (range checks only on the first and
+    // last step; no per-point type test for all-double series)
     int nseg = 0, cur_key = 0, head_key = 0;
     M cur = M::init(), head = M::init();
-    int64_t bnd = INT64_MIN;  // first timestamp past cur_key's bucket
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const int64_t i = i0 + j;
-      if (i < lo || i >= hi) continue;
-      int k = cur_key;
-      if (nseg == 0 || t[j] >= bnd) {
-        k = (int)bucket_of(P, t[j]);
-        bnd = P.run_all ? INT64_MAX : P.gbase + ((int64_t)k + 1) * P.interval;
+    if (base >= lo && base + PTS <= hi) {
+      const bool fonly = !B.is_float && sf;
+      bool done = false;
+      if (P.narrow) {
+        done = fonly ? fold_fast<M, K, true>(P, B, sf, i0, t, v, nseg, cur_key,
+                                             head_key, cur, head)
+                     : fold_fast<M, K, false>(P, B, sf, i0, t, v, nseg,
+                                              cur_key, head_key, cur, head);
       }
-      const double x = point_value(B, i, v[j], sf);
-      if (nseg == 0) {
-        cur_key = k;
-        cur = M::from(x);
-        nseg = 1;
-      } else if (k == cur_key) {
-        cur.push(x);
-      } else {
-        if (nseg == 1) {
-          head_key = cur_key;
-          head = cur;
-        } else {  // a bucket wholly inside this lane
-          rowv[cur_key] = cur.finish(&err);
-          rows[cur_key] = ST_REAL;
-        }
-        cur_key = k;
-        cur = M::from(x);
-        ++nseg;
+      if (!done) {
+        if (fonly)
+          fold_lane<M, K, true, false>(P, B, sf, i0, lo, hi, t, v, rowv, rows,
+                                       err, nseg, cur_key, head_key, cur, head);
+        else
+          fold_lane<M, K, false, false>(P, B, sf, i0, lo, hi, t, v, rowv, rows,
+                                        err, nseg, cur_key, head_key, cur,
+                                        head);
       }
+    } else {
+      fold_lane<M, K, false, true>(P, B, sf, i0, lo, hi, t, v, rowv, rows,
+                                   err, nseg, cur_key, head_key, cur, head);
     }
     if (nseg == 0) {  // lane wholly before lo (first step) or past hi
       cur_key = (i0 < lo) ? -1 : INT32_MAX;
@@ -303,17 +451,27 @@ __global__ __launch_bounds__(256) void k_bucketize_k(Params P, BatchDev B,
     // ---- segmented inclusive scan over the lanes' tail runs
     int key = cur_key;
     M st = cur;
+    int pkey, next_head;
+    M pst;
+    if (DPP) {
+      seg_scan_dpp(key, st);
+      pkey = dpp32<0x138, 0xF>(INT32_MIN, key);  // wave_shr:1
+      pst = st;
+      pst.template dpp<0x138, 0xF>();
+      next_head = dpp32<0x130, 0xF>(INT32_MIN, head_key);  // wave_shl:1
+    } else {
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int k2 = __shfl_up(key, d);
-      M o = st;
-      o.shfl_up(d);
-      if (lane >= d && k2 == key) st = M::combine(o, st);
+      for (int d = 1; d < 64; d <<= 1) {
+        const int k2 = __shfl_up(key, d);
+        M o = st;
+        o.shfl_up(d);
+        if (lane >= d && k2 == key) st = M::combine(o, st);
+      }
+      pkey = __shfl_up(key, 1);
+      pst = st;
+      pst.shfl_up(1);
+      next_head = __shfl_down(head_key, 1);
     }
-    const int pkey = __shfl_up(key, 1);
-    M pst = st;
-    pst.shfl_up(1);
-    const int next_head = __shfl_down(head_key, 1);
     if (nseg >= 2) {  // head run closes inside this lane
       const M full = (lane > 0 && pkey == head_key) ? M::combine(pst, head) : head;
       rowv[head_key] = full.finish(&err);
@@ -323,12 +481,20 @@ __global__ __launch_bounds__(256) void k_bucketize_k(Params P, BatchDev B,
       rowv[key] = st.finish(&err);
       rows[key] = ST_REAL;
     }
-    carry_key = __shfl(key, 63);
     Packed p = st.pack();
-    p.x = __shfl(p.x, 63);
-    p.y = __shfl(p.y, 63);
-    p.z = __shfl(p.z, 63);
-    p.w = __shfl(p.w, 63);
+    if (DPP) {
+      carry_key = __builtin_amdgcn_readlane(key, 63);
+      p.x = readlane_d(p.x, 63);
+      p.y = readlane_d(p.y, 63);
+      p.z = readlane_d(p.z, 63);
+      p.w = readlane_l(p.w, 63);
+    } else {
+      carry_key = __shfl(key, 63);
+      p.x = __shfl(p.x, 63);
+      p.y = __shfl(p.y, 63);
+      p.z = __shfl(p.z, 63);
+      p.w = __shfl(p.w, 63);
+    }
     carry = M::unpack(p);
   }
   if (lane == 0 && carry_key >= 0 && carry_key < P.nb) {

@@ -26,6 +26,33 @@ DEV bool is_nan(double v) { return v != v; }
 DEV bool is_inf(double v) { return v == __builtin_inf() || v == -__builtin_inf(); }
 DEV double qnan() { return __builtin_nan(""); }
 
+// DPP lane movers (VALU, no LDS round trip).  CTRL is a DPP control word
+// (row_shr:n = 0x110+n, row_bcast:15 = 0x142, row_bcast:31 = 0x143,
+// wave_shr:1 = 0x138, wave_shl:1 = 0x130); lanes whose source is invalid or
+// whose row is masked off keep their own value.
+template <int CTRL, int RM>
+DEV int32_t dpp32(int32_t x) {
+  return __builtin_amdgcn_update_dpp(x, x, CTRL, RM, 0xF, false);
+}
+template <int CTRL, int RM>
+DEV int32_t dpp32(int32_t old, int32_t x) {
+  return __builtin_amdgcn_update_dpp(old, x, CTRL, RM, 0xF, false);
+}
+template <int CTRL, int RM>
+DEV int64_t dpp64(int64_t x) {
+  const int32_t lo = dpp32<CTRL, RM>((int32_t)(uint32_t)x);
+  const int32_t hi = dpp32<CTRL, RM>((int32_t)(x >> 32));
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <int CTRL, int RM>
+DEV double dppd(double x) {
+  return __builtin_bit_cast(double, dpp64<CTRL, RM>(__builtin_bit_cast(int64_t, x)));
+}
+
+template <int CTRL, int RM> DEV double dppv(double x) { return dppd<CTRL, RM>(x); }
+template <int CTRL, int RM> DEV int64_t dppv(int64_t x) { return dpp64<CTRL, RM>(x); }
+template <int CTRL, int RM> DEV int32_t dppv(int32_t x) { return dpp32<CTRL, RM>(x); }
+
 struct Packed {
   double x, y, z;
   int64_t w;
@@ -37,7 +64,7 @@ struct Packed {
 template <int KIND>  // 0 sum, 1 avg, 2 squareSum, 3 count
 struct MSum {
   double s;
-  int64_t n;
+  int32_t n;
   DEV static MSum init() { return {0.0, 0}; }
   DEV static MSum from(double v) {
     if (is_nan(v)) return {0.0, 0};
@@ -49,6 +76,11 @@ struct MSum {
       ++n;
     }
   }
+  DEV void push_if(bool mk, double v) {  // branch free; s is never -0.0
+    const bool ok = mk & !is_nan(v);
+    s += ok ? (KIND == 2 ? v * v : v) : 0.0;
+    n += ok ? 1 : 0;
+  }
   DEV static MSum combine(const MSum& a, const MSum& b) {
     return {a.s + b.s, a.n + b.n};
   }
@@ -58,10 +90,15 @@ struct MSum {
     return KIND == 1 ? s / (double)(int32_t)n : s;
   }
   DEV Packed pack() const { return {s, 0.0, 0.0, n}; }
-  DEV static MSum unpack(const Packed& p) { return {p.x, p.w}; }
+  DEV static MSum unpack(const Packed& p) { return {p.x, (int32_t)p.w}; }
   DEV void shfl_up(int d) {
     s = __shfl_up(s, d);
     n = __shfl_up(n, d);
+  }
+  template <int CTRL, int RM>
+  DEV void dpp() {
+    s = dppv<CTRL, RM>(s);
+    n = dppv<CTRL, RM>(n);
   }
 };
 
@@ -77,6 +114,9 @@ struct MMinMax {
   DEV void push(double v) {
     if (!is_nan(v) && (MAX ? v > m : v < m)) m = v;
   }
+  DEV void push_if(bool mk, double v) {
+    m = (mk & (MAX ? v > m : v < m)) ? v : m;  // NaN compares false
+  }
   DEV static MMinMax combine(const MMinMax& a, const MMinMax& b) {
     return (MAX ? b.m > a.m : b.m < a.m) ? b : a;  // keeps the earliest
   }
@@ -86,6 +126,8 @@ struct MMinMax {
   DEV Packed pack() const { return {m, 0.0, 0.0, 0}; }
   DEV static MMinMax unpack(const Packed& p) { return {p.x}; }
   DEV void shfl_up(int d) { m = __shfl_up(m, d); }
+  template <int CTRL, int RM>
+  DEV void dpp() { m = dppv<CTRL, RM>(m); }
 };
 
 // ---------------------------------------------------------------- dev
@@ -93,7 +135,7 @@ struct MMinMax {
 // population sigma; Chan et al. merge for runs.
 struct MDev {
   double mean, m2;
-  int64_t n;
+  int32_t n;
   DEV static MDev init() { return {0.0, 0.0, 0}; }
   DEV static MDev from(double v) {
     if (is_nan(v)) return {0.0, 0.0, 0};
@@ -110,6 +152,9 @@ struct MDev {
     const double new_mean = mean + (x - mean) / (double)n;
     m2 += (x - mean) * (x - new_mean);
     mean = new_mean;
+  }
+  DEV void push_if(bool mk, double x) {
+    if (mk) push(x);
   }
   DEV static MDev combine(const MDev& a, const MDev& b) {
     if (a.n == 0) return b;
@@ -129,11 +174,17 @@ struct MDev {
     return __builtin_sqrt(m2 / (double)n);
   }
   DEV Packed pack() const { return {mean, m2, 0.0, n}; }
-  DEV static MDev unpack(const Packed& p) { return {p.x, p.y, p.w}; }
+  DEV static MDev unpack(const Packed& p) { return {p.x, p.y, (int32_t)p.w}; }
   DEV void shfl_up(int d) {
     mean = __shfl_up(mean, d);
     m2 = __shfl_up(m2, d);
     n = __shfl_up(n, d);
+  }
+  template <int CTRL, int RM>
+  DEV void dpp() {
+    mean = dppv<CTRL, RM>(mean);
+    m2 = dppv<CTRL, RM>(m2);
+    n = dppv<CTRL, RM>(n);
   }
 };
 
@@ -149,6 +200,9 @@ struct MFirstLast {
     if (LAST || !has) v = x;
     has = 1;
   }
+  DEV void push_if(bool mk, double x) {
+    if (mk) push(x);
+  }
   DEV static MFirstLast combine(const MFirstLast& a, const MFirstLast& b) {
     if (LAST) return b.has ? b : a;
     return a.has ? a : b;
@@ -159,6 +213,11 @@ struct MFirstLast {
   DEV void shfl_up(int d) {
     v = __shfl_up(v, d);
     has = __shfl_up(has, d);
+  }
+  template <int CTRL, int RM>
+  DEV void dpp() {
+    v = dppv<CTRL, RM>(v);
+    has = dppv<CTRL, RM>(has);
   }
 };
 
@@ -173,6 +232,9 @@ struct MMult {
     p = has ? p * x : x;
     has = 1;
   }
+  DEV void push_if(bool mk, double x) {
+    if (mk) push(x);
+  }
   DEV static MMult combine(const MMult& a, const MMult& b) {
     if (!a.has) return b;
     if (!b.has) return a;
@@ -184,6 +246,11 @@ struct MMult {
   DEV void shfl_up(int d) {
     p = __shfl_up(p, d);
     has = __shfl_up(has, d);
+  }
+  template <int CTRL, int RM>
+  DEV void dpp() {
+    p = dppv<CTRL, RM>(p);
+    has = dppv<CTRL, RM>(has);
   }
 };
 
@@ -203,6 +270,9 @@ struct MDiff {
     return r;
   }
   DEV void push(double x) { *this = combine(*this, from(x)); }
+  DEV void push_if(bool mk, double x) {
+    if (mk) push(x);
+  }
   DEV static MDiff combine(const MDiff& a, const MDiff& b) {
     if (!(a.flags & 1)) return b;
     if (!(b.flags & 1)) return a;
@@ -229,18 +299,27 @@ struct MDiff {
     last = __shfl_up(last, d);
     flags = __shfl_up(flags, d);
   }
+  template <int CTRL, int RM>
+  DEV void dpp() {
+    fnn = dppv<CTRL, RM>(fnn);
+    last = dppv<CTRL, RM>(last);
+    flags = dppv<CTRL, RM>(flags);
+  }
 };
 
 // ---------------------------------------------------------------- none
 // None.runDouble (:439-461): exactly one value, else IllegalDataException.
 struct MNone {
   double v;
-  int64_t n;
+  int32_t n;
   DEV static MNone init() { return {0.0, 0}; }
   DEV static MNone from(double x) { return {x, 1}; }
   DEV void push(double x) {
     if (n == 0) v = x;
     ++n;
+  }
+  DEV void push_if(bool mk, double x) {
+    if (mk) push(x);
   }
   DEV static MNone combine(const MNone& a, const MNone& b) {
     return {a.n ? a.v : b.v, a.n + b.n};
@@ -250,10 +329,15 @@ struct MNone {
     return v;
   }
   DEV Packed pack() const { return {v, 0.0, 0.0, n}; }
-  DEV static MNone unpack(const Packed& p) { return {p.x, p.w}; }
+  DEV static MNone unpack(const Packed& p) { return {p.x, (int32_t)p.w}; }
   DEV void shfl_up(int d) {
     v = __shfl_up(v, d);
     n = __shfl_up(n, d);
+  }
+  template <int CTRL, int RM>
+  DEV void dpp() {
+    v = dppv<CTRL, RM>(v);
+    n = dppv<CTRL, RM>(n);
   }
 };
 

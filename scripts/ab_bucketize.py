@@ -52,5 +52,7 @@ base = res[ks[0]]
 for k in ks[1:]:
     a0 = base.val[:int(base.offsets[-1])].view(torch.float64)
     b0 = res[k].val[:int(res[k].offsets[-1])].view(torch.float64)
-    out[k]["max_rel_diff_vs_k%d" % ks[0]] = float(((a0 - b0).abs() / a0.abs().clamp(min=1)).max())
+    if a0.numel() == b0.numel():
+        out[k]["max_rel_diff_vs_k%d" % ks[0]] = float(
+            ((a0 - b0).abs() / a0.abs().clamp(min=1)).max())
 print(json.dumps({"config": a.config, "series": n, "points": N, "variants": out}))
