@@ -8,6 +8,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_build", "libotsdb_agg.so")
+# tuning runs (scripts/ab_bucketize.py) point this at the variants build
+if os.environ.get("OTSDB_LIB"):
+    LIB_PATH = os.environ["OTSDB_LIB"]
 
 # otsdb_status
 OK = 0

@@ -17,10 +17,13 @@
 #include <type_traits>
 #include <vector>
 
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+
 #include "../../include/otsdb_agg.h"
 #include "kernels.hip"
 #include "select.hip"
 #include "decode.hip"
+#include "raw.hip"
 
 using namespace otsdb;
 
@@ -150,6 +153,8 @@ struct otsdb_ctx {
   int bucketize_k = 8;  // points per lane in k_bucketize (OTSDB_BUCKETIZE_K)
   void* dec_ws = nullptr;  // decode workspace
   size_t dec_ws_cap = 0;
+  void* ws2 = nullptr;     // raw group-by: candidates, sort, selection slab
+  size_t ws2_cap = 0;
 };
 
 namespace {
@@ -177,10 +182,14 @@ struct Plan {
 otsdb_status check_spec(const otsdb_query_spec* s) {
   if (s->agg_id < 0 || s->agg_id >= OTSDB_AGG_COUNT_IDS)
     return fail(OTSDB_E_NO_SUCH_ELEMENT, "No such aggregator: %d", s->agg_id);
+  if (s->interp < -1 || s->interp > OTSDB_INTERP_PREV)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "bad interpolation %d", s->interp);
   const bool ds = s->ds_interval_ms > 0 || s->run_all;
-  if (!ds)
-    return fail(OTSDB_E_UNSUPPORTED,
-                "raw (non-downsampled) group-by is not offloaded yet");
+  if (!ds) {  // raw group-by (raw.hip)
+    if (s->start_ms < 0)
+      return fail(OTSDB_E_ILLEGAL_ARGUMENT, "negative start");
+    return OTSDB_OK;
+  }
   if (s->ds_agg_id < 0 || s->ds_agg_id >= OTSDB_AGG_COUNT_IDS)
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "No such downsampling function");
   if (s->ds_agg_id == OTSDB_AGG_NONE)
@@ -217,6 +226,11 @@ otsdb_status make_params(const otsdb_query_spec* s, Params* P) {
   P->interp = s->interp >= 0 ? s->interp : kAggs[s->agg_id].interp;
   P->fill_value = (P->fill == OTSDB_FILL_ZERO) ? 0.0 : NAN;
   P->pct = s->agg_id >= OTSDB_AGG_P999 ? pct_of(s->agg_id) : 0.0;
+  P->pct_est = s->agg_id < OTSDB_AGG_P999   ? 0
+               : s->agg_id < OTSDB_AGG_EP999R3 ? 0
+               : s->agg_id < OTSDB_AGG_EP999R7 ? 3
+                                               : 7;
+  if (!(s->ds_interval_ms > 0 || s->run_all)) return OTSDB_OK;  // raw
   P->rate_origin_ts = 0;
   P->rate_origin_val = 0.0;
   if (s->run_all) {
@@ -707,6 +721,11 @@ otsdb_status finish(otsdb_ctx* c, int64_t G, otsdb_result* out) {
                 "previous one");
   if (err & ERR_INFINITY)
     return fail(OTSDB_E_ILLEGAL_STATE, "Got Infinity");
+  if (err & ERR_RAW_DUP)
+    return fail(OTSDB_E_UNSUPPORTED,
+                "timestamps do not increase inside a span (raw group-by)");
+  if (err & ERR_X1_MASK)
+    return fail(OTSDB_E_ILLEGAL_STATE, "x1 beyond the millisecond mask");
   if (err & ERR_SEL_TOO_BIG)
     return fail(OTSDB_E_UNSUPPORTED,
                 "percentile/median over groups of more than %d series is not "
@@ -736,6 +755,155 @@ otsdb_status read_goff(otsdb_ctx* c, const otsdb_batch* b, bool device,
   return OTSDB_OK;
 }
 
+// Raw (non-downsampled) group-by, raw.hip.  Device pointers throughout.
+otsdb_status run_raw(otsdb_ctx* c, const otsdb_query_spec* spec,
+                     const otsdb_batch* b, const BatchDev& B,
+                     const std::vector<int64_t>& goff, const Params& P,
+                     otsdb_result* out) {
+  hipStream_t st = c->stream;
+  const int64_t S = B.S, N = b->n_points;
+  const int64_t G = (int64_t)goff.size() - 1, M = goff.back();
+  const bool rate = P.rate != 0;
+  int64_t kmax = 0;
+  for (int64_t g = 0; g < G; ++g) kmax = std::max(kmax, goff[g + 1] - goff[g]);
+  // ---- phase 1 workspace: per series / member / group
+  int64_t *lo, *hi, *rts = nullptr, *rval = nullptr, *ccount, *coff, *segb,
+      *sege, *counts;
+  auto carve1 = [&](char* base) {
+    Carve cv{base};
+    lo = cv.take<int64_t>(S + 1);
+    hi = cv.take<int64_t>(S + 1);
+    if (rate) {
+      rts = cv.take<int64_t>(N + 1);
+      rval = cv.take<int64_t>(N + 1);
+    }
+    ccount = cv.take<int64_t>(M + 1);
+    coff = cv.take<int64_t>(M + 1);
+    segb = cv.take<int64_t>(G + 1);
+    sege = cv.take<int64_t>(G + 1);
+    counts = cv.take<int64_t>(G + 1);
+    return cv.off + 256;
+  };
+  otsdb_status rc = ensure(&c->ws, &c->ws_cap, carve1(nullptr));
+  if (rc) return rc;
+  carve1((char*)c->ws);
+  HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), st));
+  if (G == 0) {
+    HIP_TRY(hipMemsetAsync(out->offsets, 0, sizeof(int64_t), st));
+    return finish(c, G, out);
+  }
+  if (S > 0) {
+    hipLaunchKernelGGL(k_raw_prep, dim3(blocks_for(S, 256)), dim3(256), 0, st,
+                       P, B, lo, hi);
+    if (rate)
+      hipLaunchKernelGGL(k_raw_rate, dim3(blocks_for(S, 4)), dim3(256), 0, st,
+                         P, B, lo, hi, rts, rval, c->d_err);
+  }
+  RawView V;
+  V.ts = rate ? rts : B.ts;
+  V.val = rate ? rval : B.val;
+  V.is_float = rate ? nullptr : B.is_float;
+  V.series_float = rate ? nullptr : B.series_float;
+  V.all_double = rate || (!B.is_float && !B.series_float);
+  V.lo = lo;
+  V.hi = hi;
+  const int mixed = !V.all_double;
+  HIP_TRY(hipMemsetAsync(coff, 0, sizeof(int64_t) * (M + 1), st));
+  if (M > 0) {
+    hipLaunchKernelGGL(k_raw_cand_count, dim3(blocks_for(M, 256)), dim3(256), 0,
+                       st, P, V, M, b->group_members, ccount);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, M,
+                       (const int64_t*)ccount, coff);
+  }
+  HIP_TRY(hipMemcpyAsync(&c->h_small[2], coff + M, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const int64_t C = c->h_small[2];
+  if (C >= (int64_t(1) << 32))
+    return fail(OTSDB_E_UNSUPPORTED, "raw group-by over %lld candidate points",
+                (long long)C);
+  // ---- phase 2 workspace: candidates, sort temp, emitted-point groups
+  const int end_bit = std::max(1, 64 - __builtin_clzll((uint64_t)std::max<int64_t>(spec->end_ms, 1)));
+  size_t sort_tmp = 0;
+  if (C > 0)
+    HIP_TRY(rocprim::segmented_radix_sort_keys(
+        nullptr, sort_tmp, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+        (unsigned)C, (unsigned)G, segb, sege, 0, end_bit, st));
+  uint64_t *kin, *kout;
+  void* tmp;
+  int32_t* ugrp;
+  auto carve2 = [&](char* base) {
+    Carve cv{base};
+    kin = cv.take<uint64_t>(C + 1);
+    kout = cv.take<uint64_t>(C + 1);
+    ugrp = cv.take<int32_t>(C + 1);
+    tmp = cv.take<char>(sort_tmp + 1);
+    return cv.off + 256;
+  };
+  rc = ensure(&c->ws2, &c->ws2_cap, carve2(nullptr));
+  if (rc) return rc;
+  carve2((char*)c->ws2);
+  if (M > 0)
+    hipLaunchKernelGGL(k_raw_cand_fill, dim3(blocks_for(M, 4)), dim3(256), 0,
+                       st, P, V, M, b->group_members, (const int64_t*)coff, kin,
+                       c->d_err);
+  hipLaunchKernelGGL(k_raw_segments, dim3(blocks_for(G, 256)), dim3(256), 0, st,
+                     G, b->group_offsets, (const int64_t*)coff, segb, sege);
+  if (C > 0)
+    HIP_TRY(rocprim::segmented_radix_sort_keys(
+        tmp, sort_tmp, (const uint64_t*)kin, kout, (unsigned)C, (unsigned)G,
+        segb, sege, 0, end_bit, st));
+  hipLaunchKernelGGL(k_raw_unique, dim3(blocks_for(G, 4)), dim3(256), 0, st, G,
+                     (const int64_t*)segb, (const int64_t*)sege,
+                     (const uint64_t*)kout, counts, (const int64_t*)nullptr,
+                     (int64_t)0, (int64_t*)nullptr, (int32_t*)nullptr, 0);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, G,
+                     (const int64_t*)counts, out->offsets);
+  hipLaunchKernelGGL(k_raw_unique, dim3(blocks_for(G, 4)), dim3(256), 0, st, G,
+                     (const int64_t*)segb, (const int64_t*)sege,
+                     (const uint64_t*)kout, counts,
+                     (const int64_t*)out->offsets, out->capacity, out->ts, ugrp,
+                     1);
+  HIP_TRY(hipMemcpyAsync(&c->h_small[2], out->offsets + G, 8,
+                         hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const int64_t n_out = std::min<int64_t>(c->h_small[2], out->capacity);
+  if (n_out > 0) {
+    if (is_selection(spec->agg_id)) {
+      const int median = spec->agg_id == OTSDB_AGG_MEDIAN ? 1 : 0;
+      // keys slab: one kmax-key row per block, at most 64 Mi keys per launch
+      const int64_t per = std::max<int64_t>(
+          1, std::min<int64_t>(n_out, ((int64_t)1 << 26) / std::max<int64_t>(kmax, 1)));
+      void* p = c->dec_ws;
+      size_t cap = c->dec_ws_cap;
+      rc = ensure(&p, &cap, (size_t)(per * std::max<int64_t>(kmax, 1)) * 8);
+      c->dec_ws = p;
+      c->dec_ws_cap = cap;
+      if (rc) return rc;
+      for (int64_t u0 = 0; u0 < n_out; u0 += per) {
+        const int64_t nb = std::min(per, n_out - u0);
+        hipLaunchKernelGGL(k_raw_select, dim3((unsigned)nb), dim3(64), 0, st, P,
+                           V, median, u0, n_out, b->group_offsets,
+                           b->group_members, (const int32_t*)ugrp,
+                           (const int64_t*)out->ts, out->val, out->is_int,
+                           (uint64_t*)c->dec_ws, std::max<int64_t>(kmax, 1),
+                           c->d_err);
+      }
+    } else {
+      const bool ok = with_monoid(spec->agg_id, [&](auto tag) {
+        using Mo = decltype(tag);
+        hipLaunchKernelGGL(k_raw_eval<Mo>, dim3(blocks_for(n_out, 256)),
+                           dim3(256), 0, st, P, V, (int)spec->agg_id, mixed,
+                           n_out, b->group_offsets, b->group_members,
+                           (const int32_t*)ugrp, (const int64_t*)out->ts,
+                           out->val, out->is_int, c->d_err);
+      });
+      if (!ok) return fail(OTSDB_E_NO_SUCH_ELEMENT, "aggregator %d", spec->agg_id);
+    }
+  }
+  HIP_TRY(hipGetLastError());
+  return finish(c, G, out);
+}
+
 otsdb_status run_device_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
                              const otsdb_batch* b, otsdb_result* out,
                              std::vector<int64_t>& goff) {
@@ -749,6 +917,8 @@ otsdb_status run_device_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
                 "ts_ms/val must be 16-byte aligned (16-B streaming loads)");
   BatchDev B{b->n_series, b->offsets, b->ts_ms, b->val, b->is_float,
              b->series_float};
+  if (!(spec->ds_interval_ms > 0 || spec->run_all))
+    return run_raw(c, spec, b, B, goff, P, out);
   Work W;
   rc = run_pipeline(c, spec, B, b->group_members, goff, P, W, 0, nullptr,
                     nullptr);
@@ -796,6 +966,7 @@ void otsdb_ctx_destroy(otsdb_ctx* c) {
   if (c->ws) hipFree(c->ws);
   if (c->stage) hipFree(c->stage);
   if (c->dec_ws) hipFree(c->dec_ws);
+  if (c->ws2) hipFree(c->ws2);
   if (c->d_tiles) hipFree(c->d_tiles);
   if (c->d_err) hipFree(c->d_err);
   for (auto e : c->ev_pool) hipEventDestroy(e);
@@ -832,6 +1003,14 @@ otsdb_status otsdb_agg_plan(otsdb_ctx* c, const otsdb_query_spec* spec,
   Params P;
   rc = make_params(spec, &P);
   if (rc) return rc;
+  if (!(spec->ds_interval_ms > 0 || spec->run_all)) {
+    // raw: every emitted timestamp is a point of some member span, so the
+    // batch's point count bounds the output when each span is in one group
+    out->n_buckets = 0;
+    out->max_out_points = b->n_points;
+    out->workspace_bytes = b->n_series * 16 + b->n_points * (spec->rate ? 48 : 32);
+    return OTSDB_OK;
+  }
   out->n_buckets = P.nb;
   out->max_out_points = b->n_groups * P.nb;
   out->workspace_bytes =
@@ -948,6 +1127,9 @@ otsdb_status otsdb_agg_partials_device(otsdb_ctx* c,
   Params P;
   if (!rc) rc = check_spec(spec);
   if (!rc) rc = make_params(spec, &P);
+  if (!rc && !(spec->ds_interval_ms > 0 || spec->run_all))
+    rc = fail(OTSDB_E_UNSUPPORTED,
+              "raw group-by across ranks (union timestamps need an all-gather)");
   if (!rc && !P.run_all && !P.fill && (double)b->n_series * (double)P.nb > 4.0e9)
     rc = fail(OTSDB_E_UNSUPPORTED, "grid trimming is not supported across ranks");
   if (!rc) {

@@ -37,6 +37,9 @@ enum : int {
   ERR_INFINITY = 2,     // "Got Infinity"       -> E_ILLEGAL_STATE
   ERR_RATE_TS = 4,      // non-increasing ts    -> E_ILLEGAL_STATE
   ERR_SEL_TOO_BIG = 8,  // percentile group over the select limit
+  ERR_X1_MASK = 16,     // interpolation toward x1 >= 2^44 ms (AssertionError
+                        // in AggregationIterator.java:706-708, :776-778)
+  ERR_RAW_DUP = 32,     // timestamps not increasing inside a raw span
 };
 
 struct Params {
@@ -57,6 +60,9 @@ struct Params {
   int32_t run_all, fill, rate, counter, drop_resets, interp;
   int32_t narrow;        // grid spans < 2^32 ms and interval < 2^31 ms
   double pct;            // percentile / 100.0 (PercentileAgg)
+  int32_t pct_est;       // estimation type honoured by runLong: 0 LEGACY,
+                         // 3 R_3, 7 R_7 (Aggregators.java:676-685)
+  int32_t _pad;
 };
 
 struct BatchDev {

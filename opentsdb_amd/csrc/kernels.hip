@@ -229,41 +229,39 @@ DEV int bucket_narrow(const Params& P, int64_t ts) {
   return (int)q;
 }
 
-// Fast lane fold for lanes whose K points fall into at most two buckets
-// (the common case when buckets hold more than K points): both runs are
-// accumulated branch free with masked pushes, in point order.  Returns false
-// (nothing changed) when the lane spans three or more buckets.
+// Fast lane fold for lanes whose K points fall into at most two adjacent
+// buckets (the common case when buckets hold more than K points).  Points are
+// sorted by time, so only the first and last point need a bucket index: the
+// lane spans buckets k0..k1, and with k1 <= k0 + 1 every point before the
+// start of bucket k1 belongs to k0 (a prefix, the head run) and the rest to
+// k1.  Both runs accumulate branch free with masked pushes, in point order.
+// Returns false (nothing changed) when the lane spans three or more buckets.
 template <class M, int K, bool FLOATONLY>
 DEV bool fold_fast(const Params& P, const BatchDev& B, int sf, int64_t i0,
                    const int64_t* t, const int64_t* v, int& nseg, int& cur_key,
                    int& head_key, M& cur, M& head) {
-  int k[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j) k[j] = bucket_narrow(P, t[j]);
-  const int k0 = k[0], k1 = k[K - 1];
-  bool ok = true;
-#pragma unroll
-  for (int j = 1; j < K - 1; ++j) ok &= (k[j] == k0) | (k[j] == k1);
-  if (!ok) return false;
+  const int k0 = bucket_narrow(P, t[0]), k1 = bucket_narrow(P, t[K - 1]);
+  if (k1 - k0 > 1) return false;
+  // start of bucket k1; INT64_MIN sends every point to the one run
+  const int64_t bnd =
+      (k1 == k0) ? INT64_MIN : P.gbase + (int64_t)k1 * P.interval;
   M h = M::init(), c = M::init();
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const double x =
         FLOATONLY ? bits_to_double(v[j]) : point_value(B, i0 + j, v[j], sf);
-    const bool inh = k[j] == k0;
+    const bool inh = t[j] < bnd;
     h.push_if(inh, x);
     c.push_if(!inh, x);
   }
   head_key = k0;
+  cur_key = k1;
+  cur = c;
   if (k0 == k1) {
     nseg = 1;
-    cur_key = k0;
-    cur = h;
   } else {
     nseg = 2;
-    cur_key = k1;
     head = h;
-    cur = c;
   }
   return true;
 }

@@ -93,10 +93,6 @@ def check(engine, spec, batch, exact, scale=1.0, where=""):
 def test_reference_kat(engine, c):
     spec = kat.spec_from_case(c["spec"])
     batch = kat.batch_from_case(c)
-    if not c["spec"].get("ds_interval_ms"):
-        with pytest.raises(core.UnsupportedOperationException):
-            engine.run(spec, batch)
-        pytest.skip("raw group-by not offloaded yet (SURVEY §8f rank 2)")
     got = engine.run(spec, batch)
     for g, exp in enumerate(c["expect"]):
         pts = np.zeros(len(got[g].ts), pyoracle.POINT)
@@ -252,6 +248,78 @@ def test_empty_and_degenerate(engine):
     spec = _spec("sum", "avg", start=datasets.T0 - 10 * 3600 * 1000,
                  end=datasets.T0 - 9 * 3600 * 1000)
     check(engine, spec, b, True, where="before")
+
+
+# ------------------------------------------------- raw (no downsampling)
+def _raw(agg, start=None, end=None, rate=False, ro=None, interp=None):
+    s0 = datasets.T0 if start is None else start
+    e0 = datasets.T0 + 3 * 3600 * 1000 if end is None else end
+    return core.make_spec(s0, e0, core.Aggregators.get(agg), None, s0, e0,
+                          rate, ro, interp)
+
+
+RAW_AGGS = AGGS + ["none"]
+
+
+@pytest.mark.parametrize("kind", ["float", "int", "mixed", "nan"])
+@pytest.mark.parametrize("agg", RAW_AGGS)
+def test_raw_group_by(engine, agg, kind):
+    """AggregationIterator over the spans' own points: union emission,
+    contribution window, isInteger over current+next slots, runLong with
+    Java long arithmetic — sequential in span order, so bit-exact."""
+    b = datasets.random_batch(101, n_series=24, n_groups=4,
+                              value_kind="float" if kind == "nan" else kind,
+                              nan_frac=0.05 if kind == "nan" else 0.0,
+                              cadence_ms=37000)
+    check(engine, _raw(agg), b, True, where="raw/%s/%s" % (agg, kind))
+
+
+@pytest.mark.parametrize("interp", list(core.Interpolation))
+def test_raw_interpolation(engine, interp):
+    for kind in ("float", "int"):
+        b = datasets.random_batch(103, n_series=20, n_groups=3,
+                                  value_kind=kind, cadence_ms=23000)
+        for agg in ("sum", "max", "avg"):
+            check(engine, _raw(agg, interp=interp), b, True,
+                  where="raw/%s/%s/%s" % (interp.name, agg, kind))
+
+
+@pytest.mark.parametrize("ri", range(len(RATES)))
+def test_raw_rate(engine, ri):
+    b = datasets.random_batch(107 + ri, n_series=20, n_groups=3, counter=True,
+                              cadence_ms=31000)
+    for agg in ("sum", "avg", "max", "count", "p95", "median"):
+        for start in (datasets.T0, datasets.T0 + 61000):
+            spec = _raw(agg, start=start, rate=True, ro=RATES[ri])
+            check(engine, spec, b, True, where="rawrate%d/%s" % (ri, agg))
+
+
+def test_raw_windows_and_big_groups(engine):
+    """Unaligned / narrow windows, spans outside the window, and groups of
+    hundreds of spans (the selection path with > 64 contributions)."""
+    b = datasets.random_batch(109, n_series=12, n_groups=3, cadence_ms=13000)
+    for s, e in ((datasets.T0 + 12345, datasets.T0 + 2 * 3600 * 1000 + 999),
+                 (datasets.T0 + 3600 * 1000, datasets.T0 + 3600 * 1000),
+                 (datasets.T0 - 10 * 3600 * 1000, datasets.T0 - 9 * 3600 * 1000)):
+        for agg in ("sum", "last", "p99", "dev"):
+            check(engine, _raw(agg, s, e), b, True, where="rawwin/%s" % agg)
+    b = datasets.random_batch(111, n_series=300, big_group=True,
+                              span_ms=1800 * 1000, cadence_ms=60000,
+                              value_kind="mixed")
+    for agg in ("sum", "avg", "median", "p50", "p999", "ep95r3", "ep75r7",
+                "count", "mimmax"):
+        check(engine, _raw(agg, end=datasets.T0 + 1800 * 1000), b, True,
+              where="rawbig/" + agg)
+
+
+def test_raw_duplicate_timestamps_unsupported(engine):
+    from opentsdb_amd.batch import HostBatch
+    t = datasets.T0
+    groups = [[[(t, 1, 0), (t + 1000, 2, 0), (t + 1000, 3, 0)],
+               [(t, 5, 0), (t + 2000, 6, 0)]]]
+    b = HostBatch.from_groups(groups)
+    with pytest.raises(core.UnsupportedOperationException):
+        engine.run(_raw("sum", end=t + 5000), b)
 
 
 # ------------------------------------------------------------ generator
