@@ -195,9 +195,6 @@ otsdb_status check_spec(const otsdb_query_spec* s) {
   if (s->ds_agg_id == OTSDB_AGG_NONE)
     return fail(OTSDB_E_ILLEGAL_ARGUMENT,
                 "cannot use the NONE aggregator for downsampling");
-  if (is_selection(s->ds_agg_id))
-    return fail(OTSDB_E_UNSUPPORTED,
-                "percentile/median downsampling is not offloaded yet");
   if (s->use_calendar)
     return fail(OTSDB_E_UNSUPPORTED, "calendar downsampling");
   if (s->fill == OTSDB_FILL_SCALAR)
@@ -231,6 +228,10 @@ otsdb_status make_params(const otsdb_query_spec* s, Params* P) {
                : s->agg_id < OTSDB_AGG_EP999R7 ? 3
                                                : 7;
   if (!(s->ds_interval_ms > 0 || s->run_all)) return OTSDB_OK;  // raw
+  if (is_selection(s->ds_agg_id)) {
+    P->ds_sel = s->ds_agg_id == OTSDB_AGG_MEDIAN ? 1 : 2;
+    P->ds_pct = s->ds_agg_id >= OTSDB_AGG_P999 ? pct_of(s->ds_agg_id) : 0.0;
+  }
   P->rate_origin_ts = 0;
   P->rate_origin_val = 0.0;
   if (s->run_all) {
@@ -503,7 +504,17 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     HIP_TRY(hipMemsetAsync(W.R.state, 0, (size_t)S * NB, st));
 
   bool ok = true;
-  if (S > 0 && NB > 0) {
+  if (S > 0 && NB > 0 && P.ds_sel) {
+    // median / percentile downsampling: per-bucket selection
+    {
+      StageTimer tm(c, 3);
+      hipLaunchKernelGGL(k_prep<MSum<3>>, dim3(blocks_for(S, 256)), dim3(256),
+                         0, st, P, B, W.SM);
+    }
+    StageTimer tm(c, 0);
+    hipLaunchKernelGGL(k_ds_select, dim3((unsigned)S), dim3(64), 0, st, P, B,
+                       W.SM, W.R);
+  } else if (S > 0 && NB > 0) {
     ok = with_monoid(spec->ds_agg_id, [&](auto tag) {
       using M = decltype(tag);
       {
@@ -593,11 +604,11 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       }
     });
     if (!ok) return fail(OTSDB_E_UNSUPPORTED, "downsampler %d", spec->ds_agg_id);
+  }
+  if (S > 0 && NB > 0) {
     StageTimer tm(c, 1);
     hipLaunchKernelGGL(k_transform, dim3(blocks_for(S, 4)), dim3(256), 0, st,
                        P, S, W.SM, W.R, c->d_err);
-  } else if (S > 0) {
-    // still need the span filter for nothing: no buckets -> no output
   }
   if (G > 0 && NB > 0) {
     StageTimer tm(c, 2);

@@ -62,7 +62,9 @@ struct Params {
   double pct;            // percentile / 100.0 (PercentileAgg)
   int32_t pct_est;       // estimation type honoured by runLong: 0 LEGACY,
                          // 3 R_3, 7 R_7 (Aggregators.java:676-685)
-  int32_t _pad;
+  int32_t ds_sel;        // downsampling function: 0 monoid, 1 median,
+                         // 2 percentile (k_ds_select)
+  double ds_pct;         // its percentile / 100.0
 };
 
 struct BatchDev {

@@ -452,59 +452,6 @@ DEV double raw_key_double(uint64_t k) {
 }
 DEV uint64_t raw_lkey(int64_t v) { return (uint64_t)v ^ 0x8000000000000000ULL; }
 
-// r-th smallest (0-based) of keys[0, n) by one wavefront: 8 MSB passes of
-// 8 bits, LDS histogram per pass.  Block = one wavefront.
-DEV uint64_t wave_select(const uint64_t* keys, int64_t n, int64_t r,
-                         uint32_t* hist) {
-  const int lane = LANE;
-  uint64_t prefix = 0, mask = 0;
-  for (int shift = 56; shift >= 0; shift -= 8) {
-    for (int j = lane; j < 256; j += 64) hist[j] = 0;
-    __syncthreads();
-    for (int64_t i = lane; i < n; i += 64) {
-      const uint64_t k = keys[i];
-      if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1u);
-    }
-    __syncthreads();
-    uint32_t c[4];
-    uint32_t sum = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      c[j] = hist[4 * lane + j];
-      sum += c[j];
-    }
-    uint32_t incl = sum;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(incl, d);
-      if (lane >= d) incl += y;
-    }
-    const int64_t excl = (int64_t)incl - sum;
-    const bool mine = r >= excl && r < (int64_t)incl;
-    int digit = 0;
-    int64_t rem = 0;
-    if (mine) {
-      int64_t cum = excl;
-      int j = 0;
-      for (; j < 3; ++j) {
-        if (r < cum + c[j]) break;
-        cum += c[j];
-      }
-      digit = 4 * lane + j;
-      rem = r - cum;
-    }
-    const uint64_t who = __ballot(mine);
-    const int src = who ? __builtin_ctzll(who) : 0;
-    digit = __shfl(digit, src);
-    rem = __shfl(rem, src);
-    r = rem;
-    prefix |= (uint64_t)digit << shift;
-    mask |= (uint64_t)0xFF << shift;
-    __syncthreads();
-  }
-  return prefix;
-}
-
 // commons-math3 3.4.1 Percentile position for estimation `est`
 // (0 LEGACY, 3 R_3, 7 R_7), SURVEY §8a a11
 DEV double pct_position(double p, int64_t n, int est) {
@@ -586,8 +533,9 @@ __global__ __launch_bounds__(64) void k_raw_select(
   }
   uint64_t k0 = 0, k1 = 0;
   if (!empty) {
-    k0 = wave_select(keys, n, r0, hist);
-    k1 = (r1 == r0) ? k0 : wave_select(keys, n, r1, hist);
+    auto key_at = [&](int64_t i) { return keys[i]; };
+    k0 = wave_select(n, r0, hist, key_at);
+    k1 = (r1 == r0) ? k0 : wave_select(n, r1, hist, key_at);
   }
   if (lane != 0) return;
   int64_t bits;

@@ -217,4 +217,215 @@ __global__ void k_sel_finish(int64_t nb, int64_t n_lg,
   out_val[o] = r;
 }
 
+// ------------------------------------------------------------------------
+// r-th smallest (0-based) of n keys, key_at(i) for i in [0, n), by one
+// wavefront (the block must be exactly one wavefront: the LDS histogram is
+// fenced with __syncthreads): 8 MSB passes of 8 bits.
+// ------------------------------------------------------------------------
+template <class F>
+DEV uint64_t wave_select(int64_t n, int64_t r, uint32_t* hist, F key_at) {
+  const int lane = LANE;
+  uint64_t prefix = 0, mask = 0;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int j = lane; j < 256; j += 64) hist[j] = 0;
+    __syncthreads();
+    for (int64_t i = lane; i < n; i += 64) {
+      const uint64_t k = key_at(i);
+      if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255], 1u);
+    }
+    __syncthreads();
+    uint32_t c[4];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      c[j] = hist[4 * lane + j];
+      sum += c[j];
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d);
+      if (lane >= d) incl += y;
+    }
+    const int64_t excl = (int64_t)incl - sum;
+    const bool mine = r >= excl && r < (int64_t)incl;
+    int digit = 0;
+    int64_t rem = 0;
+    if (mine) {
+      int64_t cum = excl;
+      int j = 0;
+      for (; j < 3; ++j) {
+        if (r < cum + c[j]) break;
+        cum += c[j];
+      }
+      digit = 4 * lane + j;
+      rem = r - cum;
+    }
+    const uint64_t who = __ballot(mine);
+    const int src = who ? __builtin_ctzll(who) : 0;
+    digit = __shfl(digit, src);
+    rem = __shfl(rem, src);
+    r = rem;
+    prefix |= (uint64_t)digit << shift;
+    mask |= (uint64_t)0xFF << shift;
+    __syncthreads();
+  }
+  return prefix;
+}
+
+// Median.runDouble (Aggregators.java:412-431) / PercentileAgg.runDouble
+// (:687-706, LEGACY whatever the name) over n non-NaN values given as the
+// one or two order statistics the estimator reads.
+DEV void sel_ranks(int median, double p, int64_t n, int64_t* r0, int64_t* r1,
+                   double* pos) {
+  *r0 = *r1 = 0;
+  *pos = 0.0;
+  if (n <= 0) return;
+  if (median) {
+    *r0 = *r1 = n / 2;
+  } else if (n > 1) {
+    *pos = p * (double)(n + 1);
+    if (*pos < 1) {
+      *r0 = *r1 = 0;
+    } else if (*pos >= (double)n) {
+      *r0 = *r1 = n - 1;
+    } else {
+      const int64_t ip = (int64_t)__builtin_floor(*pos);
+      *r0 = ip - 1;
+      *r1 = ip;
+    }
+  }
+}
+DEV double sel_value(int median, int64_t n, double pos, double lo, double hi) {
+  if (n <= 0) return qnan();
+  if (median || n == 1) return lo;
+  if (pos >= 1 && pos < (double)n) return lo + (pos - __builtin_floor(pos)) * (hi - lo);
+  return lo;
+}
+
+// ------------------------------------------------------------------------
+// k_ds_select: median / percentile DOWNSAMPLING (Downsampler.java:162-228:
+// function.runDouble over the values of each interval).  One wavefront per
+// series (block = 64); lanes take consecutive buckets, find each bucket's
+// points by binary search, and select over the non-NaN values: buckets of
+// up to DS_SMALL values by an insertion sort in LDS, larger ones by a
+// wave-wide radix select.  Bucket index nb stands for the first bucket past
+// the window (k_prep's of_val).
+// ------------------------------------------------------------------------
+constexpr int DS_SMALL = 16;
+
+__global__ __launch_bounds__(64) void k_ds_select(Params P, BatchDev B,
+                                                  SeriesMeta SM, Rows R) {
+  __shared__ uint64_t sk[DS_SMALL][64];
+  __shared__ uint32_t hist[256];
+  const int lane = LANE;
+  const int64_t s = blockIdx.x;
+  if (s >= B.S || !SM.keep[s]) return;
+  const int64_t lo = SM.lo[s], hi = SM.hi[s], p1 = B.offsets[s + 1];
+  const int sf = B.series_float ? (int)B.series_float[s] : 1;
+  const int median = P.ds_sel == 1;
+  const double p = P.ds_pct;
+  double* rowv = R.val + s * P.nb;
+  uint8_t* rows = R.state + s * P.nb;
+  auto value = [&](int64_t i) {
+    const int64_t b = B.val[i];
+    const int f = B.is_float ? (int)B.is_float[i] : sf;
+    return f ? __longlong_as_double(b) : (double)b;
+  };
+  // buckets that can hold points: [b_first, b_last] (+ nb for of_val)
+  int64_t b_first = 0, b_last = -1;
+  if (lo < hi) {
+    b_first = P.run_all ? 0 : (B.ts[lo] - P.gbase) / P.interval;
+    b_last = P.run_all ? 0 : (B.ts[hi - 1] - P.gbase) / P.interval;
+  }
+  const bool of = SM.of_has[s] != 0;
+  const int64_t n_b = (b_last - b_first + 1) + (of ? 1 : 0);
+  for (int64_t c0 = 0; c0 < n_b; c0 += 64) {
+    const int64_t j = c0 + lane;
+    const bool act = j < n_b;
+    const bool is_of = act && of && j == n_b - 1;
+    const int64_t b = is_of ? P.nb : b_first + j;
+    int64_t a = 0, e = 0;
+    if (act) {
+      if (is_of) {
+        a = hi;
+        e = lower_bound(B.ts, hi, p1, SM.of_ts[s] + P.interval);
+      } else if (P.run_all) {
+        a = lo;
+        e = hi;
+      } else {
+        const int64_t t0 = P.gbase + b * P.interval;
+        a = lower_bound(B.ts, lo, hi, t0);
+        e = lower_bound(B.ts, a, hi, t0 + P.interval);
+      }
+    }
+    const int64_t cnt = e - a;
+    // small buckets: per-lane insertion sort of the non-NaN keys
+    int n = 0;
+    const bool small = cnt <= DS_SMALL;
+    if (act && cnt > 0 && small) {
+      for (int64_t i = a; i < e; ++i) {
+        const double v = value(i);
+        if (is_nan(v)) continue;
+        const uint64_t k = dkey(v);
+        int q = n++;
+        while (q > 0 && sk[q - 1][lane] > k) {
+          sk[q][lane] = sk[q - 1][lane];
+          --q;
+        }
+        sk[q][lane] = k;
+      }
+      int64_t r0, r1;
+      double pos;
+      sel_ranks(median, p, n, &r0, &r1, &pos);
+      const double v = n ? sel_value(median, n, pos, key_value(sk[r0][lane]),
+                                     key_value(sk[r1][lane]))
+                         : qnan();
+      if (is_of) {
+        SM.of_val[s] = v;
+      } else {
+        rowv[b] = v;
+        rows[b] = ST_REAL;
+      }
+    }
+    // large buckets: the whole wave selects, one bucket at a time
+    uint64_t big = __ballot(act && cnt > DS_SMALL);
+    while (big) {
+      const int l = __builtin_ctzll(big);
+      big &= big - 1;
+      const int64_t la = __shfl(a, l), le = __shfl(e, l);
+      const int64_t lb = __shfl(b, l);
+      const bool lof = __shfl((int)is_of, l) != 0;
+      // non-NaN count
+      int64_t nn = 0;
+      for (int64_t i = la + lane; i < le; i += 64) nn += !is_nan(value(i));
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) nn += __shfl_xor(nn, d);
+      // NaNs (either sign) take the largest key: ranks below nn never
+      // reach them
+      auto key_at = [&](int64_t i) {
+        const double v = value(la + i);
+        return is_nan(v) ? ~0ULL : dkey(v);
+      };
+      int64_t r0, r1;
+      double pos;
+      sel_ranks(median, p, nn, &r0, &r1, &pos);
+      double v = qnan();
+      if (nn > 0) {
+        const uint64_t k0 = wave_select(le - la, r0, hist, key_at);
+        const uint64_t k1 = (r1 == r0) ? k0 : wave_select(le - la, r1, hist, key_at);
+        v = sel_value(median, nn, pos, key_value(k0), key_value(k1));
+      }
+      if (lane == 0) {
+        if (lof) {
+          SM.of_val[s] = v;
+        } else {
+          rowv[lb] = v;
+          rows[lb] = ST_REAL;
+        }
+      }
+    }
+  }
+}
+
 }  // namespace otsdb

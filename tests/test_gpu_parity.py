@@ -138,6 +138,31 @@ def test_downsample_functions(engine, ds):
                   where="%s/%s/%s" % (ds, agg, kind))
 
 
+SEL_DS = ["median", "p50", "p75", "p95", "p99", "p999", "ep90r3", "ep50r7"]
+
+
+@pytest.mark.parametrize("ds", SEL_DS)
+def test_selection_downsampling(engine, ds):
+    """median / percentile as the downsampling function: per-bucket
+    selection (LDS sort for small buckets, wave radix select for large)."""
+    for kind, nan in (("float", 0.1), ("int", 0.0), ("mixed", 0.0)):
+        b = datasets.random_batch(27, n_series=24, n_groups=3, value_kind=kind,
+                                  nan_frac=nan)
+        for interval in ("1m", "1h"):  # 6 and 360 points per bucket
+            for agg, fill in (("sum", "none"), ("max", "nan"), ("p90", "zero")):
+                spec = _spec(agg, ds, fill, interval=interval)
+                check(engine, spec, b, agg != "sum", scale=1e4,
+                      where="%s/%s/%s/%s" % (ds, kind, interval, agg))
+    b = datasets.random_batch(29, n_series=12, n_groups=2, counter=True)
+    spec = _spec("sum", ds, rate=True, ro=RATES[1], interval="5m")
+    check(engine, spec, b, False, scale=1.0, where="%s/rate" % ds)
+    d = core.DownsamplingSpecification("0all-" + ds)
+    spec = core.make_spec(datasets.T0, datasets.T0 + 4 * 3600 * 1000,
+                          core.Aggregators.get("max"), d,
+                          datasets.T0 + 600000, datasets.T0 + 7200000)
+    check(engine, spec, b, True, where="%s/all" % ds)
+
+
 @pytest.mark.parametrize("fill", ["none", "nan", "zero", "null"])
 @pytest.mark.parametrize("aligned", [True, False])
 def test_fill_policies_and_window(engine, fill, aligned):
