@@ -244,6 +244,40 @@ otsdb_status otsdb_agg_finalize_device(otsdb_ctx* ctx,
                                        const uint8_t* emit,
                                        otsdb_result* out, void* hip_stream);
 
+/* ---- multi-GPU median / percentiles (series-sharded) -------------------- */
+/* Exact selection across ranks by radix select whose 256-bin histograms are
+ * summed over the ranks.  The protocol, every rank in step:
+ *
+ *   otsdb_sel_prepare_device(ctx, spec, batch, counts, emit)
+ *       local shard -> per-(group, bucket) non-NaN contribution counts
+ *       (int64 [G*n_buckets]) and emit flags (u8) in DEVICE memory
+ *   all-reduce counts (sum) and emit (max)
+ *   for pass in 0..7:
+ *       otsdb_sel_hist_device(ctx, pass, counts, emit, hist_prev, hist)
+ *           (pass 0 reads the global counts/emit; pass > 0 applies the
+ *           global histogram of the previous pass, hist_prev) and writes
+ *           this rank's histogram: u32 [G*n_buckets][2][256]
+ *       all-reduce hist (sum); it becomes hist_prev
+ *   otsdb_sel_finish_device(ctx, hist_last, result)
+ *
+ * Every rank ends with the full result.  The batch's group_offsets span all
+ * G global groups (empty where the rank holds no member).  Between prepare
+ * and finish the context must not run other queries (the session lives in
+ * its workspace).  Replaces PercentileAgg/Median.runDouble over the spans of
+ * a group (Aggregators.java:397-431, :657-708) when the spans are spread
+ * over GPUs.                                                               */
+otsdb_status otsdb_sel_prepare_device(otsdb_ctx* ctx,
+                                      const otsdb_query_spec* spec,
+                                      const otsdb_batch* batch,
+                                      int64_t* counts, uint8_t* emit,
+                                      void* hip_stream);
+otsdb_status otsdb_sel_hist_device(otsdb_ctx* ctx, int32_t pass,
+                                   const int64_t* counts, const uint8_t* emit,
+                                   uint32_t* hist_prev, uint32_t* hist,
+                                   void* hip_stream);
+otsdb_status otsdb_sel_finish_device(otsdb_ctx* ctx, uint32_t* hist_last,
+                                     otsdb_result* out, void* hip_stream);
+
 /* ---- compacted-cell decode (RowSeq) ------------------- */
 /* The storage rows of a query as the scanner hands them to Span.addRow
  * (Span.java:177-220): one compacted column per (series, hour) row —

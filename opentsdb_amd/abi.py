@@ -113,7 +113,8 @@ EXPORTS = [
     "otsdb_agg_run_device", "otsdb_agg_partials_device",
     "otsdb_agg_finalize_device", "otsdb_gen_counts_device",
     "otsdb_gen_fill_device", "otsdb_prof_enable", "otsdb_prof_read",
-    "otsdb_decode_cells_device",
+    "otsdb_decode_cells_device", "otsdb_sel_prepare_device",
+    "otsdb_sel_hist_device", "otsdb_sel_finish_device",
 ]
 
 _lib = None
@@ -171,6 +172,12 @@ def load(path=None):
     lib.otsdb_decode_cells_device.argtypes = [vp, C.POINTER(Cells), i64, vp,
                                               vp, vp, vp, i64, vp]
     lib.otsdb_decode_cells_device.restype = C.c_int
+    lib.otsdb_sel_prepare_device.argtypes = [vp, PS, PB, vp, vp, vp]
+    lib.otsdb_sel_prepare_device.restype = C.c_int
+    lib.otsdb_sel_hist_device.argtypes = [vp, i32, vp, vp, vp, vp, vp]
+    lib.otsdb_sel_hist_device.restype = C.c_int
+    lib.otsdb_sel_finish_device.argtypes = [vp, vp, PR, vp]
+    lib.otsdb_sel_finish_device.restype = C.c_int
     lib.otsdb_prof_enable.argtypes = [vp, C.c_int]
     lib.otsdb_prof_enable.restype = C.c_int
     lib.otsdb_prof_read.argtypes = [vp, vp, vp, C.c_int, C.c_int]

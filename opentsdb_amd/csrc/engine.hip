@@ -125,6 +125,20 @@ struct Carve {
   }
 };
 
+// device buffers of one query's pipeline, carved from the context workspace
+struct Work {
+  SeriesMeta SM;
+  Rows R;
+  Packed* partial;
+  uint8_t* tile_emit;
+  double* out_val;
+  uint8_t* out_emit;
+  int64_t* counts;
+  uint64_t* keys = nullptr;
+  SelState* sel = nullptr;
+  uint32_t* hist = nullptr;
+};
+
 }  // namespace
 
 struct otsdb_ctx {
@@ -142,6 +156,7 @@ struct otsdb_ctx {
   int64_t* d_tiles = nullptr;
   size_t d_tiles_cap = 0;
   int64_t n_tiles = 0, n_multi = 0, n_large = 0, n_large_chunks = 0;
+  bool tiles_sel_all = false;
   std::mutex mu;  // one query at a time per context
   // stage timing (otsdb_prof_*)
   bool prof = false;
@@ -155,6 +170,15 @@ struct otsdb_ctx {
   size_t dec_ws_cap = 0;
   void* ws2 = nullptr;     // raw group-by: candidates, sort, selection slab
   size_t ws2_cap = 0;
+  // cross-rank selection session (otsdb_sel_*): lives in `ws` between calls
+  struct {
+    bool active = false;
+    Params P;
+    otsdb_query_spec spec;
+    Work W;
+    int64_t G = 0, NB = 0, M = 0;
+    int median = 0;
+  } sel;
 };
 
 namespace {
@@ -275,8 +299,12 @@ otsdb_status make_params(const otsdb_query_spec* s, Params* P) {
   return OTSDB_OK;
 }
 
-otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff) {
-  if (c->d_tiles && goff == c->goff_cache) return OTSDB_OK;
+// sel_all: every group (even one without local members) joins the radix
+// select lists — the cross-rank selection protocol needs global segments
+otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff,
+                         bool sel_all = false) {
+  if (c->d_tiles && goff == c->goff_cache && sel_all == c->tiles_sel_all)
+    return OTSDB_OK;
   const int64_t G = (int64_t)goff.size() - 1;
   std::vector<int64_t> tg, tm0, tm1, mg, mt0, mt1, ag, at0, at1;
   std::vector<int64_t> lgg, lgo, lgk, lgc{0};  // groups for radix select
@@ -299,7 +327,7 @@ otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff) {
     ag.push_back(g);
     at0.push_back(t0);
     at1.push_back(t1);
-    if (b - a > SEL_K) {
+    if (b - a > SEL_K || sel_all) {
       lgg.push_back(g);
       lgo.push_back(a);
       lgk.push_back(b - a);
@@ -341,6 +369,7 @@ otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff) {
                            hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->goff_cache = goff;
+  c->tiles_sel_all = sel_all;
   c->n_tiles = T;
   c->n_multi = MG;
   c->n_large = LG;
@@ -414,18 +443,7 @@ inline unsigned blocks_for(int64_t n, int per) {
   return (unsigned)((n + per - 1) / per);
 }
 
-struct Work {
-  SeriesMeta SM;
-  Rows R;
-  Packed* partial;
-  uint8_t* tile_emit;
-  double* out_val;
-  uint8_t* out_emit;
-  int64_t* counts;
-  uint64_t* keys = nullptr;
-  SelState* sel = nullptr;
-  uint32_t* hist = nullptr;
-};
+
 
 // Everything up to dense (group, bucket) results / partials.
 // mode 0: final dense results; mode 1: per-group partials into `gpart/gemit`
@@ -436,7 +454,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   hipStream_t st = c->stream;
   const int64_t S = B.S;
   const int64_t G = (int64_t)goff.size() - 1;
-  otsdb_status rc = build_tiles(c, goff);
+  otsdb_status rc = build_tiles(c, goff, mode == 2);
   if (rc) return rc;
   const Tiles T = tiles_of(c, G);
   const int64_t nb = P.nb;
@@ -469,7 +487,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   const int64_t NB = P.nb;
 
   // workspace
-  const bool sel_large = is_selection(spec->agg_id) && T.LG > 0;
+  const bool sel_large = is_selection(spec->agg_id) && (T.LG > 0 || mode == 2);
   auto carve = [&](char* base) {
     Carve cv{base};
     W.SM.lo = cv.take<int64_t>(S);
@@ -498,7 +516,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   carve((char*)c->ws);
 
   HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), st));
-  if (G * NB > 0 && mode == 0)
+  if (G * NB > 0 && mode != 1)
     HIP_TRY(hipMemsetAsync(W.out_emit, 0, (size_t)G * NB, st));
   if (S > 0 && NB > 0)
     HIP_TRY(hipMemsetAsync(W.R.state, 0, (size_t)S * NB, st));
@@ -613,9 +631,9 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   if (G > 0 && NB > 0) {
     StageTimer tm(c, 2);
     if (is_selection(spec->agg_id)) {
-      if (mode != 0)
+      if (mode == 1)
         return fail(OTSDB_E_UNSUPPORTED,
-                    "percentiles across ranks are not offloaded yet");
+                    "percentiles across ranks: use the otsdb_sel_* protocol");
       const int median = spec->agg_id == OTSDB_AGG_MEDIAN ? 1 : 0;
       // n (non-NaN contributions) and the emit mask of every group
       using MC = MSum<3>;
@@ -629,6 +647,16 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
                            dim3(256), 0, st, NB, T.MG, T.mg, T.mt0, T.mt1,
                            W.partial, W.tile_emit, W.out_val, W.out_emit,
                            (Packed*)nullptr, c->d_err);
+      if (mode == 2) {
+        // cross-rank protocol: local counts + keys only (otsdb_sel_*)
+        const int64_t M = goff.back();
+        if (M > 0)
+          hipLaunchKernelGGL(k_keys_transpose,
+                             dim3(blocks_for(M, 64), blocks_for(NB, 64)),
+                             dim3(256), 0, st, NB, M, d_members, W.R, W.keys);
+        HIP_TRY(hipGetLastError());
+        return OTSDB_OK;
+      }
       // groups of <= SEL_K series: sort in LDS
       hipLaunchKernelGGL(k_group_select,
                          dim3(blocks_for(T.T * NB, SEL_THREADS)),
@@ -962,7 +990,9 @@ otsdb_status otsdb_ctx_create(int device, otsdb_ctx** out) {
   otsdb_ctx* c = new otsdb_ctx();
   c->device = device;
   if (const char* k = getenv("OTSDB_BUCKETIZE_K")) c->bucketize_k = atoi(k);
-  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  // a blocking stream: ordered with the legacy default stream torch uses,
+  // so tensors torch writes are complete before this context reads them
+  HIP_TRY(hipStreamCreate(&c->stream));
   HIP_TRY(hipMalloc(&c->d_err, 256));
   c->d_mm = (unsigned long long*)((char*)c->d_err + 64);
   HIP_TRY(hipHostMalloc(&c->h_small, 64));
@@ -1217,6 +1247,133 @@ otsdb_status otsdb_agg_finalize_device(otsdb_ctx* c,
       if (!rc) rc = finish(c, G, out);
     }
   }
+  c->stream = saved;
+  return rc;
+}
+
+// ---- cross-rank median / percentile -------------------------
+otsdb_status otsdb_sel_prepare_device(otsdb_ctx* c, const otsdb_query_spec* spec,
+                                      const otsdb_batch* b, int64_t* counts,
+                                      uint8_t* emit, void* hip_stream) {
+  if (!c || !spec || !b || !counts || !emit)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  c->sel.active = false;
+  hipStream_t saved = c->stream;
+  if (hip_stream) c->stream = (hipStream_t)hip_stream;
+  std::vector<int64_t> goff;
+  otsdb_status rc = read_goff(c, b, true, goff);
+  Params P;
+  if (!rc) rc = check_spec(spec);
+  if (!rc && !is_selection(spec->agg_id))
+    rc = fail(OTSDB_E_ILLEGAL_ARGUMENT, "otsdb_sel_* needs median/percentile");
+  if (!rc && !(spec->ds_interval_ms > 0 || spec->run_all))
+    rc = fail(OTSDB_E_UNSUPPORTED, "raw group-by across ranks");
+  if (!rc) rc = make_params(spec, &P);
+  if (!rc && !P.run_all && !P.fill && (double)b->n_series * (double)P.nb > 4.0e9)
+    rc = fail(OTSDB_E_UNSUPPORTED, "grid trimming is not supported across ranks");
+  if (!rc) {
+    BatchDev B{b->n_series, b->offsets, b->ts_ms, b->val, b->is_float,
+               b->series_float};
+    Work W;
+    rc = run_pipeline(c, spec, B, b->group_members, goff, P, W, 2, nullptr,
+                      nullptr);
+    const int64_t G = (int64_t)goff.size() - 1, GB = G * P.nb;
+    if (!rc && GB > 0) {
+      hipLaunchKernelGGL(k_dense_to_counts, dim3(blocks_for(GB, 256)),
+                         dim3(256), 0, c->stream, GB, (const double*)W.out_val,
+                         (const uint8_t*)W.out_emit, counts, emit);
+      HIP_TRY(hipGetLastError());
+    }
+    if (!rc) {
+      HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
+                             hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if ((int)(c->h_small[0] & 0xFFFFFFFF) & ERR_RATE_TS)
+        rc = fail(OTSDB_E_ILLEGAL_STATE,
+                  "Next timestamp is supposed to be strictly greater");
+    }
+    if (!rc) {
+      c->sel.active = true;
+      c->sel.P = P;
+      c->sel.spec = *spec;
+      c->sel.W = W;
+      c->sel.G = G;
+      c->sel.NB = P.nb;
+      c->sel.M = goff.back();
+      c->sel.median = spec->agg_id == OTSDB_AGG_MEDIAN ? 1 : 0;
+    }
+  }
+  c->stream = saved;
+  return rc;
+}
+
+otsdb_status otsdb_sel_hist_device(otsdb_ctx* c, int32_t pass,
+                                   const int64_t* counts, const uint8_t* emit,
+                                   uint32_t* hist_prev, uint32_t* hist_out,
+                                   void* hip_stream) {
+  if (!c || !hist_out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->sel.active) return fail(OTSDB_E_ILLEGAL_STATE, "no selection session");
+  if (pass < 0 || pass > 7) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "pass %d", pass);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  auto& S = c->sel;
+  const int64_t G = S.G, NB = S.NB, GB = G * NB;
+  const Tiles T = tiles_of(c, G);
+  if (pass == 0) {
+    if (!counts || !emit) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null counts");
+    if (GB > 0) {
+      hipLaunchKernelGGL(k_counts_to_dense, dim3(blocks_for(GB, 256)), dim3(256),
+                         0, st, GB, counts, emit, S.W.out_val, S.W.out_emit);
+      hipLaunchKernelGGL(k_sel_init, dim3(blocks_for(GB, 256)), dim3(256), 0,
+                         st, NB, G, T.lg_g, (const double*)S.W.out_val,
+                         (const uint8_t*)S.W.out_emit, S.W.sel, S.median,
+                         S.P.pct);
+    }
+  } else {
+    if (!hist_prev) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null hist_prev");
+    if (GB > 0)
+      hipLaunchKernelGGL(k_radix_select, dim3(blocks_for(GB * 2, 256)),
+                         dim3(256), 0, st, pass - 1, GB, hist_prev, S.W.sel);
+  }
+  if (GB > 0) {
+    HIP_TRY(hipMemsetAsync(hist_out, 0, (size_t)GB * 512 * 4, st));
+    if (T.LGCH > 0)
+      hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)(T.LGCH * NB)), dim3(256),
+                         0, st, pass, NB, S.M, G, T.lg_off, T.lg_k, T.lg_ch0,
+                         (const uint64_t*)S.W.keys, (const SelState*)S.W.sel,
+                         hist_out);
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(st));
+  return OTSDB_OK;
+}
+
+otsdb_status otsdb_sel_finish_device(otsdb_ctx* c, uint32_t* hist_last,
+                                     otsdb_result* out, void* hip_stream) {
+  if (!c || !hist_last || !out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!c->sel.active) return fail(OTSDB_E_ILLEGAL_STATE, "no selection session");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t saved = c->stream;
+  if (hip_stream) c->stream = (hipStream_t)hip_stream;
+  auto& S = c->sel;
+  const int64_t G = S.G, NB = S.NB, GB = G * NB;
+  const Tiles T = tiles_of(c, G);
+  HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
+  if (GB > 0) {
+    hipLaunchKernelGGL(k_radix_select, dim3(blocks_for(GB * 2, 256)), dim3(256),
+                       0, c->stream, 7, GB, hist_last, S.W.sel);
+    hipLaunchKernelGGL(k_sel_finish, dim3(blocks_for(GB, 256)), dim3(256), 0,
+                       c->stream, NB, G, T.lg_g, (const SelState*)S.W.sel,
+                       (const uint8_t*)S.W.out_emit, S.W.out_val, c->d_err,
+                       S.median, S.P.pct);
+  }
+  otsdb_status rc = compact(c, S.P, G, S.W.out_val, S.W.out_emit, S.W.counts, out);
+  if (!rc) rc = finish(c, G, out);
+  S.active = false;
   c->stream = saved;
   return rc;
 }

@@ -217,6 +217,27 @@ __global__ void k_sel_finish(int64_t nb, int64_t n_lg,
   out_val[o] = r;
 }
 
+// cross-rank protocol (otsdb_sel_*): dense (group, bucket) non-NaN counts
+// as doubles <-> the int64 counts ranks all-reduce
+__global__ void k_dense_to_counts(int64_t GB, const double* __restrict__ val,
+                                  const uint8_t* __restrict__ emit,
+                                  int64_t* __restrict__ counts,
+                                  uint8_t* __restrict__ emit_out) {
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= GB) return;
+  counts[o] = emit[o] ? (int64_t)val[o] : 0;
+  emit_out[o] = emit[o];
+}
+__global__ void k_counts_to_dense(int64_t GB, const int64_t* __restrict__ counts,
+                                  const uint8_t* __restrict__ emit,
+                                  double* __restrict__ val,
+                                  uint8_t* __restrict__ emit_out) {
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= GB) return;
+  val[o] = (double)counts[o];
+  emit_out[o] = emit[o] ? 1 : 0;
+}
+
 // ------------------------------------------------------------------------
 // r-th smallest (0-based) of n keys, key_at(i) for i in [0, n), by one
 // wavefront (the block must be exactly one wavefront: the LDS histogram is

@@ -6,7 +6,9 @@ no data-path collective.  Groups that span ranks are reduced to 32-byte
 per-(group, bucket) partials on every rank (otsdb_agg_partials_device),
 all-gathered over RCCL (torch.distributed, backend "nccl"; "gloo" in CPU
 tests) and merged in rank order, which is series order, by
-otsdb_agg_finalize_device.
+otsdb_agg_finalize_device.  Median / percentiles across ranks run the
+otsdb_sel_* protocol instead: all-reduced contribution counts, then eight
+radix-select passes whose 256-bin histograms are all-reduced (exact).
 """
 import numpy as np
 
@@ -38,6 +40,26 @@ def shared_groups(group_of_series, world):
     return np.nonzero((hi > lo) & (hi >= 0))[0]
 
 
+def _staged(group):
+    """gloo collectives run on host tensors; RCCL on device tensors."""
+    import torch.distributed as dist
+    return dist.get_backend(group) == "gloo"
+
+
+def all_reduce(t, op="sum", group=None):
+    """In-place all-reduce of a device tensor (staged through the host for
+    gloo)."""
+    import torch.distributed as dist
+    o = dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX
+    if _staged(group):
+        h = t.cpu()
+        dist.all_reduce(h, op=o, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=o, group=group)
+    return t
+
+
 def all_gather_partials(partials, emit, group=None):
     """partials: [GB, 4] int64 tensor (raw otsdb_partial words), emit: [GB]
     uint8.  Returns rank-major [world, GB, 4] / [world, GB] tensors — the
@@ -45,11 +67,14 @@ def all_gather_partials(partials, emit, group=None):
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    dev = partials.device
+    if dev.type != "cpu" and _staged(group):
+        partials, emit = partials.cpu(), emit.cpu()
     gp = [torch.empty_like(partials) for _ in range(world)]
     ge = [torch.empty_like(emit) for _ in range(world)]
     dist.all_gather(gp, partials.contiguous(), group=group)
     dist.all_gather(ge, emit.contiguous(), group=group)
-    return torch.stack(gp), torch.stack(ge)
+    return torch.stack(gp).to(dev), torch.stack(ge).to(dev)
 
 
 def run_sharded(engine, spec, dbatch, n_groups_global, torch_mod=None,
@@ -72,10 +97,10 @@ def run_sharded(engine, spec, dbatch, n_groups_global, torch_mod=None,
                         device=dev)
     emit = torch.zeros(max(GB, 1), dtype=torch.uint8, device=dev)
     b = dbatch.as_abi()
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     engine._check(engine.lib.otsdb_agg_partials_device(
         engine.ctx, C.byref(spec), C.byref(b), parts.data_ptr(),
-        emit.data_ptr(), None))
-    torch.cuda.synchronize()
+        emit.data_ptr(), stream))
     gp, ge = all_gather_partials(parts[:GB], emit[:GB], group)
     world = dist.get_world_size(group)
     res = DeviceResult(torch, n_groups_global, GB, dev)
@@ -83,8 +108,135 @@ def run_sharded(engine, spec, dbatch, n_groups_global, torch_mod=None,
     engine._check(engine.lib.otsdb_agg_finalize_device(
         engine.ctx, C.byref(spec), n_groups_global, nb, world,
         gp.contiguous().data_ptr(), ge.contiguous().data_ptr(), C.byref(r),
-        None))
+        stream))
     return res
+
+
+class ShardedSelect:
+    """One rank's side of the otsdb_sel_* protocol (include/otsdb_agg.h):
+    prepare -> counts/emit; hist(pass) x 8; finish.  The collectives between
+    the steps are the caller's (run_sharded_select, or an in-process
+    emulation in the GPU tests)."""
+
+    HIST_WORDS = 512  # u32 per (group, bucket): 2 targets x 256 bins
+
+    @staticmethod
+    def _stream():
+        """torch's current stream: the protocol's kernels queue behind the
+        tensor copies/collectives that feed them (the context's own stream
+        may be non-blocking)."""
+        import ctypes as C
+        import torch
+        return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def __init__(self, engine, spec, dbatch, n_groups_global):
+        import torch
+        self.engine, self.spec, self.dbatch = engine, spec, dbatch
+        self.G = n_groups_global
+        sz = engine.plan(spec, dbatch)
+        self.nb = int(sz.n_buckets)
+        self.GB = self.G * self.nb
+        self.dev = dbatch.ts.device
+        n = max(self.GB, 1)
+        self.counts = torch.zeros(n, dtype=torch.int64, device=self.dev)
+        self.emit = torch.zeros(n, dtype=torch.uint8, device=self.dev)
+        self.hist = torch.zeros(n * self.HIST_WORDS, dtype=torch.int32,
+                                device=self.dev)
+        self.prev = torch.zeros_like(self.hist)
+
+    def prepare(self):
+        import ctypes as C
+        b = self.dbatch.as_abi()
+        self.engine._check(self.engine.lib.otsdb_sel_prepare_device(
+            self.engine.ctx, C.byref(self.spec), C.byref(b),
+            self.counts.data_ptr(), self.emit.data_ptr(), self._stream()))
+        return self.counts, self.emit
+
+    def hist_pass(self, p):
+        """Local histogram of pass p; for p > 0 self.prev must hold the
+        all-reduced histogram of pass p - 1."""
+        self.engine._check(self.engine.lib.otsdb_sel_hist_device(
+            self.engine.ctx, int(p), self.counts.data_ptr(),
+            self.emit.data_ptr(), self.prev.data_ptr(), self.hist.data_ptr(),
+            self._stream()))
+        return self.hist
+
+    def set_prev(self, global_hist):
+        self.prev.copy_(global_hist)
+
+    def finish(self):
+        import ctypes as C
+        import torch
+        from .engine import DeviceResult
+        res = DeviceResult(torch, self.G, max(self.GB, 1), self.dev)
+        r = res.as_abi()
+        self.engine._check(self.engine.lib.otsdb_sel_finish_device(
+            self.engine.ctx, self.prev.data_ptr(), C.byref(r), self._stream()))
+        return res
+
+
+def run_sharded_select(engine, spec, dbatch, n_groups_global, group=None):
+    """Median / percentile over series-sharded groups: exact radix select
+    with RCCL all-reduces of the counts and of each pass's histograms."""
+    sel = ShardedSelect(engine, spec, dbatch, n_groups_global)
+    counts, emit = sel.prepare()
+    all_reduce(counts, "sum", group)
+    all_reduce(emit, "max", group)
+    for p in range(8):
+        h = sel.hist_pass(p)
+        all_reduce(h, "sum", group)
+        sel.set_prev(h)
+    return sel.finish()
+
+
+def shard_host_batch(hb, world, rank):
+    """Rank `rank`'s contiguous series range of a HostBatch, with group
+    offsets over every global group (members renumbered locally)."""
+    from .batch import HostBatch
+    a, b = shard_range(hb.n_series, world, rank)
+    offs = hb.offsets[a:b + 1] - hb.offsets[a]
+    p0, p1 = hb.offsets[a], hb.offsets[b]
+    g_off = [0]
+    members = []
+    for g in range(hb.n_groups):
+        m = hb.group_members[hb.group_offsets[g]:hb.group_offsets[g + 1]]
+        loc = m[(m >= a) & (m < b)] - a
+        members.extend(loc.tolist())
+        g_off.append(len(members))
+    return HostBatch(offs, hb.ts[p0:p1], hb.val[p0:p1],
+                     None if hb.is_float is None else hb.is_float[p0:p1],
+                     None if hb.series_float is None else hb.series_float[a:b],
+                     np.array(g_off, np.int64), np.array(members, np.int64))
+
+
+def to_device(hb, device="cuda"):
+    """HostBatch -> DeviceBatch (HBM-resident torch tensors)."""
+    import torch
+    from .engine import DeviceBatch
+
+    def t(x):
+        if x is None:
+            return None
+        y = torch.from_numpy(np.ascontiguousarray(x)).to(device)
+        return y
+    ts = torch.zeros(max(len(hb.ts), 2), dtype=torch.int64, device=device)
+    val = torch.zeros_like(ts)
+    if len(hb.ts):
+        ts[:len(hb.ts)] = t(hb.ts)
+        val[:len(hb.ts)] = t(hb.val)
+    db = DeviceBatch(t(hb.offsets), ts[:len(hb.ts)], val[:len(hb.ts)],
+                     t(hb.group_offsets), t(hb.group_members),
+                     t(hb.is_float), t(hb.series_float))
+    db.n_points_total = len(hb.ts)
+    return db
+
+
+def run_sharded_any(engine, spec, dbatch, n_groups_global, group=None):
+    """Dispatch: selection aggregators take the histogram protocol, every
+    other aggregator the partial all-gather."""
+    if spec.agg_id == 5 or spec.agg_id >= 17:  # median, p*, ep*
+        return run_sharded_select(engine, spec, dbatch, n_groups_global, group)
+    return run_sharded(engine, spec, dbatch, n_groups_global, group=group)
 
 
 def merge_partials_reference(parts_rank_major, kind="sum"):

@@ -89,3 +89,27 @@ def test_partial_exchange_gloo_world2():
     s, n = odist.merge_partials_reference(gp)
     exp_s = gp[0, :, 0].view(np.float64) + gp[1, :, 0].view(np.float64)
     assert np.array_equal(s, exp_s)
+
+
+def test_shard_host_batch_partitions_series_and_groups():
+    """Each rank's shard keeps its contiguous series range, its points, and
+    group offsets over every global group; together the shards rebuild the
+    batch (members in SpanCmp order)."""
+    from tests import datasets
+    hb = datasets.random_batch(7, n_series=23, n_groups=4)
+    for world in (1, 2, 3, 5):
+        members = [[] for _ in range(hb.n_groups)]
+        pts = []
+        for r in range(world):
+            sh = odist.shard_host_batch(hb, world, r)
+            a, b = odist.shard_range(hb.n_series, world, r)
+            assert sh.n_series == b - a and sh.n_groups == hb.n_groups
+            assert sh.offsets[0] == 0
+            pts.append(sh.ts)
+            for g in range(hb.n_groups):
+                loc = sh.group_members[sh.group_offsets[g]:sh.group_offsets[g + 1]]
+                members[g].extend((loc + a).tolist())
+        assert np.array_equal(np.concatenate(pts), hb.ts)
+        for g in range(hb.n_groups):
+            exp = hb.group_members[hb.group_offsets[g]:hb.group_offsets[g + 1]]
+            assert members[g] == exp.tolist()

@@ -1,0 +1,187 @@
+"""Series-sharded (multi-GPU) path on the one GPU of the test box.
+
+The cross-rank protocols are exercised exactly as ranks run them, with the
+collectives done in-process: each emulated rank has its own context, its
+shard of the series (contiguous SpanCmp range, dist.shard_host_batch) and
+group offsets over every global group.  Then two real processes run
+dist.run_sharded_any over gloo (both on cuda:0) — the code path bench.py and
+a node launch take, with RCCL swapped for gloo.  Reference: the oracle over
+the unsharded batch.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from opentsdb_amd import core, dist as odist
+from opentsdb_amd.engine import DataPoints, Engine
+from oracle import pyoracle
+from tests import datasets
+from tests.test_gpu_parity import ORDER_FREE, compare, _spec
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engines():
+    from opentsdb_amd import build
+    build.build()
+    es = [Engine(0) for _ in range(3)]
+    yield es
+    for e in es:
+        e.close()
+
+
+def _host(res, G):
+    offs = res.offsets.cpu().numpy()
+    ts, val, ii = (res.ts.cpu().numpy(), res.val.cpu().numpy(),
+                   res.is_int.cpu().numpy())
+    return [DataPoints(ts[offs[g]:offs[g + 1]], val[offs[g]:offs[g + 1]],
+                       ii[offs[g]:offs[g + 1]]) for g in range(G)]
+
+
+def _partials_emulated(engines, spec, hb, world):
+    import ctypes as C
+    import torch
+    from opentsdb_amd.engine import DeviceResult
+    G = hb.n_groups
+    parts, emits, nb = [], [], None
+    for r in range(world):
+        e = engines[0]
+        db = odist.to_device(odist.shard_host_batch(hb, world, r))
+        nb = int(e.plan(spec, db).n_buckets)
+        GB = G * nb
+        p = torch.zeros((max(GB, 1), 4), dtype=torch.int64, device="cuda")
+        m = torch.zeros(max(GB, 1), dtype=torch.uint8, device="cuda")
+        b = db.as_abi()
+        e._check(e.lib.otsdb_agg_partials_device(
+            e.ctx, C.byref(spec), C.byref(b), p.data_ptr(), m.data_ptr(), None))
+        parts.append(p[:GB])
+        emits.append(m[:GB])
+    gp = torch.stack(parts).contiguous()
+    ge = torch.stack(emits).contiguous()
+    res = DeviceResult(torch, G, max(G * nb, 1), "cuda")
+    r = res.as_abi()
+    e = engines[0]
+    e._check(e.lib.otsdb_agg_finalize_device(
+        e.ctx, C.byref(spec), G, nb, world, gp.data_ptr(), ge.data_ptr(),
+        C.byref(r), None))
+    torch.cuda.synchronize()
+    return _host(res, G)
+
+
+def _select_emulated(engines, spec, hb, world):
+    import torch
+    G = hb.n_groups
+    sels = [odist.ShardedSelect(engines[r], spec,
+                                odist.to_device(odist.shard_host_batch(hb, world, r)),
+                                G) for r in range(world)]
+    cs, es = zip(*[s.prepare() for s in sels])
+    counts = torch.stack(cs).sum(0)
+    emit = torch.stack(es).max(0).values
+    for s in sels:
+        s.counts.copy_(counts)
+        s.emit.copy_(emit)
+    for p in range(8):
+        h = torch.stack([s.hist_pass(p).clone() for s in sels]).sum(0)
+        for s in sels:
+            s.set_prev(h.to(torch.int32))
+    outs = [_host(s.finish(), G) for s in sels]
+    for o in outs[1:]:  # every rank ends with the same result
+        for a, b in zip(outs[0], o):
+            assert np.array_equal(a.ts, b.ts) and np.array_equal(a.bits, b.bits)
+    return outs[0]
+
+
+AGGS = ["sum", "zimsum", "avg", "dev", "min", "max", "mimmin", "mimmax",
+        "count", "first", "last", "diff", "mult", "squareSum", "pfsum"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("agg", AGGS)
+def test_partials_across_ranks(engines, agg, world):
+    """Per-(group, bucket) partials merged in rank (= series) order:
+    order-free aggregators bit-exact, sums within 1e-12."""
+    hb = datasets.random_batch(201, n_series=40, n_groups=3, nan_frac=0.02)
+    for ds, fill in (("avg", "none"), ("max", "nan"), ("sum", "zero")):
+        spec = _spec(agg, ds, fill)
+        ref = pyoracle.group_by(spec, hb)
+        got = _partials_emulated(engines, spec, hb, world)
+        # downsample avg/sum reduce buckets in a wave tree (1e-12)
+        compare(got, ref, agg in ORDER_FREE and ds == "max", scale=100.0,
+                where="w%d/%s/%s/%s" % (world, agg, ds, fill))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("agg", ["median", "p50", "p90", "p99", "p999",
+                                 "ep95r3", "ep50r7"])
+def test_percentiles_across_ranks(engines, agg, world):
+    """The otsdb_sel_* protocol: exact selection with all-reduced counts and
+    histograms — bit-identical to the single-GPU oracle result."""
+    hb = datasets.random_batch(203, n_series=90, n_groups=2, nan_frac=0.05,
+                               span_ms=3600 * 1000, cadence_ms=20000)
+    for ds, fill in (("avg", "none"), ("max", "nan")):
+        spec = _spec(agg, ds, fill, end=datasets.T0 + 3600 * 1000)
+        ref = pyoracle.group_by(spec, hb)
+        got = _select_emulated(engines, spec, hb, world)
+        compare(got, ref, ds == "max", scale=100.0,
+                where="w%d/%s/%s" % (world, agg, fill))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+QUERIES = [("sum", "avg", "none"), ("dev", "max", "nan"), ("p99", "avg", "nan"),
+           ("median", "max", "none")]
+
+
+def _rank_main(rank, world, port, q):
+    import torch
+    import torch.distributed as tdist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    e = Engine(0)
+    hb = datasets.random_batch(205, n_series=50, n_groups=3, nan_frac=0.02)
+    out = []
+    for agg, ds, fill in QUERIES:
+        spec = _spec(agg, ds, fill)
+        db = odist.to_device(odist.shard_host_batch(hb, world, rank))
+        res = odist.run_sharded_any(e, spec, db, hb.n_groups)
+        torch.cuda.synchronize()
+        out.append([(d.ts.copy(), d.bits.copy(), d.is_int.copy())
+                    for d in _host(res, hb.n_groups)])
+    if rank == 0:
+        q.put(out)
+    tdist.barrier()
+    tdist.destroy_process_group()
+    e.close()
+
+
+def test_two_processes_gloo():
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    out = q.get(timeout=240)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    hb = datasets.random_batch(205, n_series=50, n_groups=3, nan_frac=0.02)
+    for (agg, ds, fill), groups in zip(QUERIES, out):
+        ref = pyoracle.group_by(_spec(agg, ds, fill), hb)
+        got = [DataPoints(t, b, i) for t, b, i in groups]
+        compare(got, ref, ds == "max" and agg not in ("sum", "dev"), scale=100.0,
+                where="gloo/%s" % agg)
