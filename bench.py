@@ -67,6 +67,9 @@ def cpu_baseline(config, target_s):
                           config, n, pts, len(hb.group_offsets) - 1, dt)}
 
 
+_last = None
+
+
 def main():
     args = parse()
     import numpy as np
@@ -84,20 +87,36 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     cfg = workload.CONFIGS[args.config]
-    n_series = args.series or cfg["n_series"]
+    n_series = args.series or workload.default_series_per_gpu(args.config)
+    # groups that span ranks ({dc=*}, no group-by) take the cross-rank
+    # exchange: partial all-gather, or the histogram protocol for
+    # percentiles (opentsdb_amd/dist.py); host groups stay rank-local
+    sharded = world > 1 and workload.spans_ranks(args.config)
+    G_glob = (workload.n_groups_global(args.config, n_series * world)
+              if sharded else None)
     eng = Engine(local)
     g = workload.gen_spec(args.config)
     t_gen = time.perf_counter()
     db = workload.generate_device(eng, g, series0=rank * n_series,
-                                  n_series=n_series, config=args.config)
+                                  n_series=n_series, config=args.config,
+                                  n_groups=G_glob)
     t_gen = time.perf_counter() - t_gen
     n_points = db.n_points_total
     spec = workload.query_spec(args.config)
     sz = eng.plan(spec, db)
     res = DeviceResult(torch, db.n_groups, int(sz.max_out_points), "cuda")
+    if sharded:
+        from opentsdb_amd import dist as odist
+
+        def step():
+            global _last
+            _last = odist.run_sharded_any(eng, spec, db, G_glob)
+    else:
+        def step():
+            run_device(eng, spec, db, res)
 
     for _ in range(args.warmup):
-        run_device(eng, spec, db, res)
+        step()
     torch.cuda.synchronize()
     import ctypes as C
     eng.lib.otsdb_prof_enable(eng.ctx, 1)
@@ -108,7 +127,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        run_device(eng, spec, db, res)
+        step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -121,7 +140,7 @@ def main():
     stage_ms = [ms[i] / max(n[i], 1) for i in range(5)]
 
     total_points = n_points * world
-    out_points = int(res.offsets[-1].item())
+    out_points = int((_last if sharded else res).offsets[-1].item())
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -172,7 +191,8 @@ def main():
                 "groups_per_gpu": db.n_groups,
                 "buckets": int(sz.n_buckets),
                 "output_points_per_gpu": out_points,
-                "parallelism": "series-sharded dp%d" % world,
+                "parallelism": "series-sharded dp%d%s" % (
+                    world, " + RCCL exchange" if sharded else ""),
                 "stage_ms": {"bucketize": stage_ms[0],
                              "transform": stage_ms[1],
                              "group": stage_ms[2], "prep": stage_ms[3],

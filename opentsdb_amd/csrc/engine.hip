@@ -165,7 +165,7 @@ struct otsdb_ctx {
   size_t ev_used = 0;
   double prof_ms[8] = {0};
   int64_t prof_n[8] = {0};
-  int bucketize_k = 8;  // points per lane in k_bucketize (OTSDB_BUCKETIZE_K)
+  int bucketize_k = 0;  // k_bucketize variant (OTSDB_BUCKETIZE_K; 0 = production)
   void* dec_ws = nullptr;  // decode workspace
   size_t dec_ws_cap = 0;
   void* ws2 = nullptr;     // raw group-by: candidates, sort, selection slab
@@ -445,6 +445,21 @@ inline unsigned blocks_for(int64_t n, int per) {
 
 
 
+// Whether the k_bucketize variant `code` (OTSDB_BUCKETIZE_K) launched for
+// downsampler `ds_agg` writes sentinel rows through the LDS ring sink.
+bool bucketize_uses_ring(int code, int ds_agg) {
+  if (code == 2 || code == 4 || code == 8) return false;
+#ifdef OTSDB_BUCKETIZE_VARIANTS
+  static const int kDirect[] = {16, 41, 81, 86, 88, 46, 48, 99, 80, 40, 97,
+                                85, 89, 49, 82, 42, 96, 201, 202, 203, 204,
+                                205, 206};
+  if (ds_agg == OTSDB_AGG_AVG)
+    for (int d : kDirect)
+      if (code == d) return false;
+#endif
+  return true;
+}
+
 // Everything up to dense (group, bucket) results / partials.
 // mode 0: final dense results; mode 1: per-group partials into `gpart/gemit`
 otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
@@ -518,7 +533,15 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), st));
   if (G * NB > 0 && mode != 1)
     HIP_TRY(hipMemsetAsync(W.out_emit, 0, (size_t)G * NB, st));
-  if (S > 0 && NB > 0)
+  // the production k_bucketize (ring sink) leaves sentinel rows whose states
+  // k_transform writes; the other kernels store states into a zeroed row
+#ifdef OTSDB_BUCKETIZE_VARIANTS
+  // tuning build: the variant may change between queries of one context, so
+  // an A/B compares kernels over the same workspace placement
+  if (const char* k = getenv("OTSDB_BUCKETIZE_K")) c->bucketize_k = atoi(k);
+#endif
+  P.sentinel = !P.ds_sel && bucketize_uses_ring(c->bucketize_k, spec->ds_agg_id);
+  if (S > 0 && NB > 0 && !P.sentinel)
     HIP_TRY(hipMemsetAsync(W.R.state, 0, (size_t)S * NB, st));
 
   bool ok = true;
@@ -555,11 +578,53 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         // tuning variants (K, prefetch, non-temporal), avg downsampler only
         case 16: case 41: case 81: case 86: case 88: case 46: case 48: case 99:
         case 80: case 40: case 97: case 85: case 89: case 49: case 82: case 42: case 96:
+        case 201: case 202: case 203: case 204: case 205: case 206:
+        case 401: case 402: case 403: case 404: case 405: case 406:
+        case 407: case 408: case 409:
           if constexpr (std::is_same<M, MSum<1>>::value) {
             const int v = c->bucketize_k;
             Params P0 = P;  // 80/40: the generic (branchy) fold only
             P0.narrow = 0;
-            if (v == 80)
+            if (v >= 401 && v <= 404) {  // LDS ring sink variants
+              if (v == 401)
+                hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 0, 256>),
+                                   grid, blk, 0, st, P, B, W.SM, W.R);
+              else if (v == 402)
+                hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 0, 512>),
+                                   grid, blk, 0, st, P, B, W.SM, W.R);
+              else if (v == 403)
+                hipLaunchKernelGGL((k_bucketize_k<M, 4, 0, 0, 1, 0, 0, 256>),
+                                   grid, blk, 0, st, P, B, W.SM, W.R);
+              else
+                hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 256>),
+                                   grid, blk, 0, st, P, B, W.SM, W.R);
+            } else if (v == 405) {  // ablation: ring, no row stores
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 2, 1, 256>),
+                                 grid, blk, 0, st, P, B, W.SM, W.R);
+            } else if (v == 406) {  // non-temporal row stores
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 2, 1, 0, 1, 256>),
+                                 grid, blk, 0, st, P, B, W.SM, W.R);
+            } else if (v == 407) {  // 4 KiB flushes
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 1024, 512>),
+                                 grid, blk, 0, st, P, B, W.SM, W.R);
+            } else if (v == 408) {
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 2, 1, 0, 1, 1024, 512>),
+                                 grid, blk, 0, st, P, B, W.SM, W.R);
+            } else if (v == 409) {
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 512, 256>),
+                                 grid, blk, 0, st, P, B, W.SM, W.R);
+            } else if (v >= 201 && v <= 206) {  // LDS-DMA staged variants
+              auto L = [&](auto kern, int wpb) {
+                hipLaunchKernelGGL(kern, dim3(blocks_for(S, wpb)),
+                                   dim3(64 * wpb), 0, st, P, B, W.SM, W.R);
+              };
+              if (v == 201) L(k_bucketize_lds<M, 4, 4, 4>, 4);
+              else if (v == 202) L(k_bucketize_lds<M, 4, 3, 4>, 4);
+              else if (v == 203) L(k_bucketize_lds<M, 8, 3, 2>, 2);
+              else if (v == 204) L(k_bucketize_lds<M, 4, 4, 2>, 2);
+              else if (v == 205) L(k_bucketize_lds<M, 8, 4, 1>, 1);
+              else L(k_bucketize_lds<M, 2, 8, 4>, 4);
+            } else if (v == 80)
               hipLaunchKernelGGL((k_bucketize_k<M, 8>), grid, blk, 0, st, P0,
                                  B, W.SM, W.R);
             else if (v == 40)
@@ -616,9 +681,13 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
           }
           [[fallthrough]];
 #endif
-        default:
+        case 8:  // direct (scattered) row stores
           hipLaunchKernelGGL((k_bucketize_k<M, 8>), grid, blk, 0, st, P, B,
                              W.SM, W.R);
+          break;
+        default:  // production: LDS ring sink, sentinel rows, DPP scan
+          hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 256>), grid,
+                             blk, 0, st, P, B, W.SM, W.R);
       }
     });
     if (!ok) return fail(OTSDB_E_UNSUPPORTED, "downsampler %d", spec->ds_agg_id);
@@ -626,7 +695,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   if (S > 0 && NB > 0) {
     StageTimer tm(c, 1);
     hipLaunchKernelGGL(k_transform, dim3(blocks_for(S, 4)), dim3(256), 0, st,
-                       P, S, W.SM, W.R, c->d_err);
+                       P, B, W.SM, W.R, c->d_err);
   }
   if (G > 0 && NB > 0) {
     StageTimer tm(c, 2);

@@ -65,7 +65,16 @@ struct Params {
   int32_t ds_sel;        // downsampling function: 0 monoid, 1 median,
                          // 2 percentile (k_ds_select)
   double ds_pct;         // its percentile / 100.0
+  int32_t sentinel;      // rows written by the ring sink: k_bucketize left
+                         // no state bytes; a bucket of [first, last] point
+                         // bucket is absent iff its value is kAbsentBits
+  int32_t _pad2;
 };
+
+// value bits of an absent bucket in sentinel rows: a signalling NaN, which
+// no arithmetic produces and which the sink never stores for a real bucket
+// (NaN results are stored as the canonical quiet NaN)
+constexpr int64_t kAbsentBits = (int64_t)0x7FF4DEAD0BADF00DULL;
 
 struct BatchDev {
   int64_t S;

@@ -266,13 +266,75 @@ DEV bool fold_fast(const Params& P, const BatchDev& B, int sf, int64_t i0,
   return true;
 }
 
+DEV void wait_vmcnt(int n) {
+  // s_waitcnt vmcnt(n) (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14,
+  // expcnt and lgkmcnt at their no-wait maxima)
+  switch (n) {
+#define OTSDB_W(N) case N: __builtin_amdgcn_s_waitcnt(((N) & 0xF) | (0x7 << 4) | (0xF << 8) | (((N) >> 4) << 14)); break;
+    OTSDB_W(0) OTSDB_W(1) OTSDB_W(2) OTSDB_W(3) OTSDB_W(4) OTSDB_W(5)
+    OTSDB_W(6) OTSDB_W(7) OTSDB_W(8) OTSDB_W(9) OTSDB_W(10) OTSDB_W(11)
+    OTSDB_W(12) OTSDB_W(13) OTSDB_W(14) OTSDB_W(15) OTSDB_W(16) OTSDB_W(17)
+    OTSDB_W(18) OTSDB_W(19) OTSDB_W(20) OTSDB_W(21) OTSDB_W(22) OTSDB_W(23)
+    OTSDB_W(24) OTSDB_W(25) OTSDB_W(26) OTSDB_W(27) OTSDB_W(28) OTSDB_W(29)
+    OTSDB_W(30) OTSDB_W(31) OTSDB_W(32)
+#undef OTSDB_W
+    default: __builtin_amdgcn_s_waitcnt(0x7F << 4); break;  // vmcnt(0)
+  }
+}
+
+// Where closed buckets go.  Directly (one scattered 8-B value store and one
+// 1-B state store per closing lane), or through a per-wavefront LDS ring of
+// WIN bucket values that sink_flush drains in runs of 64 consecutive buckets,
+// absent ones included (kAbsentBits): the row leaves the CU as contiguous
+// 512-B stores and no state byte is written (k_transform derives the states,
+// Params.sentinel) — the scattered stores cost 2 of k_bucketize's 17 ms on
+// C2.
+struct RowSink {
+  double* rowv;
+  uint8_t* rows;
+  double* rv;      // LDS ring values, or null
+  int mask;        // WIN - 1
+  int direct;      // wave-uniform: write straight to HBM this step
+  int states;      // direct writes also store the state byte (no ring)
+  int nostore;     // tuning ablation (ABL == 2): the flush stores nothing
+  int nt;          // flush with non-temporal stores
+  DEV void put(int k, double v) {
+    if (states) {
+      rowv[k] = v;
+      rows[k] = ST_REAL;
+      return;
+    }
+    v = is_nan(v) ? qnan() : v;  // never the absent pattern
+    if (direct) rowv[k] = v;
+    else rv[k & mask] = v;
+  }
+};
+
+DEV double absent_value() { return __longlong_as_double(kAbsentBits); }
+
+// drains the ring's buckets [flushed, limit) (all final) to the row
+DEV void sink_flush(RowSink& S, int64_t& flushed, int64_t limit) {
+  const int lane = LANE;
+  for (int64_t f = flushed; f < limit; f += 64) {
+    const int64_t b = f + lane;
+    if (b < limit) {
+      const int i = (int)(b & S.mask);
+      const double v = S.rv[i];
+      if (S.nt) __builtin_nontemporal_store(v, &S.rowv[b]);
+      else if (!S.nostore || v == 1234.5678) S.rowv[b] = v;  // ablation
+      S.rv[i] = absent_value();
+    }
+  }
+  if (limit > flushed) flushed = limit;
+}
+
 // Folds the K points of one lane in order: the first run (which may continue
 // from the previous lane) goes to `head`, the last run (which may continue
 // into the next lane) stays in `cur`, runs in between close here.
 template <class M, int K, bool FLOATONLY, bool CHECKED>
 DEV void fold_lane(const Params& P, const BatchDev& B, int sf, int64_t i0,
                    int64_t lo, int64_t hi, const int64_t* t, const int64_t* v,
-                   double* rowv, uint8_t* rows, int& err, int& nseg,
+                   RowSink& S, int& err, int& nseg,
                    int& cur_key, int& head_key, M& cur, M& head) {
   int64_t bnd = INT64_MIN;  // first timestamp past cur_key's bucket
 #pragma unroll
@@ -296,8 +358,7 @@ DEV void fold_lane(const Params& P, const BatchDev& B, int sf, int64_t i0,
         head_key = cur_key;
         head = cur;
       } else {  // a bucket wholly inside this lane
-        rowv[cur_key] = cur.finish(&err);
-        rows[cur_key] = ST_REAL;
+        S.put(cur_key, cur.finish(&err));
       }
       cur_key = k;
       cur = M::from(x);
@@ -337,22 +398,189 @@ DEV int64_t readlane_l(int64_t b, int l) {
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
+// One step of the bucket reduction over the K consecutive points t[], v[]
+// of every lane (points i0 .. i0+K-1 of the series, step base `base`):
+// lane-local fold, the previous step's open bucket, the segmented wave scan
+// over the lanes' tail runs, the row writes and the new carry.
+template <class M, int K, int DPP>
+DEV void reduce_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
+                     int64_t hi, int64_t base, int64_t i0, const int64_t* t,
+                     const int64_t* v, RowSink& S, int& err,
+                     int& carry_key, M& carry) {
+  constexpr int PTS = 64 * K;
+  const int lane = LANE;
+  // ---- lane-local sequential fold (range checks only on the first and
+  // last step; no per-point type test for all-double series)
+  int nseg = 0, cur_key = 0, head_key = 0;
+  M cur = M::init(), head = M::init();
+  if (base >= lo && base + PTS <= hi) {
+    const bool fonly = !B.is_float && sf;
+    bool done = false;
+    if (P.narrow) {
+      done = fonly ? fold_fast<M, K, true>(P, B, sf, i0, t, v, nseg, cur_key,
+                                           head_key, cur, head)
+                   : fold_fast<M, K, false>(P, B, sf, i0, t, v, nseg,
+                                            cur_key, head_key, cur, head);
+    }
+    if (!done) {
+      if (fonly)
+        fold_lane<M, K, true, false>(P, B, sf, i0, lo, hi, t, v, S,
+                                     err, nseg, cur_key, head_key, cur, head);
+      else
+        fold_lane<M, K, false, false>(P, B, sf, i0, lo, hi, t, v, S,
+                                      err, nseg, cur_key, head_key, cur,
+                                      head);
+    }
+  } else {
+    fold_lane<M, K, false, true>(P, B, sf, i0, lo, hi, t, v, S,
+                                 err, nseg, cur_key, head_key, cur, head);
+  }
+  if (nseg == 0) {  // lane wholly before lo (first step) or past hi
+    cur_key = (i0 < lo) ? -1 : INT32_MAX;
+    head_key = cur_key;
+  } else if (nseg == 1) {
+    head_key = cur_key;
+  }
+  // ---- previous step's open bucket
+  if (lane == 0) {
+    if (nseg >= 1 && carry_key == head_key) {
+      if (nseg == 1) cur = M::combine(carry, cur);
+      else head = M::combine(carry, head);
+    } else if (carry_key >= 0 && carry_key < P.nb) {
+      S.put(carry_key, carry.finish(&err));
+    }
+  }
+  // ---- segmented inclusive scan over the lanes' tail runs
+  int key = cur_key;
+  M st = cur;
+  int pkey, next_head;
+  M pst;
+  if (DPP) {
+    seg_scan_dpp(key, st);
+    pkey = dpp32<0x138, 0xF>(INT32_MIN, key);  // wave_shr:1
+    pst = st;
+    pst.template dpp<0x138, 0xF>();
+    next_head = dpp32<0x130, 0xF>(INT32_MIN, head_key);  // wave_shl:1
+  } else {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int k2 = __shfl_up(key, d);
+      M o = st;
+      o.shfl_up(d);
+      if (lane >= d && k2 == key) st = M::combine(o, st);
+    }
+    pkey = __shfl_up(key, 1);
+    pst = st;
+    pst.shfl_up(1);
+    next_head = __shfl_down(head_key, 1);
+  }
+  if (nseg >= 2) {  // head run closes inside this lane
+    const M full = (lane > 0 && pkey == head_key) ? M::combine(pst, head) : head;
+    S.put(head_key, full.finish(&err));
+  }
+  if (nseg >= 1 && lane < 63 && next_head != key) {
+    S.put(key, st.finish(&err));
+  }
+  Packed p = st.pack();
+  if (DPP) {
+    carry_key = __builtin_amdgcn_readlane(key, 63);
+    p.x = readlane_d(p.x, 63);
+    p.y = readlane_d(p.y, 63);
+    p.z = readlane_d(p.z, 63);
+    p.w = readlane_l(p.w, 63);
+  } else {
+    carry_key = __shfl(key, 63);
+    p.x = __shfl(p.x, 63);
+    p.y = __shfl(p.y, 63);
+    p.z = __shfl(p.z, 63);
+    p.w = __shfl(p.w, 63);
+  }
+  carry = M::unpack(p);
+}
+
+// Ring bookkeeping around one step (WIN > 0).  Before the step: every
+// bucket the step can write lies in [k_open, k_hi]; if that range does not
+// fit the ring behind the flushed mark, drain what is final and, failing
+// that (a gap of more than WIN buckets inside one step), write this step
+// straight to HBM.  After it: drain the final buckets in runs of 64.
+DEV int64_t step_last_key(const Params& P, const BatchDev& B, int64_t base,
+                          int64_t hi, int64_t pts) {
+  const int64_t e = (base + pts < hi ? base + pts : hi) - 1;
+  return bucket_of(P, B.ts[e]);
+}
+
+template <int WIN, int K>
+DEV void ring_before(const Params& P, const BatchDev& B, RowSink& S,
+                     int64_t& flushed, int64_t lo, int64_t hi, int64_t base,
+                     const int64_t* t, int carry_key) {
+  if (WIN == 0) return;
+  constexpr int64_t pts = 64 * K;
+  // last key of the step: from lane 63's last point when the step is full
+  // (already in registers; a scalar reload would wait on HBM every step)
+  const int64_t k_hi =
+      (base + pts <= hi)
+          ? bucket_of(P, readlane_l(t[K - 1], 63))
+          : step_last_key(P, B, base, hi, pts);
+  if (k_hi >= flushed + WIN) {
+    const int64_t k_open = (carry_key >= 0 && carry_key < P.nb)
+                               ? carry_key
+                               : bucket_of(P, B.ts[base > lo ? base : lo]);
+    sink_flush(S, flushed, k_open);
+    if (k_hi >= flushed + WIN) {
+      // a gap of more than WIN buckets inside this step: mark the span
+      // absent, then let the step store straight to HBM behind it
+      const int lane = LANE;
+      for (int64_t f = flushed; f <= k_hi; f += 64)
+        if (f + lane <= k_hi) S.rowv[f + lane] = absent_value();
+      wait_vmcnt(0);
+      S.direct = 1;
+    }
+  }
+}
+
+template <int WIN, int FL>
+DEV void ring_after(const Params& P, const BatchDev& B, RowSink& S,
+                    int64_t& flushed, int64_t hi, int64_t base, int64_t pts,
+                    int carry_key) {
+  if (WIN == 0) return;
+  // buckets below the open one (or the whole step, past the end) are final
+  const int64_t limit = (carry_key >= 0 && carry_key < P.nb)
+                            ? carry_key
+                            : step_last_key(P, B, base, hi, pts) + 1;
+  if (S.direct) {
+    if (limit > flushed) flushed = limit;
+    S.direct = 0;
+    return;
+  }
+  const int64_t full = flushed + ((limit - flushed) / FL) * FL;
+  if (full > flushed) sink_flush(S, flushed, full);
+}
+
 template <class M, int K, int PF = 0, int NT = 0, int WAVES = 1, int ABL = 0,
-          int DPP = 0>
+          int DPP = 0, int WIN = 0, int FL = 64>
 __global__ __launch_bounds__(256, WAVES) void k_bucketize_k(Params P,
                                                             BatchDev B,
                                                             SeriesMeta SM,
                                                             Rows R) {
   static_assert(K % 2 == 0, "K must be even (16-byte loads)");
+  static_assert((WIN & (WIN - 1)) == 0, "WIN: power of two");
+  constexpr int WS = WIN > 0 ? WIN : 1;
+  __shared__ double ring_v[4][WS];
   const int lane = LANE;
-  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int w = threadIdx.x >> 6;
+  const int64_t s = (int64_t)blockIdx.x * 4 + w;
   if (s >= B.S) return;
   if (!SM.keep[s]) return;
   const int64_t lo = SM.lo[s], hi = SM.hi[s];
   if (lo >= hi) return;
   const int sf = B.series_float ? (int)B.series_float[s] : 1;
-  double* rowv = R.val + s * P.nb;
-  uint8_t* rows = R.state + s * P.nb;
+  RowSink S{R.val + s * P.nb, R.state + s * P.nb, ring_v[w], WS - 1,
+            WIN == 0, WIN == 0, ABL == 2, NT == 2};
+  int64_t flushed = 0;
+  if (WIN) {
+    for (int i = lane; i < WIN; i += 64) ring_v[w][i] = absent_value();
+    flushed = bucket_of(P, B.ts[lo]);
+  }
   int err = 0;
 
   int carry_key = INT32_MIN;
@@ -366,7 +594,7 @@ __global__ __launch_bounds__(256, WAVES) void k_bucketize_k(Params P,
         const ll2_t* pt = reinterpret_cast<const ll2_t*>(B.ts + i0 + j);
         const ll2_t* pv = reinterpret_cast<const ll2_t*>(B.val + i0 + j);
         ll2_t tt, vv;
-        if (NT) {
+        if (NT == 1) {
           tt = __builtin_nontemporal_load(pt);
           vv = __builtin_nontemporal_load(pv);
         } else {
@@ -401,103 +629,106 @@ __global__ __launch_bounds__(256, WAVES) void k_bucketize_k(Params P,
       int64_t x = 0;
 #pragma unroll
       for (int j = 0; j < K; ++j) x ^= t[j] + v[j];
-      if (x == 42) rows[0] = 1;
+      if (x == 42) S.rows[0] = 1;
       continue;
     }
-    // ---- lane-local sequential fold (range checks only on the first and
-    // last step; no per-point type test for all-double series)
-    int nseg = 0, cur_key = 0, head_key = 0;
-    M cur = M::init(), head = M::init();
-    if (base >= lo && base + PTS <= hi) {
-      const bool fonly = !B.is_float && sf;
-      bool done = false;
-      if (P.narrow) {
-        done = fonly ? fold_fast<M, K, true>(P, B, sf, i0, t, v, nseg, cur_key,
-                                             head_key, cur, head)
-                     : fold_fast<M, K, false>(P, B, sf, i0, t, v, nseg,
-                                              cur_key, head_key, cur, head);
-      }
-      if (!done) {
-        if (fonly)
-          fold_lane<M, K, true, false>(P, B, sf, i0, lo, hi, t, v, rowv, rows,
-                                       err, nseg, cur_key, head_key, cur, head);
-        else
-          fold_lane<M, K, false, false>(P, B, sf, i0, lo, hi, t, v, rowv, rows,
-                                        err, nseg, cur_key, head_key, cur,
-                                        head);
-      }
-    } else {
-      fold_lane<M, K, false, true>(P, B, sf, i0, lo, hi, t, v, rowv, rows,
-                                   err, nseg, cur_key, head_key, cur, head);
+    // drain the buckets the previous step finished only now, after this
+    // step's loads are issued: vmcnt retires loads and stores in issue
+    // order, so stores issued before a load would hold up its data
+    if (base != base0)
+      ring_after<WIN, FL>(P, B, S, flushed, hi, base - PTS, PTS, carry_key);
+    ring_before<WIN, K>(P, B, S, flushed, lo, hi, base, t, carry_key);
+    reduce_step<M, K, DPP>(P, B, sf, lo, hi, base, i0, t, v, S, err,
+                           carry_key, carry);
+  }
+  if (carry_key >= 0 && carry_key < P.nb && lane == 0)
+    S.put(carry_key, carry.finish(&err));
+  // every bucket from the first point's to the last point's is written; a
+  // last step that went direct already stored its buckets behind `flushed`
+  // (the ring only holds absent slots there)
+  if (WIN && !S.direct) sink_flush(S, flushed, bucket_of(P, B.ts[hi - 1]) + 1);
+}
+
+// ------------------------------------------------------------------------
+// k_bucketize_lds: k_bucketize_k with the point stream staged by LDS-DMA
+// (global_load_lds_dwordx4: HBM -> LDS with no VGPR destination).  Each
+// wavefront keeps NBUF stages of its series in an LDS ring and issues stage
+// s + NBUF - 1 before it reduces stage s, so NBUF - 1 stages (K*(NBUF-1)
+// wave-instructions of 1 KiB) stay in flight while it computes — latency
+// hiding that no longer costs registers (the register-staged kernel holds
+// its in-flight points in 32 VGPRs at K = 8 and runs at 4 waves/SIMD).
+// A stage is 64*K points of ts and of val, lane-linear: lane l of load j
+// brings points 128j + 2l, 128j + 2l + 1.  vmcnt counts LDS-DMA in issue
+// order with every other vector memory op, so the counted wait below (the
+// glds issued after stage s) covers stage s; younger row stores only make it
+// wait longer.  Steps that reach past the series' end (the last one) read
+// HBM directly, range checked.
+// ------------------------------------------------------------------------
+
+template <class M, int K, int NBUF, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_bucketize_lds(Params P,
+                                                           BatchDev B,
+                                                           SeriesMeta SM,
+                                                           Rows R) {
+  static_assert(K % 2 == 0 && K * (NBUF - 1) <= 32, "K, NBUF");
+  constexpr int PTS = 64 * K;
+  __shared__ __attribute__((aligned(16))) int64_t ring[WPB][NBUF][2][PTS];
+  const int lane = LANE;
+  const int w = threadIdx.x >> 6;
+  const int64_t s = (int64_t)blockIdx.x * WPB + w;
+  if (s >= B.S) return;
+  if (!SM.keep[s]) return;
+  const int64_t lo = SM.lo[s], hi = SM.hi[s];
+  if (lo >= hi) return;
+  const int sf = B.series_float ? (int)B.series_float[s] : 1;
+  RowSink S{R.val + s * P.nb, R.state + s * P.nb, nullptr, 0, 1, 1, 0, 0};
+  int err = 0;
+  int carry_key = INT32_MIN;
+  M carry = M::init();
+  const int64_t base0 = lo & ~(int64_t)1;
+  // steps whose PTS points all lie before hi come through the LDS ring
+  const int64_t nfull = (hi - base0) / PTS;
+  auto issue = [&](int64_t st) {
+    const int64_t b = base0 + st * PTS;
+    int64_t* slot = &ring[w][st % NBUF][0][0];
+#pragma unroll
+    for (int j = 0; j < K / 2; ++j) {
+      __builtin_amdgcn_global_load_lds(B.ts + b + 128 * j + 2 * lane,
+                                       slot + 128 * j, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(B.val + b + 128 * j + 2 * lane,
+                                       slot + PTS + 128 * j, 16, 0, 0);
     }
-    if (nseg == 0) {  // lane wholly before lo (first step) or past hi
-      cur_key = (i0 < lo) ? -1 : INT32_MAX;
-      head_key = cur_key;
-    } else if (nseg == 1) {
-      head_key = cur_key;
-    }
-    // ---- previous step's open bucket
-    if (lane == 0) {
-      if (nseg >= 1 && carry_key == head_key) {
-        if (nseg == 1) cur = M::combine(carry, cur);
-        else head = M::combine(carry, head);
-      } else if (carry_key >= 0 && carry_key < P.nb) {
-        rowv[carry_key] = carry.finish(&err);
-        rows[carry_key] = ST_REAL;
+  };
+  for (int64_t st = 0; st < NBUF - 1 && st < nfull; ++st) issue(st);
+  int64_t st = 0;
+  for (int64_t base = base0; base < hi; base += PTS, ++st) {
+    const int64_t i0 = base + (int64_t)K * lane;
+    int64_t t[K], v[K];
+    if (st < nfull) {
+      if (st + NBUF - 1 < nfull) issue(st + NBUF - 1);
+      const int64_t after = (nfull - 1 - st) < (NBUF - 1) ? (nfull - 1 - st)
+                                                          : (NBUF - 1);
+      wait_vmcnt((int)after * K);
+      const int64_t* slot = &ring[w][st % NBUF][0][0];
+#pragma unroll
+      for (int j = 0; j < K; j += 2) {
+        const ll2_t tt = *reinterpret_cast<const ll2_t*>(slot + K * lane + j);
+        const ll2_t vv = *reinterpret_cast<const ll2_t*>(slot + PTS + K * lane + j);
+        t[j] = tt.x; t[j + 1] = tt.y;
+        v[j] = vv.x; v[j + 1] = vv.y;
       }
-    }
-    // ---- segmented inclusive scan over the lanes' tail runs
-    int key = cur_key;
-    M st = cur;
-    int pkey, next_head;
-    M pst;
-    if (DPP) {
-      seg_scan_dpp(key, st);
-      pkey = dpp32<0x138, 0xF>(INT32_MIN, key);  // wave_shr:1
-      pst = st;
-      pst.template dpp<0x138, 0xF>();
-      next_head = dpp32<0x130, 0xF>(INT32_MIN, head_key);  // wave_shl:1
     } else {
 #pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int k2 = __shfl_up(key, d);
-        M o = st;
-        o.shfl_up(d);
-        if (lane >= d && k2 == key) st = M::combine(o, st);
+      for (int j = 0; j < K; ++j) {
+        t[j] = (i0 + j < hi) ? B.ts[i0 + j] : 0;
+        v[j] = (i0 + j < hi) ? B.val[i0 + j] : 0;
       }
-      pkey = __shfl_up(key, 1);
-      pst = st;
-      pst.shfl_up(1);
-      next_head = __shfl_down(head_key, 1);
     }
-    if (nseg >= 2) {  // head run closes inside this lane
-      const M full = (lane > 0 && pkey == head_key) ? M::combine(pst, head) : head;
-      rowv[head_key] = full.finish(&err);
-      rows[head_key] = ST_REAL;
-    }
-    if (nseg >= 1 && lane < 63 && next_head != key) {
-      rowv[key] = st.finish(&err);
-      rows[key] = ST_REAL;
-    }
-    Packed p = st.pack();
-    if (DPP) {
-      carry_key = __builtin_amdgcn_readlane(key, 63);
-      p.x = readlane_d(p.x, 63);
-      p.y = readlane_d(p.y, 63);
-      p.z = readlane_d(p.z, 63);
-      p.w = readlane_l(p.w, 63);
-    } else {
-      carry_key = __shfl(key, 63);
-      p.x = __shfl(p.x, 63);
-      p.y = __shfl(p.y, 63);
-      p.z = __shfl(p.z, 63);
-      p.w = __shfl(p.w, 63);
-    }
-    carry = M::unpack(p);
+    reduce_step<M, K, 0>(P, B, sf, lo, hi, base, i0, t, v, S, err,
+                         carry_key, carry);
   }
   if (lane == 0 && carry_key >= 0 && carry_key < P.nb) {
-    rowv[carry_key] = carry.finish(&err);
-    rows[carry_key] = ST_REAL;
+    S.put(carry_key, carry.finish(&err));
   }
 }
 
@@ -527,37 +758,64 @@ DEV double interp_value(int method, int64_t x, int64_t x0, double y0,
 //  * otherwise interpolation between the series' own points (:754-793),
 //    contributing iff first <= x <= last (or a point exists past the window).
 // ------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_transform(Params P, int64_t S,
+__global__ __launch_bounds__(256) void k_transform(Params P, BatchDev B,
                                                    SeriesMeta SM, Rows R,
                                                    int* err_word) {
   const int lane = LANE;
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (s >= S) return;
-  if (!SM.keep[s]) return;
+  if (s >= B.S) return;
   const int64_t nb = P.nb;
   double* rowv = R.val + s * nb;
   uint8_t* rows = R.state + s * nb;
+  const bool sent = P.sentinel != 0;
+  if (!SM.keep[s]) {
+    if (sent)  // no memset before a sentinel-row query: clear the states
+      for (int64_t b = lane; b < nb; b += 64) rows[b] = ST_ABSENT;
+    return;
+  }
   const bool fill = P.fill != 0 && !P.run_all;
+  // sentinel rows: buckets [kf, kl] (first / last point's bucket) hold a
+  // value or kAbsentBits, the others are absent
+  int64_t kf = 0, kl = -1;
+  if (sent && SM.lo[s] < SM.hi[s]) {
+    kf = bucket_of(P, B.ts[SM.lo[s]]);
+    kl = bucket_of(P, B.ts[SM.hi[s] - 1]);
+  }
+  auto real_at = [&](int64_t b, double v) {
+    return sent ? (b >= kf && b <= kl && __double_as_longlong(v) != kAbsentBits)
+                : rows[b] == ST_REAL;
+  };
 
   if (!P.rate) {
     if (fill) {
       for (int64_t c0 = 0; c0 < nb; c0 += 64) {
         const int64_t b = c0 + lane;
-        if (b < nb && rows[b] != ST_REAL) {
-          rowv[b] = P.fill_value;
-          rows[b] = ST_REAL;
+        if (b < nb) {
+          if (!real_at(b, rowv[b])) {
+            rowv[b] = P.fill_value;
+            rows[b] = ST_REAL;
+          } else if (sent) {
+            rows[b] = ST_REAL;
+          }
         }
       }
       return;
     }
     // NONE fill: interpolate inside gaps, and toward the point past the
     // window when there is one.
+    const bool of = SM.of_has[s] != 0;
     int64_t carry_idx = -1;
     double carry_val = 0.0;
     for (int64_t c0 = 0; c0 < nb; c0 += 64) {
       const int64_t b = c0 + lane;
-      const bool p = b < nb && rows[b] == ST_REAL;
-      const double v = p ? rowv[b] : 0.0;
+      const double vb = b < nb ? rowv[b] : 0.0;
+      const bool p = b < nb && real_at(b, vb);
+      const double v = p ? vb : 0.0;
+      if (sent && b < nb)  // every state of the row, written once
+        rows[b] = p ? ST_REAL
+                    : (((b > kf && b < kl) || (of && kf <= kl && b > kl))
+                           ? ST_INTERP
+                           : ST_ABSENT);
       const int64_t incl = wave_incl_max(p ? b : -1);
       int64_t prev = __shfl_up(incl, 1);
       if (lane == 0) prev = -1;
@@ -606,9 +864,10 @@ __global__ __launch_bounds__(256) void k_transform(Params P, int64_t S,
   for (int64_t c0 = 0; c0 < nb; c0 += 64) {
     const int64_t b = c0 + lane;
     const bool inb = b < nb;
-    const uint8_t st = inb ? rows[b] : 0;
+    const double vb = inb ? rowv[b] : 0.0;
+    const uint8_t st = (inb && real_at(b, vb)) ? ST_REAL : 0;
     const bool pt = inb && (fill || st == ST_REAL);
-    const double pv = (st == ST_REAL) ? rowv[b] : P.fill_value;
+    const double pv = (st == ST_REAL) ? vb : P.fill_value;
     const int64_t t = bucket_ts(P, b);
     const int64_t incl = wave_incl_max(pt ? b : -1);
     int64_t prev = __shfl_up(incl, 1);

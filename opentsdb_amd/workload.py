@@ -77,6 +77,41 @@ def query_spec(name, series0=0):
                           ro, normalize=True)
 
 
+# configs quoted on 8 GPUs: the config's series count is the node total
+NODE_CONFIGS = {"C3": 8, "C5": 8}
+
+
+def default_series_per_gpu(name):
+    c = CONFIGS[name]
+    return c["n_series"] // NODE_CONFIGS.get(name, 1)
+
+
+def n_groups_global(name, n_series_total):
+    g = CONFIGS[name]["group"]
+    if g == "host":
+        return (n_series_total + 9) // 10
+    if g == "dc":
+        return min(16, (n_series_total + 9) // 10)
+    return 1
+
+
+def spans_ranks(name):
+    """Groups of this config can hold series of several ranks."""
+    return CONFIGS[name]["group"] != "host"
+
+
+def global_groups(name, series0, n, G):
+    """Group CSR of series [series0, series0+n) over ALL G global groups
+    (empty groups where this shard has no member) — the layout of the
+    cross-rank protocols."""
+    gid = group_ids(name, series0, n)
+    order = np.argsort(gid, kind="stable").astype(np.int64)
+    counts = np.bincount(gid, minlength=G)
+    g_off = np.zeros(G + 1, np.int64)
+    np.cumsum(counts, out=g_off[1:])
+    return g_off, order
+
+
 def local_groups(name, series0, n):
     """Group CSR for series [series0, series0+n) with group ids made dense
     and kept in ByteMap (= numeric) order; returns (g_off, members,
@@ -91,7 +126,7 @@ def local_groups(name, series0, n):
 
 
 def generate_device(engine, gspec, series0, n_series, group_size=None,
-                    config=None, device="cuda"):
+                    config=None, device="cuda", n_groups=None):
     """Generates series [series0, series0+n) straight into HBM and returns a
     DeviceBatch (torch tensors)."""
     import ctypes as C
@@ -110,7 +145,9 @@ def generate_device(engine, gspec, series0, n_series, group_size=None,
         engine.ctx, C.byref(gspec), series0, n_series, offsets.data_ptr(),
         ts.data_ptr(), val.data_ptr(), None))
     torch.cuda.synchronize()
-    if config is not None:
+    if config is not None and n_groups is not None:
+        g_off, members = global_groups(config, series0, n_series, n_groups)
+    elif config is not None:
         g_off, members, _ = local_groups(config, series0, n_series)
     else:
         gs = group_size or n_series

@@ -1,5 +1,8 @@
-"""A/B of k_bucketize variants (points per lane K) in ONE process,
-interleaved rounds (methodology rule: cdna_hip_programming.md §5.4 r24)."""
+"""A/B of k_bucketize variants in ONE process and ONE context (same input
+and workspace placement), interleaved rounds (methodology rule:
+cdna_hip_programming.md §5.4 r24).  Needs the variants build
+(OTSDB_LIB=.../libotsdb_agg_variants.so), which re-reads OTSDB_BUCKETIZE_K
+per query."""
 import argparse, ctypes as C, json, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
@@ -16,11 +19,8 @@ ap.add_argument("--reps", type=int, default=5)
 a = ap.parse_args()
 torch.cuda.set_device(0)
 ks = [int(x) for x in a.ks.split(",")]
-engs = {}
-for k in ks:
-    os.environ["OTSDB_BUCKETIZE_K"] = str(k)
-    engs[k] = Engine(0)
-e0 = engs[ks[0]]
+e0 = Engine(0)
+engs = {k: e0 for k in ks}
 cfg = workload.CONFIGS[a.config]
 n = a.series or cfg["n_series"]
 db = workload.generate_device(e0, workload.gen_spec(a.config), 0, n, config=a.config)
@@ -29,11 +29,13 @@ sz = e0.plan(spec, db)
 res = {k: DeviceResult(torch, db.n_groups, int(sz.max_out_points), "cuda") for k in ks}
 times = {k: [] for k in ks}
 for k in ks:
+    os.environ["OTSDB_BUCKETIZE_K"] = str(k)
     run_device(engs[k], spec, db, res[k])
 torch.cuda.synchronize()
 for r in range(a.rounds):
     for k in ks:
         e = engs[k]
+        os.environ["OTSDB_BUCKETIZE_K"] = str(k)
         e.lib.otsdb_prof_enable(e.ctx, 1)
         e.lib.otsdb_prof_read(e.ctx, None, None, 0, 1)
         for _ in range(a.reps):
