@@ -5,7 +5,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-KS=${PMC_KS:-8}
+KS=${PMC_KS:-0}
 CFG=${PMC_CFG:-C2}
 OUT=gpurun_out/pmc_${CFG}
 mkdir -p "$OUT"
