@@ -172,9 +172,11 @@ def main():
     # dominant kernel: k_bucketize streams every point once (16 B/point)
     kb_s = stage_ms[0] / 1e3
     achieved = BYTES_PER_POINT * n_points / kb_s / 1e9 if kb_s > 0 else None
+    # PMC traffic of this exact workload (scripts/gpu_pmc.sh, default size,
+    # one GPU), per k_bucketize launch
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and not args.series and world == 1:
         with open(pmc) as f:
             traffic = json.load(f).get("k_bucketize_hbm_bytes_per_launch")
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OTSDB_ABI_VERSION 1
+#define OTSDB_ABI_VERSION 2
 
 /* ------------------------------------------------------------------------ */
 /* Status codes — 1:1 with the exceptions of the reference path.             */
@@ -133,13 +133,31 @@ typedef struct {
   int32_t ds_agg_id;       /* downsampling function (not NONE)             */
   int32_t fill;            /* otsdb_fill                                   */
   int32_t run_all;         /* "0all-<agg>" downsampling                    */
-  int32_t use_calendar;    /* "<n><u>c-" downsampling -> E_UNSUPPORTED     */
+  int32_t use_calendar;    /* "<n><u>c-" downsampling: needs cal_edges     */
   int32_t rate;            /* RateSpan applied after downsampling          */
   int32_t counter;         /* RateOptions.counter                          */
   int32_t drop_resets;     /* RateOptions.drop_resets                      */
   int32_t _pad;
   int64_t counter_max;     /* RateOptions.counter_max (default Long.MAX)   */
   int64_t reset_value;     /* RateOptions.reset_value (default 0)          */
+  /* Calendar downsampling (use_calendar = 1): the bucket edges, ms, strictly
+   * ascending, HOST memory (copied during the call).  cal_edges[0] =
+   * DateTime.previousInterval(start_ms, n, unit, tz) (DateTime.java:450-610)
+   * and cal_edges[k+1] = cal_edges[k] stepped once the way the Downsampler
+   * steps its calendars (Calendar.add(unit, n), or 7n days for weeks,
+   * Downsampler.java:387-394), continued until two edges lie past end_ms
+   * (past the batch's last point if spans hold points beyond the window).
+   * Bucket k is [cal_edges[k], cal_edges[k+1]) with timestamp cal_edges[k]
+   * (ValuesInInterval.getIntervalTimestamp, :437-449).  The reference
+   * anchors each series at previousInterval(its first point); the caller
+   * passes a table only when every such anchor in [start_ms, end_ms] is an
+   * edge (the grid does not depend on the series) and otherwise keeps the
+   * Java iterators.  A point past the window whose bucket end is not in the
+   * table is OTSDB_E_UNSUPPORTED.  NULL with use_calendar = 1 ->
+   * OTSDB_E_UNSUPPORTED.  ds_interval_ms stays DownsamplingSpecification's
+   * nominal interval (parseDuration), which the scan bounds use.          */
+  const int64_t* cal_edges;
+  int64_t n_cal_edges;
 } otsdb_query_spec;
 
 /* ------------------------------------------------------------------------ */

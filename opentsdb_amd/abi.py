@@ -42,6 +42,8 @@ class QuerySpec(C.Structure):
         ("_pad", C.c_int32),
         ("counter_max", C.c_int64),
         ("reset_value", C.c_int64),
+        ("cal_edges", C.c_void_p),
+        ("n_cal_edges", C.c_int64),
     ]
 
 

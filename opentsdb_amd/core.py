@@ -244,6 +244,7 @@ class DownsamplingSpecification:
             self.string_interval = None
             self.use_calendar = False
             self.run_all = False
+            self.timezone = None
             return
         if specification is None:
             raise IllegalArgumentException(
@@ -258,6 +259,7 @@ class DownsamplingSpecification:
                 "Invalid downsampling specifier '%s': must consist of "
                 "interval, function, and optional fill policy" % specification)
         self.run_all = False
+        self.timezone = None  # DateTime.timezones.get(UTC_ID)
         if "all" in parts[0]:
             self.interval = self.NO_INTERVAL
             self.use_calendar = False
@@ -299,6 +301,28 @@ class DownsamplingSpecification:
 
     def useCalendar(self):
         return self.use_calendar
+
+    def setUseCalendar(self, use_calendar):
+        self.use_calendar = bool(use_calendar)
+
+    def getStringInterval(self):
+        return self.string_interval
+
+    def setTimezone(self, timezone):
+        """DownsamplingSpecification.setTimezone (:202-207): a zone name or
+        tzinfo."""
+        if timezone is None:
+            raise IllegalArgumentException("Timezone cannot be null")
+        self.timezone = timezone
+
+    def getTimezone(self):
+        return self.timezone
+
+    def calendar_interval(self):
+        """(n, calendar unit) as the Downsampler ctor parses string_interval
+        (Downsampler.java:131-141)."""
+        from . import jcalendar
+        return jcalendar.parse_calendar_interval(self.string_interval)
 
 
 # -------------------------------------------------------------- RateOptions
@@ -367,7 +391,8 @@ def to_ms(t):
 # ---------------------------------------------------------- query spec
 def make_spec(start_time, end_time, aggregator, downsampler=None,
               query_start=0, query_end=0, rate=False, rate_options=None,
-              interpolation=None, normalize=False):
+              interpolation=None, normalize=False, cal_edges=None,
+              cal_cover_ms=None):
     """Builds the otsdb_query_spec of one AggregationIterator.create call
     (AggregationIterator.java:351-380).  start/end are the iterator window in
     ms; with normalize=True they are SpanGroup bounds (seconds or ms) and are
@@ -390,6 +415,20 @@ def make_spec(start_time, end_time, aggregator, downsampler=None,
         s.fill = int(downsampler.getFillPolicy())
         s.run_all = int(bool(downsampler.run_all))
         s.use_calendar = int(bool(downsampler.useCalendar()))
+        if s.use_calendar and not s.run_all:
+            # the query's calendar grid (opentsdb_amd/jcalendar.py); raises
+            # UnsupportedOperationException when it depends on the series
+            import numpy as np
+            from . import jcalendar
+            if cal_edges is None:
+                n, unit = downsampler.calendar_interval()
+                cal_edges = jcalendar.calendar_edges(
+                    s.start_ms, s.end_ms, n, unit, downsampler.getTimezone(),
+                    cover_ms=cal_cover_ms)
+            edges = np.ascontiguousarray(cal_edges, np.int64)
+            s._cal_edges_ref = edges  # keeps the table alive with the spec
+            s.cal_edges = edges.ctypes.data
+            s.n_cal_edges = len(edges)
     ro = rate_options or RateOptions()
     s.rate = int(bool(rate))
     s.counter = int(ro.counter)

@@ -165,6 +165,8 @@ struct otsdb_ctx {
   size_t ev_used = 0;
   double prof_ms[8] = {0};
   int64_t prof_n[8] = {0};
+  void* cal = nullptr;  // calendar bucket edges of the current query
+  size_t cal_cap = 0;
   int bucketize_k = 0;  // k_bucketize variant (OTSDB_BUCKETIZE_K; 0 = production)
   void* dec_ws = nullptr;  // decode workspace
   size_t dec_ws_cap = 0;
@@ -219,8 +221,19 @@ otsdb_status check_spec(const otsdb_query_spec* s) {
   if (s->ds_agg_id == OTSDB_AGG_NONE)
     return fail(OTSDB_E_ILLEGAL_ARGUMENT,
                 "cannot use the NONE aggregator for downsampling");
-  if (s->use_calendar)
-    return fail(OTSDB_E_UNSUPPORTED, "calendar downsampling");
+  if (s->use_calendar && !s->run_all) {
+    if (!s->cal_edges || s->n_cal_edges < 2)
+      return fail(OTSDB_E_UNSUPPORTED,
+                  "calendar downsampling without a bucket-edge table");
+    for (int64_t k = 1; k < s->n_cal_edges; ++k)
+      if (s->cal_edges[k] <= s->cal_edges[k - 1])
+        return fail(OTSDB_E_ILLEGAL_ARGUMENT,
+                    "cal_edges must increase strictly (index %lld)",
+                    (long long)k);
+    if (s->cal_edges[0] > s->start_ms)
+      return fail(OTSDB_E_ILLEGAL_ARGUMENT,
+                  "cal_edges[0] must be previousInterval(start_ms)");
+  }
   if (s->fill == OTSDB_FILL_SCALAR)
     return fail(OTSDB_E_UNSUPPORTED, "unhandled fill policy");
   if (s->fill < 0 || s->fill > OTSDB_FILL_SCALAR)
@@ -232,8 +245,62 @@ otsdb_status check_spec(const otsdb_query_spec* s) {
   return OTSDB_OK;
 }
 
+// Calendar grid (otsdb_query_spec.cal_edges): the fixed-interval rules of
+// make_params restated on the edge table — seek to the first edge >= start
+// (ValuesInInterval.seekInterval rounds up, Downsampler.java:431-441), NONE:
+// every edge <= end_ms; filling: [previousInterval(start),
+// previousInterval(end)) advanced once when both coincide
+// (FillingDownsampler.java:113-131).  With a context the table is copied to
+// the device and P->cal points at the grid's bucket 0.
+otsdb_status make_cal_params(const otsdb_query_spec* s, Params* P,
+                             otsdb_ctx* c) {
+  const int64_t* e = s->cal_edges;
+  const int64_t n = s->n_cal_edges;
+  auto first_ge = [&](int64_t t) {
+    return (int64_t)(std::lower_bound(e, e + n, t) - e);
+  };
+  auto last_le = [&](int64_t t) {
+    return (int64_t)(std::upper_bound(e, e + n, t) - e) - 1;
+  };
+  const int64_t k_seek = first_ge(s->start_ms);
+  int64_t nb;
+  if (P->fill) {
+    const int64_t kA = last_le(s->start_ms);
+    int64_t kE = last_le(s->end_ms);
+    if (kE == kA) kE = kA + 1;
+    nb = std::max<int64_t>(0, kE - k_seek);
+    if (kA >= 0 && kA < k_seek) {
+      P->rate_origin_ts = e[kA];
+      P->rate_origin_val = P->fill_value;
+    }
+  } else {
+    nb = std::max<int64_t>(0, last_le(s->end_ms) - k_seek + 1);
+  }
+  if (k_seek + nb >= n)
+    return fail(OTSDB_E_UNSUPPORTED,
+                "calendar table ends before the window (%lld edges)",
+                (long long)n);
+  P->nb = nb;
+  P->gbase = e[k_seek];
+  P->seek_ts = e[k_seek];
+  P->stop_ts = e[k_seek + nb];
+  P->narrow = 0;
+  P->cal_lo = -k_seek;
+  P->cal_n = n - k_seek;
+  P->cal = nullptr;
+  if (c) {
+    otsdb_status rc = ensure(&c->cal, &c->cal_cap, sizeof(int64_t) * n);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(c->cal, e, sizeof(int64_t) * n,
+                           hipMemcpyHostToDevice, c->stream));
+    P->cal = (const int64_t*)c->cal + k_seek;
+  }
+  return OTSDB_OK;
+}
+
 // Grid of buckets every series row is laid out on.
-otsdb_status make_params(const otsdb_query_spec* s, Params* P) {
+otsdb_status make_params(const otsdb_query_spec* s, Params* P,
+                         otsdb_ctx* c = nullptr) {
   memset(P, 0, sizeof(*P));
   P->start_ms = s->start_ms;
   P->end_ms = s->end_ms;
@@ -275,6 +342,7 @@ otsdb_status make_params(const otsdb_query_spec* s, Params* P) {
   const int64_t iv = s->ds_interval_ms;
   P->interval = iv;
   P->inv_interval = 1.0 / (double)iv;
+  if (s->use_calendar) return make_cal_params(s, P, c);
   const int64_t grid0 = align_down(s->start_ms + iv - 1, iv);
   P->gbase = grid0;
   P->seek_ts = grid0;
@@ -476,7 +544,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
 
   // grid trimming for very wide windows (NONE fill only): the rows span only
   // the buckets that hold data
-  if (!P.run_all && !P.fill && (double)S * (double)nb > 4.0e9) {
+  if (!P.run_all && !P.fill && !P.cal && (double)S * (double)nb > 4.0e9) {
     unsigned long long init[2] = {~0ULL, 0ULL};
     HIP_TRY(hipMemcpyAsync(c->d_mm, init, 16, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_bounds, dim3(blocks_for(S, 256)), dim3(256), 0, st, P,
@@ -550,7 +618,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     {
       StageTimer tm(c, 3);
       hipLaunchKernelGGL(k_prep<MSum<3>>, dim3(blocks_for(S, 256)), dim3(256),
-                         0, st, P, B, W.SM);
+                         0, st, P, B, W.SM, c->d_err);
     }
     StageTimer tm(c, 0);
     hipLaunchKernelGGL(k_ds_select, dim3((unsigned)S), dim3(64), 0, st, P, B,
@@ -561,7 +629,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       {
         StageTimer tm(c, 3);
         hipLaunchKernelGGL(k_prep<M>, dim3(blocks_for(S, 256)), dim3(256), 0,
-                           st, P, B, W.SM);
+                           st, P, B, W.SM, c->d_err);
       }
       StageTimer tm(c, 0);
       const dim3 grid(blocks_for(S, 4)), blk(256);
@@ -838,6 +906,9 @@ otsdb_status finish(otsdb_ctx* c, int64_t G, otsdb_result* out) {
     return fail(OTSDB_E_UNSUPPORTED,
                 "percentile/median over groups of more than %d series is not "
                 "offloaded yet", SEL_K);
+  if (err & ERR_CAL_RANGE)
+    return fail(OTSDB_E_UNSUPPORTED,
+                "a point past the window lies outside the calendar table");
   if (total > out->capacity)
     return fail(OTSDB_E_CAPACITY, "result capacity %lld < %lld points",
                 (long long)out->capacity, (long long)total);
@@ -1018,7 +1089,7 @@ otsdb_status run_device_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
   otsdb_status rc = check_spec(spec);
   if (rc) return rc;
   Params P;
-  rc = make_params(spec, &P);
+  rc = make_params(spec, &P, c);
   if (rc) return rc;
   if ((((uintptr_t)b->ts_ms) | ((uintptr_t)b->val)) & 15)
     return fail(OTSDB_E_ILLEGAL_ARGUMENT,
@@ -1077,6 +1148,7 @@ void otsdb_ctx_destroy(otsdb_ctx* c) {
   if (c->stage) hipFree(c->stage);
   if (c->dec_ws) hipFree(c->dec_ws);
   if (c->ws2) hipFree(c->ws2);
+  if (c->cal) hipFree(c->cal);
   if (c->d_tiles) hipFree(c->d_tiles);
   if (c->d_err) hipFree(c->d_err);
   for (auto e : c->ev_pool) hipEventDestroy(e);
@@ -1236,7 +1308,7 @@ otsdb_status otsdb_agg_partials_device(otsdb_ctx* c,
   otsdb_status rc = read_goff(c, b, true, goff);
   Params P;
   if (!rc) rc = check_spec(spec);
-  if (!rc) rc = make_params(spec, &P);
+  if (!rc) rc = make_params(spec, &P, c);
   if (!rc && !(spec->ds_interval_ms > 0 || spec->run_all))
     rc = fail(OTSDB_E_UNSUPPORTED,
               "raw group-by across ranks (union timestamps need an all-gather)");
@@ -1282,7 +1354,7 @@ otsdb_status otsdb_agg_finalize_device(otsdb_ctx* c,
   if (hip_stream) c->stream = (hipStream_t)hip_stream;
   otsdb_status rc = check_spec(spec);
   Params P;
-  if (!rc) rc = make_params(spec, &P);
+  if (!rc) rc = make_params(spec, &P, c);
   if (!rc && P.nb != n_buckets)
     rc = fail(OTSDB_E_ILLEGAL_ARGUMENT, "n_buckets %lld != plan %lld",
               (long long)n_buckets, (long long)P.nb);
@@ -1339,7 +1411,7 @@ otsdb_status otsdb_sel_prepare_device(otsdb_ctx* c, const otsdb_query_spec* spec
     rc = fail(OTSDB_E_ILLEGAL_ARGUMENT, "otsdb_sel_* needs median/percentile");
   if (!rc && !(spec->ds_interval_ms > 0 || spec->run_all))
     rc = fail(OTSDB_E_UNSUPPORTED, "raw group-by across ranks");
-  if (!rc) rc = make_params(spec, &P);
+  if (!rc) rc = make_params(spec, &P, c);
   if (!rc && !P.run_all && !P.fill && (double)b->n_series * (double)P.nb > 4.0e9)
     rc = fail(OTSDB_E_UNSUPPORTED, "grid trimming is not supported across ranks");
   if (!rc) {

@@ -40,6 +40,7 @@ enum : int {
   ERR_X1_MASK = 16,     // interpolation toward x1 >= 2^44 ms (AssertionError
                         // in AggregationIterator.java:706-708, :776-778)
   ERR_RAW_DUP = 32,     // timestamps not increasing inside a raw span
+  ERR_CAL_RANGE = 64,   // a point past the window outside the calendar table
 };
 
 struct Params {
@@ -69,6 +70,11 @@ struct Params {
                          // no state bytes; a bucket of [first, last] point
                          // bucket is absent iff its value is kAbsentBits
   int32_t _pad2;
+  // calendar grid (otsdb_query_spec.cal_edges, device copy): bucket b is
+  // [cal[b], cal[b+1]); valid indices cal_lo <= b < cal_n (cal_lo <= 0 when
+  // the table starts before the grid's first bucket); null = fixed interval
+  const int64_t* cal;
+  int64_t cal_lo, cal_n;
 };
 
 // value bits of an absent bucket in sentinel rows: a signalling NaN, which

@@ -20,8 +20,21 @@ DEV int64_t align_ts(int64_t t, int64_t iv) { return t - t % iv; }
 
 // floor(rel / interval) for rel >= 0 without a 64-bit divide: double
 // reciprocal estimate + one correction step each way.
+// calendar grid: the b with cal[b] <= ts < cal[b+1] (binary search over the
+// table; clamped to [cal_lo - 1, cal_n - 1] outside it)
+DEV int64_t cal_bucket(const Params& P, int64_t ts) {
+  int64_t lo = P.cal_lo, hi = P.cal_n;  // first index with cal[i] > ts
+  while (lo < hi) {
+    const int64_t m = lo + ((hi - lo) >> 1);
+    if (P.cal[m] <= ts) lo = m + 1;
+    else hi = m;
+  }
+  return lo - 1;
+}
+
 DEV int64_t bucket_of(const Params& P, int64_t ts) {
   if (P.run_all) return 0;
+  if (P.cal) return cal_bucket(P, ts);
   const int64_t rel = ts - P.gbase;
   int64_t q = (int64_t)((double)rel * P.inv_interval);
   int64_t r = rel - q * P.interval;
@@ -33,7 +46,7 @@ DEV int64_t bucket_of(const Params& P, int64_t ts) {
 }
 
 DEV int64_t bucket_ts(const Params& P, int64_t b) {
-  return P.run_all ? P.out_ts0 : P.gbase + b * P.interval;
+  return P.run_all ? P.out_ts0 : P.cal ? P.cal[b] : P.gbase + b * P.interval;
 }
 
 DEV double point_value(const BatchDev& B, int64_t i, int64_t bits, int sf) {
@@ -69,8 +82,19 @@ DEV int64_t wave_incl_max(int64_t x) {
 // interpolate up to end_time, AggregationIterator.java:760-775).
 // One thread per series.
 // ------------------------------------------------------------------------
+DEV void k_prep_store(SeriesMeta SM, int64_t s, bool keep, int64_t lo,
+                      int64_t hi, uint8_t of_has, int64_t of_ts,
+                      double of_val) {
+  SM.keep[s] = keep;
+  SM.lo[s] = lo;
+  SM.hi[s] = hi;
+  SM.of_has[s] = of_has;
+  SM.of_ts[s] = of_ts;
+  SM.of_val[s] = of_val;
+}
+
 template <class M>
-__global__ void k_prep(Params P, BatchDev B, SeriesMeta SM) {
+__global__ void k_prep(Params P, BatchDev B, SeriesMeta SM, int* err_word) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= B.S) return;
   const int64_t p0 = B.offsets[s], p1 = B.offsets[s + 1];
@@ -86,8 +110,20 @@ __global__ void k_prep(Params P, BatchDev B, SeriesMeta SM) {
     if (!P.run_all && P.fill == 0 && hi < p1) {
       const int sf = B.series_float ? (int)B.series_float[s] : 1;
       const int64_t t = B.ts[hi];
-      of_ts = align_ts(t, P.interval);
-      const int64_t e = of_ts + P.interval;
+      int64_t e;
+      if (P.cal) {  // the calendar bucket holding t (Downsampler.java:383-397)
+        const int64_t k = cal_bucket(P, t);
+        if (k < P.cal_lo || k + 1 >= P.cal_n) {
+          atomicOr(err_word, ERR_CAL_RANGE);
+          k_prep_store(SM, s, keep, lo, hi, 0, 0, 0.0);
+          return;
+        }
+        of_ts = P.cal[k];
+        e = P.cal[k + 1];
+      } else {
+        of_ts = align_ts(t, P.interval);
+        e = of_ts + P.interval;
+      }
       M st = M::init();
       for (int64_t i = hi; i < p1 && B.ts[i] < e; ++i)
         st.push(point_value(B, i, B.val[i], sf));
@@ -96,11 +132,7 @@ __global__ void k_prep(Params P, BatchDev B, SeriesMeta SM) {
       of_has = 1;
     }
   }
-  SM.lo[s] = lo;
-  SM.hi[s] = hi;
-  SM.of_has[s] = of_has;
-  SM.of_ts[s] = of_ts;
-  SM.of_val[s] = of_val;
+  k_prep_store(SM, s, keep, lo, hi, of_has, of_ts, of_val);
 }
 
 // ------------------------------------------------------------------------
@@ -344,7 +376,7 @@ DEV void fold_lane(const Params& P, const BatchDev& B, int sf, int64_t i0,
     int k = cur_key;
     if (nseg == 0 || t[j] >= bnd) {
       k = (int)bucket_of(P, t[j]);
-      bnd = P.run_all ? INT64_MAX : P.gbase + ((int64_t)k + 1) * P.interval;
+      bnd = P.run_all ? INT64_MAX : bucket_ts(P, (int64_t)k + 1);
     }
     const double x = FLOATONLY ? bits_to_double(v[j]) : point_value(B, i, v[j], sf);
     if (nseg == 0) {

@@ -356,8 +356,8 @@ __global__ __launch_bounds__(64) void k_ds_select(Params P, BatchDev B,
   // buckets that can hold points: [b_first, b_last] (+ nb for of_val)
   int64_t b_first = 0, b_last = -1;
   if (lo < hi) {
-    b_first = P.run_all ? 0 : (B.ts[lo] - P.gbase) / P.interval;
-    b_last = P.run_all ? 0 : (B.ts[hi - 1] - P.gbase) / P.interval;
+    b_first = bucket_of(P, B.ts[lo]);
+    b_last = bucket_of(P, B.ts[hi - 1]);
   }
   const bool of = SM.of_has[s] != 0;
   const int64_t n_b = (b_last - b_first + 1) + (of ? 1 : 0);
@@ -370,14 +370,16 @@ __global__ __launch_bounds__(64) void k_ds_select(Params P, BatchDev B,
     if (act) {
       if (is_of) {
         a = hi;
-        e = lower_bound(B.ts, hi, p1, SM.of_ts[s] + P.interval);
+        const int64_t of_end =
+            P.cal ? P.cal[cal_bucket(P, SM.of_ts[s]) + 1]
+                  : SM.of_ts[s] + P.interval;
+        e = lower_bound(B.ts, hi, p1, of_end);
       } else if (P.run_all) {
         a = lo;
         e = hi;
       } else {
-        const int64_t t0 = P.gbase + b * P.interval;
-        a = lower_bound(B.ts, lo, hi, t0);
-        e = lower_bound(B.ts, a, hi, t0 + P.interval);
+        a = lower_bound(B.ts, lo, hi, bucket_ts(P, b));
+        e = lower_bound(B.ts, a, hi, bucket_ts(P, b + 1));
       }
     }
     const int64_t cnt = e - a;

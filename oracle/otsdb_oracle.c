@@ -508,7 +508,39 @@ typedef struct {
   int filling;
   int fill_policy;
   int64_t f_timestamp, f_end_timestamp;
+  /* calendar ("<n><u>c-"): the caller's edge table stands in for
+   * java.util.Calendar (otsdb_query_spec.cal_edges); previous_calendar /
+   * next_calendar are edge indices */
+  int cal;
+  const int64_t* edges;
+  int64_t n_edges;
+  int64_t prev_cal, next_cal;       /* ValuesInInterval                    */
+  int64_t f_prev_cal, f_next_cal;   /* FillingDownsampler                  */
 } ds_view;
+
+/* DateTime.previousInterval(ts) on the table: the edge <= ts. */
+static int64_t cal_prev(ds_view* d, int64_t ts) {
+  int64_t lo = 0, hi = d->n_edges; /* first edge > ts */
+  while (lo < hi) {
+    int64_t m = lo + (hi - lo) / 2;
+    if (d->edges[m] <= ts) lo = m + 1; else hi = m;
+  }
+  if (lo == 0 || lo >= d->n_edges)
+    jthrow(d->v.exc, OTSDB_E_UNSUPPORTED,
+           "timestamp %lld outside the calendar table", (long long)ts);
+  return lo - 1;
+}
+/* Calendar.add(unit, interval) on an edge index. */
+static int64_t cal_step(ds_view* d, int64_t k) {
+  if (k + 1 >= d->n_edges)
+    jthrow(d->v.exc, OTSDB_E_UNSUPPORTED, "calendar table exhausted");
+  return k + 1;
+}
+static int64_t cal_ts(ds_view* d, int64_t k) {
+  if (k < 0 || k >= d->n_edges)
+    jthrow(d->v.exc, OTSDB_E_UNSUPPORTED, "calendar table exhausted");
+  return d->edges[k];
+}
 
 static inline int64_t ds_align(ds_view* d, int64_t t) {
   return t - jmod(t, d->interval);
@@ -544,15 +576,31 @@ static void vii_initialize_if_not_done(ds_view* d) {
     d->initialized = 1;
     if (d->source->has_next(d->source)) {
       vii_move_to_next_value(d);
-      if (!d->run_all)
-        d->timestamp_end_interval = ds_align(d, d->next_dp.ts) + d->interval;
+      if (!d->run_all) {
+        if (d->cal) {  /* Downsampler.java:333-343 */
+          d->prev_cal = cal_prev(d, d->next_dp.ts);
+          d->next_cal = cal_step(d, d->prev_cal);
+          d->timestamp_end_interval = cal_ts(d, d->next_cal);
+        } else {
+          d->timestamp_end_interval = ds_align(d, d->next_dp.ts) + d->interval;
+        }
+      }
     }
   }
 }
 
 static void vii_reset_end_of_interval(ds_view* d) {
-  if (d->has_next_value_from_source && !d->run_all)
-    d->timestamp_end_interval = ds_align(d, d->next_dp.ts) + d->interval;
+  if (d->has_next_value_from_source && !d->run_all) {
+    if (d->cal) {  /* Downsampler.java:383-397 */
+      while (d->next_dp.ts >= d->timestamp_end_interval) {
+        d->prev_cal = cal_step(d, d->prev_cal);
+        d->next_cal = cal_step(d, d->next_cal);
+        d->timestamp_end_interval = cal_ts(d, d->next_cal);
+      }
+    } else {
+      d->timestamp_end_interval = ds_align(d, d->next_dp.ts) + d->interval;
+    }
+  }
 }
 
 static void vii_move_to_next_interval(ds_view* d) {
@@ -562,6 +610,7 @@ static void vii_move_to_next_interval(ds_view* d) {
 
 static int64_t vii_interval_timestamp(ds_view* d) {
   if (d->run_all) return d->timestamp_end_interval;
+  if (d->cal) return cal_ts(d, d->prev_cal);  /* Downsampler.java:443-444 */
   return ds_align(d, d->timestamp_end_interval - d->interval);
 }
 
@@ -627,8 +676,15 @@ static void ds_next(view_t* v, dp_t* out) {
         default: jthrow(v->exc, OTSDB_E_UNSUPPORTED, "unhandled fill policy");
       }
     }
-    if (!d->run_all) d->f_timestamp += d->interval;
-    out->ts = d->run_all ? d->query_start : d->f_timestamp - d->interval;
+    if (d->cal) {  /* FillingDownsampler.java:276-284, :296-298 */
+      d->f_prev_cal += 1;
+      d->f_next_cal += 1;
+      d->f_timestamp = cal_ts(d, d->f_next_cal);
+      out->ts = cal_ts(d, d->f_prev_cal);
+    } else {
+      if (!d->run_all) d->f_timestamp += d->interval;
+      out->ts = d->run_all ? d->query_start : d->f_timestamp - d->interval;
+    }
   }
   out->is_int = 0;
   out->bits = d2bits(d->value);
@@ -637,8 +693,15 @@ static void ds_next(view_t* v, dp_t* out) {
 static void ds_seek(view_t* v, int64_t t) {
   ds_view* d = (ds_view*)v;
   /* ValuesInInterval.seekInterval, Downsampler.java:431 */
-  if (d->run_all) d->source->seek(d->source, t);
-  else d->source->seek(d->source, ds_align(d, t + d->interval - 1));
+  if (d->run_all) {
+    d->source->seek(d->source, t);
+  } else if (d->cal) {  /* Downsampler.java:431-441 */
+    int64_t k = cal_prev(d, t);
+    if (t > cal_ts(d, k)) k = cal_step(d, k);
+    d->source->seek(d->source, cal_ts(d, k));
+  } else {
+    d->source->seek(d->source, ds_align(d, t + d->interval - 1));
+  }
   d->initialized = 0;
 }
 
@@ -656,7 +719,11 @@ static void ds_init(ds_view* d, view_t* src, const otsdb_query_spec* s,
   d->query_start = s->query_start_ms;
   d->query_end = s->query_end_ms;
   d->next_dp_null = 1;
+  d->cal = s->use_calendar && !s->run_all;
+  d->edges = s->cal_edges;
+  d->n_edges = s->n_cal_edges;
   if (d->run_all) d->timestamp_end_interval = d->query_end;
+  else if (d->cal) d->timestamp_end_interval = JLONG_MIN;
   else d->timestamp_end_interval = d->interval;
   d->fill_policy = s->fill;
   d->filling = s->fill != OTSDB_FILL_NONE;
@@ -664,6 +731,13 @@ static void ds_init(ds_view* d, view_t* src, const otsdb_query_spec* s,
     if (d->run_all) {
       d->f_timestamp = start_time;
       d->f_end_timestamp = end_time;
+    } else if (d->cal) {  /* FillingDownsampler.java:113-131 */
+      d->f_next_cal = cal_prev(d, start_time);
+      d->f_prev_cal = d->f_next_cal - 1;
+      int64_t end_cal = cal_prev(d, end_time);
+      if (end_cal == d->f_next_cal) end_cal = cal_step(d, end_cal);
+      d->f_timestamp = cal_ts(d, d->f_next_cal);
+      d->f_end_timestamp = cal_ts(d, end_cal);
     } else {
       d->f_timestamp = ds_align(d, start_time);
       d->f_end_timestamp = ds_align(d, end_time);
@@ -1005,7 +1079,8 @@ static int spec_check(const otsdb_query_spec* s, exc_t* e) {
     if (s->ds_agg_id == OTSDB_AGG_NONE)
       jthrow(e, OTSDB_E_ILLEGAL_ARGUMENT,
              "cannot use the NONE aggregator for downsampling");
-    if (s->use_calendar) jthrow(e, OTSDB_E_UNSUPPORTED, "calendar downsampling");
+    if (s->use_calendar && !s->run_all && (!s->cal_edges || s->n_cal_edges < 2))
+      jthrow(e, OTSDB_E_UNSUPPORTED, "calendar downsampling without edges");
   }
   return 0;
 }

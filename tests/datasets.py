@@ -13,7 +13,7 @@ T0 = 1356998400000  # BaseTsdbTest base time, ms
 def random_batch(seed, n_series=40, n_groups=5, span_ms=3 * 3600 * 1000,
                  cadence_ms=10000, value_kind="float", nan_frac=0.0,
                  empty_frac=0.05, outside=True, counter=False,
-                 big_group=False):
+                 big_group=False, t0=T0):
     rng = np.random.default_rng(seed)
     offs = [0]
     tss, vals, isf = [], [], []
@@ -23,7 +23,7 @@ def random_batch(seed, n_series=40, n_groups=5, span_ms=3 * 3600 * 1000,
             continue
         n = span_ms // cadence_ms
         phase = int(rng.integers(0, cadence_ms))
-        t = T0 + phase + cadence_ms * np.arange(n, dtype=np.int64)
+        t = t0 + phase + cadence_ms * np.arange(n, dtype=np.int64)
         keep = rng.random(n) > 0.05
         # an outage
         if rng.random() < 0.4:

@@ -342,6 +342,382 @@ add(kind="scan_bounds", name="scan_ms", interval_ms=60000,
     cite="test/core/TestTsdbQueryDownsample.java:106-126")
 
 
+# ------------------------------------------------- calendar downsampling
+# test/core/TestDownsampler.java:390-1180, :1368-1400.  Each reference test
+# iterates `while (downsampler.hasNext())` and asserts every emitted point
+# against a sequence its loop computes; the loops are transcribed below as
+# generators (_seq_*).  The number of points is not asserted by most of those
+# tests: it is taken from bucketing the test's points on the calendar grid,
+# and the generator must agree with that bucketing on every point (checked
+# here at generation time) — so both the sequences and the counts are
+# pinned to the reference's literals.
+DST_TS = 1450137600000
+TZ_AF, TZ_TV, TZ_FJ = "Asia/Kabul", "Pacific/Funafuti", "Pacific/Fiji"
+
+
+def _cal_case(name, ds, tz, points, seq, cite, seek=None, n=None):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__)))))
+    from opentsdb_amd import jcalendar as J
+    iv, unit = J.parse_calendar_interval(ds.split("-")[0][:-1])
+    first = points[0][0] if seek is None else seek
+    edges = J.bucket_edges_for_series(min(first, points[0][0]),
+                                      points[-1][0], iv, unit, tz)
+    lo = 0
+    if seek is not None:
+        k = J.edge_index(edges, seek)
+        if seek > edges[k]:
+            k += 1
+        lo = edges[k]
+    sums = {}
+    for t, v, _ in points:
+        if t < lo:
+            continue
+        k = J.edge_index(edges, t)
+        sums[edges[k]] = sums.get(edges[k], 0) + v
+    got = sorted(sums.items())
+    if n is not None:
+        assert len(got) == n, (name, got)
+    exp = []
+    it = seq()
+    for _ in got:
+        exp.append(next(it))
+    assert [(t, float(v)) for t, v in got] == [(t, float(v)) for t, v in exp], (
+        name, got, exp)
+    add(kind="view", name=name,
+        spec=dict(ds_string=ds, tz=tz, query_start_ms=0, query_end_ms=LMAX),
+        points=points, seek=seek,
+        expect=[D(t, v) for t, v in exp], tol=1e-3, cite=cite)
+
+
+P6 = [L(BASE + 5000, 1), L(BASE + 15000, 2), L(BASE + 25000, 4),
+      L(BASE + 35000, 8), L(BASE + 45000, 16), L(BASE + 55000, 32)]
+
+
+def _seq_const(ts, v):
+    def g():
+        while True:
+            yield ts, v
+    return g
+
+
+# :390-416 testDownsampler_calendar (asserts exactly 1 point)
+_cal_case("cal_1dc_denver", "1dc-sum", "America/Denver", P6,
+          _seq_const(1356937200000, 63), "test/core/TestDownsampler.java:390-416",
+          n=1)
+PH = [L(BASE, 1), L(BASE + 1800000, 2), L(BASE + 3599000, 3),
+      L(BASE + 3600000, 4), L(BASE + 5400000, 5), L(BASE + 7199000, 6)]
+
+
+def _seq_hour_tv():
+    ts, v = BASE, 6
+    while True:
+        yield ts, v
+        ts += 3600000
+        v = 15
+
+
+def _seq_hour_af():
+    ts, v = 1356996600000, 1
+    while True:
+        yield ts, v
+        ts += 3600000
+        v = 9 if v == 1 else 11
+
+
+_cal_case("cal_1hc_tv", "1hc-sum", TZ_TV, PH, _seq_hour_tv,
+          "test/core/TestDownsampler.java:418-441")
+_cal_case("cal_1hc_af", "1hc-sum", TZ_AF, PH, _seq_hour_af,
+          "test/core/TestDownsampler.java:443-463")
+_cal_case("cal_4hc_af", "4hc-sum", TZ_AF, PH,
+          _seq_const(1356996600000, 21), "test/core/TestDownsampler.java:465-477")
+PD = [L(DST_TS, 1), L(DST_TS + 86399000, 2), L(DST_TS + 126001000, 3),
+      L(DST_TS + 172799000, 4), L(DST_TS + 172800000, 5),
+      L(DST_TS + 242999000, 6)]
+
+
+def _seq_day(ts, vals):
+    def g():
+        t, i = ts, 0
+        while True:
+            yield t, vals[min(i, len(vals) - 1)]
+            t += 86400000
+            i += 1
+    return g
+
+
+_cal_case("cal_1dc_utc", "1dc-sum", None, PD, _seq_day(DST_TS, [3, 7, 11]),
+          "test/core/TestDownsampler.java:480-506")
+_cal_case("cal_1dc_tv", "1dc-sum", TZ_TV, PD,
+          _seq_day(1450094400000, [1, 5, 9, 6]),
+          "test/core/TestDownsampler.java:508-530")
+_cal_case("cal_1dc_fj", "1dc-sum", TZ_FJ, PD,
+          _seq_day(1450090800000, [1, 2, 12, 6]),
+          "test/core/TestDownsampler.java:532-553")
+_cal_case("cal_1dc_af", "1dc-sum", TZ_AF, PD,
+          _seq_day(1450121400000, [1, 5, 15]),
+          "test/core/TestDownsampler.java:555-574")
+_cal_case("cal_3dc_af", "3dc-sum", TZ_AF, PD, _seq_const(1450121400000, 21),
+          "test/core/TestDownsampler.java:576-589")
+PW = [L(DST_TS, 1), L(DST_TS + 86400000 * 7, 2), L(1451129400000, 3),
+      L(DST_TS + 86400000 * 21, 4), L(1452367799000, 5)]
+
+
+def _seq_week_utc():
+    ts, v = 1449964800000, 1
+    while True:
+        yield ts, v
+        ts = 1451779200000 if ts == 1450569600000 else ts + 86400000 * 7
+        v = 5 if v == 1 else 9
+
+
+def _seq_week_tv():
+    ts, v = 1449921600000, 1
+    while True:
+        yield ts, v
+        ts = 1451736000000 if ts == 1450526400000 else ts + 86400000 * 7
+        v = 5 if v == 1 else (4 if v == 5 else 5)
+
+
+def _seq_week_fj():
+    ts, v = 1449918000000, 1
+    while True:
+        yield ts, v
+        ts += 86400000 * 7
+        v += 1
+
+
+def _seq_week_af():
+    ts, v = 1449948600000, 1
+    while True:
+        yield ts, v
+        ts = 1450553400000 if ts == 1449948600000 else 1451763000000
+        v = 5 if v == 1 else 9
+
+
+def _seq_2week_af():
+    ts, v = 1449948600000, 6
+    while True:
+        yield ts, v
+        ts, v = 1451158200000, 9
+
+
+_cal_case("cal_1wc_utc", "1wc-sum", None, PW, _seq_week_utc,
+          "test/core/TestDownsampler.java:591-626")
+_cal_case("cal_1wc_tv", "1wc-sum", TZ_TV, PW, _seq_week_tv,
+          "test/core/TestDownsampler.java:628-653")
+_cal_case("cal_1wc_fj", "1wc-sum", TZ_FJ, PW, _seq_week_fj,
+          "test/core/TestDownsampler.java:655-670")
+_cal_case("cal_1wc_af", "1wc-sum", TZ_AF, PW, _seq_week_af,
+          "test/core/TestDownsampler.java:672-695")
+_cal_case("cal_2wc_af", "2wc-sum", TZ_AF, PW, _seq_2week_af,
+          "test/core/TestDownsampler.java:697-713")
+DEC1 = 1448928000000
+PM = [L(DEC1, 1), L(1451559600000, 2), L(1451606400000, 3),
+      L(1454284800000, 4), L(1456704000000, 5), L(1456772400000, 6)]
+
+
+def _seq_month_utc():
+    ts, v = DEC1, 3
+    while True:
+        yield ts, v
+        if ts == 1448928000000:
+            ts = 1451606400000
+        else:
+            ts, v = 1454284800000, 15
+
+
+def _seq_month_tv():
+    ts, v = 1448884800000, 3
+    while True:
+        yield ts, v
+        if ts == 1448884800000:
+            ts = 1451563200000
+        elif ts == 1451563200000:
+            v, ts = 9, 1454241600000
+        else:
+            ts, v = 1456747200000, 6
+
+
+def _seq_month_af():
+    ts, v = 1448911800000, 3
+    while True:
+        yield ts, v
+        if ts == 1448911800000:
+            ts = 1451590200000
+        else:
+            ts, v = 1454268600000, 15
+
+
+def _seq_3month_tv():
+    ts, v = 1443614400000, 3
+    while True:
+        yield ts, v
+        ts, v = 1451563200000, 18
+
+
+_cal_case("cal_1nc_utc", "1nc-sum", None, PM, _seq_month_utc,
+          "test/core/TestDownsampler.java:715-742")
+_cal_case("cal_1nc_tv", "1nc-sum", TZ_TV, PM, _seq_month_tv,
+          "test/core/TestDownsampler.java:744-766")
+_cal_case("cal_1nc_af", "1nc-sum", TZ_AF, PM, _seq_month_af,
+          "test/core/TestDownsampler.java:791-808")
+_cal_case("cal_3nc_tv", "3nc-sum", TZ_TV, PM, _seq_3month_tv,
+          "test/core/TestDownsampler.java:810-824")
+
+
+def _seq_pairs(ts_list, npts):
+    """(1 << j++) + (1 << j++) per bucket over the given bucket starts."""
+    def g():
+        j = 0
+        for t in ts_list:
+            yield t, float((1 << j) + (1 << (j + 1)))
+            j += 2
+    return g
+
+
+def _month_points(t0_list):
+    """testDownsampler_1month's data: two points per bucket, at the bucket
+    start and half way to the next start (+1 for the UTC case)."""
+    pts = []
+    for i, (a, b) in enumerate(zip(t0_list, t0_list[1:])):
+        pts.append(L(a, 1 << (2 * i)))
+        pts.append(L(a + (b - a) // 2, 1 << (2 * i + 1)))
+    return pts
+
+
+# :937-960 testDownsampler_1month (UTC; bucket starts = Calendar month
+# starts from Jan 2013; the second point sits at (start + (next+1)) / 2)
+_M13 = [1356998400000, 1359676800000, 1362096000000, 1364774400000,
+        1367366400000, 1370044800000, 1372636800000, 1375315200000,
+        1377993600000, 1380585600000, 1383264000000, 1385856000000,
+        1388534400000]
+_pts = []
+for _i in range(12):
+    _a, _b = _M13[_i], _M13[_i + 1] + 1
+    _pts.append(L(_a, 1 << (2 * _i)))
+    _pts.append(L(_a + (_b - _a) // 2, 1 << (2 * _i + 1)))
+_cal_case("cal_1nc_utc_12", "1nc-sum", None, _pts, _seq_pairs(_M13[:12], 24),
+          "test/core/TestDownsampler.java:937-960", n=12)
+# :1110-1135 testDownsampler_1year (UTC, 2 buckets)
+_Y = [1356998400000, 1388534400000, 1420070400000]
+_cal_case("cal_1yc_utc", "1yc-sum", None, _month_points(_Y),
+          _seq_pairs(_Y[:2], 4), "test/core/TestDownsampler.java:1110-1135",
+          n=2)
+# :1368-1400 testSeek_useCalendar (second half: "1yc-sum", seek one ms past
+# 2015-01-01 -> only 2016's bucket)
+PY = [L(1356998400000, 1), L(1388534400000, 2), L(1420070400000, 4),
+      L(1451606400000, 8)]
+_cal_case("cal_seek_1yc", "1yc-sum", None, PY, _seq_const(1451606400000, 8),
+          "test/core/TestDownsampler.java:1387-1397", seek=1420070400001, n=1)
+
+
+def _seq_seek_exact():
+    yield 1420070400000, 4
+    yield 1451606400000, 8
+
+
+_cal_case("cal_seek_1yc_exact", "1yc-sum", None, PY, _seq_seek_exact,
+          "test/core/TestDownsampler.java:1368-1386", seek=1420070400000, n=2)
+
+
+# --------------------------------------- DateTime.previousInterval KATs
+# test/utils/TestDateTime.java:548-963 (assertEquals(expected,
+# previousInterval(ts, interval, unit[, tz]))), transcribed as data.
+# Units as DateTime.unitsToCalendarType names them ("w" = DAY_OF_WEEK);
+# WEEK_OF_YEAR is not reachable from a downsampling spec and is skipped.
+_D, _N = 1450152145123, 1431699673432   # DST_TS, NON_DST_TS
+_AF, _NZ, _TV, _FJ = "Asia/Kabul", "Pacific/Chatham", "Pacific/Funafuti", \
+    "Pacific/Fiji"
+_PI = [
+    # previousIntervalMilliseconds :548-589
+    (_D, 1, "ms", None, _D), (_N, 1, "ms", None, _N),
+    (_D, 100, "ms", None, 1450152145100), (1450152145000, 100, "ms", None,
+                                           1450152145000),
+    (_D, 799, "ms", None, 1450152144769),
+    (_D, 100, "ms", _AF, 1450152145100), (_N, 100, "ms", _AF, 1431699673400),
+    (_D, 100, "ms", _NZ, 1450152145100), (_N, 100, "ms", _NZ, 1431699673400),
+    (_D, 100, "ms", _TV, 1450152145100), (_N, 100, "ms", _TV, 1431699673400),
+    (_D, 100, "ms", _FJ, 1450152145100), (_N, 100, "ms", _FJ, 1431699673400),
+    (_D, 60000, "ms", None, 1450152120000), (_N, 60000, "ms", None,
+                                             1431699660000),
+    # previousIntervalSeconds :591-636
+    (_D, 1, "s", None, 1450152145000), (_N, 1, "s", None, 1431699673000),
+    (_D, 30, "s", None, 1450152120000), (_N, 30, "s", None, 1431699660000),
+    (1450152120000, 30, "s", None, 1450152120000),
+    (_N, 29, "s", None, 1431699647000), (_D, 29, "s", None, 1450152145000),
+    (_D, 30, "s", _AF, 1450152120000), (_N, 30, "s", _AF, 1431699660000),
+    (_D, 30, "s", _NZ, 1450152120000), (_N, 30, "s", _NZ, 1431699660000),
+    (_D, 30, "s", _TV, 1450152120000), (_N, 30, "s", _TV, 1431699660000),
+    (_D, 30, "s", _FJ, 1450152120000), (_N, 30, "s", _FJ, 1431699660000),
+    (_D, 60000, "s", None, 1450152000000), (_N, 60000, "s", None,
+                                            1431698400000),
+    # previousIntervalMinutes :638-690
+    (_D, 1, "m", None, 1450152120000), (_N, 1, "m", None, 1431699660000),
+    (_D, 30, "m", None, 1450152000000), (_N, 30, "m", None, 1431698400000),
+    (1431698400000, 30, "m", None, 1431698400000),
+    (_N, 29, "m", None, 1431698460000), (_D, 29, "m", None, 1450151520000),
+    (_D, 30, "m", _AF, 1450152000000), (_N, 30, "m", _AF, 1431698400000),
+    (_D, 15, "m", _AF, 1450152000000), (_N, 15, "m", _AF, 1431699300000),
+    (_D, 30, "m", _NZ, 1450151100000), (_N, 30, "m", _NZ, 1431699300000),
+    (_D, 30, "m", _TV, 1450152000000), (_N, 30, "m", _TV, 1431698400000),
+    (_D, 30, "m", _FJ, 1450152000000), (_N, 30, "m", _FJ, 1431698400000),
+    (_D, 120, "m", None, 1450152000000), (_N, 120, "m", None, 1431698400000),
+    # previousIntervalHours :692-739
+    (_D, 1, "h", None, 1450152000000), (_N, 1, "h", None, 1431698400000),
+    (_D, 12, "h", None, 1450137600000), (_N, 12, "h", None, 1431691200000),
+    (1450137600000, 12, "h", None, 1450137600000),
+    (_N, 15, "h", None, 1431680400000), (_D, 15, "h", None, 1450116000000),
+    (_D, 12, "h", _AF, 1450121400000), (_N, 12, "h", _AF, 1431675000000),
+    (_D, 12, "h", _NZ, 1450131300000), (_N, 12, "h", _NZ, 1431688500000),
+    (_D, 12, "h", _TV, 1450137600000), (_N, 12, "h", _TV, 1431691200000),
+    (_D, 12, "h", _FJ, 1450134000000), (_N, 12, "h", _FJ, 1431691200000),
+    (_D, 36, "h", None, 1450094400000), (_N, 36, "h", None, 1431604800000),
+    # previousIntervalDays :741-787
+    (_D, 1, "d", None, 1450137600000), (_N, 1, "d", None, 1431648000000),
+    (_D, 7, "d", None, 1449705600000), (_N, 7, "d", None, 1431561600000),
+    (1449705600000, 7, "d", None, 1449705600000),
+    (1330516800000, 1, "d", None, 1330473600000),
+    (_D, 1, "d", _AF, 1450121400000), (_N, 1, "d", _AF, 1431631800000),
+    (_D, 1, "d", _NZ, 1450088100000), (_N, 1, "d", _NZ, 1431688500000),
+    (_D, 1, "d", _TV, 1450094400000), (_N, 1, "d", _TV, 1431691200000),
+    (_D, 1, "d", _FJ, 1450090800000), (_N, 1, "d", _FJ, 1431691200000),
+    (_D, 60, "d", None, 1445990400000), (_N, 60, "d", None, 1430438400000),
+    # previousIntervalWeeks :789-833 (Locale.US: weeks start on Sunday)
+    (_D, 1, "w", None, 1449964800000), (_N, 1, "w", None, 1431216000000),
+    (_D, 2, "w", None, 1449964800000), (_N, 2, "w", None, 1431216000000),
+    (1435795200000, 2, "w", None, 1435449600000),
+    (_D, 1, "w", _AF, 1449948600000), (_N, 1, "w", _AF, 1431199800000),
+    (_D, 1, "w", _NZ, 1449915300000), (_N, 1, "w", _NZ, 1431170100000),
+    (_D, 1, "w", _TV, 1449921600000), (_N, 1, "w", _TV, 1431172800000),
+    (_D, 1, "w", _FJ, 1449918000000), (_N, 1, "w", _FJ, 1431172800000),
+    (_D, 104, "w", None, 1449964800000), (_N, 104, "w", None, 1431216000000),
+    # previousIntervalMonths :878-925
+    (_D, 1, "n", None, 1448928000000), (_N, 1, "n", None, 1430438400000),
+    (_D, 3, "n", None, 1443657600000), (_N, 3, "n", None, 1427846400000),
+    (1443657600000, 3, "n", None, 1443657600000),
+    (_D, 5, "n", None, 1446336000000), (_N, 5, "n", None, 1420070400000),
+    (_D, 1, "n", _AF, 1448911800000), (_N, 1, "n", _AF, 1430422200000),
+    (_D, 1, "n", _NZ, 1448878500000), (_N, 1, "n", _NZ, 1430392500000),
+    (_D, 1, "n", _TV, 1448884800000), (_N, 1, "n", _TV, 1430395200000),
+    (_D, 1, "n", _FJ, 1448881200000), (_N, 1, "n", _FJ, 1430395200000),
+    (_D, 24, "n", None, 1420070400000), (_N, 24, "n", None, 1420070400000),
+    # previousIntervalYears :927-962
+    (_D, 1, "y", None, 1420070400000), (_N, 1, "y", None, 1420070400000),
+    (_D, 5, "y", None, 1420070400000), (_N, 5, "y", None, 1420070400000),
+    (1420070400000, 5, "y", None, 1420070400000),
+    (_D, 1, "y", _AF, 1420054200000), (_N, 1, "y", _AF, 1420054200000),
+    (_D, 1, "y", _NZ, 1420020900000), (_N, 1, "y", _NZ, 1420020900000),
+    (_D, 1, "y", _TV, 1420027200000), (_N, 1, "y", _TV, 1420027200000),
+    (_D, 1, "y", _FJ, 1420023600000), (_N, 1, "y", _FJ, 1420023600000),
+]
+for _k, (_t, _iv, _u, _tz, _e) in enumerate(_PI):
+    add(kind="prev_interval", name="prev_%d_%s%s_%s" % (_k, _iv, _u, _tz),
+        ts=_t, interval=_iv, unit=_u, tz=_tz, expect=_e,
+        cite="test/utils/TestDateTime.java:548-963")
+
+
 def _enc(x):
     if isinstance(x, float):
         if math.isnan(x):

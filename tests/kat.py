@@ -26,9 +26,24 @@ def dec(x):
     return x
 
 
-def spec_from_case(d):
+def view_cal_edges(d, points, seek=None):
+    """Calendar grid of a lone Downsampler over one series: anchored at its
+    first point (the seek position when seeked), Downsampler.java:330-345."""
+    from opentsdb_amd import jcalendar as J
+    ds = core.DownsamplingSpecification(d["ds_string"])
+    n, unit = ds.calendar_interval()
+    first = points[0][0] if seek is None else min(seek, points[0][0])
+    return J.bucket_edges_for_series(first, points[-1][0], n, unit,
+                                     d.get("tz"))
+
+
+def spec_from_case(d, cal_edges=None):
     ds = None
-    if d.get("ds_interval_ms"):
+    if d.get("ds_string"):
+        ds = core.DownsamplingSpecification(d["ds_string"])
+        if d.get("tz"):
+            ds.setTimezone(d["tz"])
+    elif d.get("ds_interval_ms"):
         ds = core.DownsamplingSpecification(
             interval_ms=d["ds_interval_ms"],
             function=core.Aggregators.get(d["ds_agg"]),
@@ -42,7 +57,8 @@ def spec_from_case(d):
         core.Aggregators.get(d.get("agg", "sum")), ds,
         d.get("query_start_ms", 0), d.get("query_end_ms", 0),
         d.get("rate", False), ro,
-        None if interp is None else core.Interpolation[interp])
+        None if interp is None else core.Interpolation[interp],
+        cal_edges=cal_edges)
 
 
 def batch_from_case(c):

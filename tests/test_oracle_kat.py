@@ -37,8 +37,11 @@ def test_agg_double(c):
 
 @pytest.mark.parametrize("c", kat.load_cases("view"), ids=lambda c: c["name"])
 def test_view(c):
-    spec = kat.spec_from_case(c["spec"])
     pts = c["points"]
+    edges = None
+    if c["spec"].get("ds_string", "").split("-")[0].endswith("c"):
+        edges = kat.view_cal_edges(c["spec"], pts, c.get("seek"))
+    spec = kat.spec_from_case(c["spec"], edges)
     ts = [p[0] for p in pts]
     bits = [np.float64(kat.dec(p[1])).view(np.int64) if p[2] else int(p[1])
             for p in pts]
@@ -102,3 +105,14 @@ def test_decode_row_seconds_and_ms():
         base * 1000 + 1500]
     assert [kat.point_value(b, i) for b, i in zip(got["bits"], got["is_int"])] \
         == [-2, 300, 2.5, -7]
+
+
+@pytest.mark.parametrize("c", kat.load_cases("prev_interval"),
+                         ids=lambda c: c["name"])
+def test_previous_interval(c):
+    """The calendar-grid anchor (host side of calendar downsampling) against
+    DateTime.previousInterval's own known answers."""
+    from opentsdb_amd import jcalendar
+    got = jcalendar.previous_interval(c["ts"], c["interval"], c["unit"],
+                                      c["tz"])
+    assert got == c["expect"], (got, c["expect"])
