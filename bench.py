@@ -98,11 +98,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (a multi-rank run on a one-GPU box): every rank on
+    # device 0 and gloo instead of RCCL; the driver's runs use neither
+    if os.environ.get("OTSDB_BENCH_SAME_DEVICE"):
+        local = 0
+    backend = os.environ.get("OTSDB_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl",
+                                    device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     cfg = workload.CONFIGS[args.config]
     n_series = args.series or workload.default_series_per_gpu(args.config)
@@ -160,10 +169,11 @@ def main():
     total_points = n_points * world
     out_points = int((_last if sharded else res).offsets[-1].item())
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dev = "cuda" if backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tp = torch.tensor([n_points], dtype=torch.int64, device="cuda")
+        tp = torch.tensor([n_points], dtype=torch.int64, device=dev)
         dist.all_reduce(tp)
         total_points = int(tp.item())
     step_s = elapsed / args.steps

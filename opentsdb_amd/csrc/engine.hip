@@ -137,6 +137,8 @@ struct Work {
   uint64_t* keys = nullptr;
   SelState* sel = nullptr;
   uint32_t* hist = nullptr;
+  Packed* comb = nullptr;      // two-level combine: first-level slices
+  uint8_t* comb_emit = nullptr;
 };
 
 }  // namespace
@@ -156,6 +158,7 @@ struct otsdb_ctx {
   int64_t* d_tiles = nullptr;
   size_t d_tiles_cap = 0;
   int64_t n_tiles = 0, n_multi = 0, n_large = 0, n_large_chunks = 0;
+  int64_t max_chunks = 0;  // most chunks in one group
   bool tiles_sel_all = false;
   std::mutex mu;  // one query at a time per context
   // stage timing (otsdb_prof_*)
@@ -404,6 +407,8 @@ otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff,
   }
   const int64_t LG = (int64_t)lgg.size();
   const int64_t T = (int64_t)tg.size(), MG = (int64_t)mg.size();
+  int64_t max_chunks = 0;
+  for (int64_t k = 0; k < G; ++k) max_chunks = std::max(max_chunks, at1[k] - at0[k]);
   // layout: tg tm0 tm1 [T] | mg mt0 mt1 [MG] | ag at0 at1 [G] |
   //         lg_g lg_off lg_k [LG] | lg_ch0 [LG+1] | single [T]
   const size_t n64 = 3 * T + 3 * MG + 3 * G + 4 * LG + 1;
@@ -442,6 +447,7 @@ otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff,
   c->n_multi = MG;
   c->n_large = LG;
   c->n_large_chunks = lgc.back();
+  c->max_chunks = max_chunks;
   return OTSDB_OK;
 }
 
@@ -450,6 +456,7 @@ struct Tiles {
   const int64_t *lg_g, *lg_off, *lg_k, *lg_ch0;
   const uint8_t* single;
   int64_t T, MG, G, LG, LGCH;
+  int64_t max_chunks;
 };
 
 Tiles tiles_of(otsdb_ctx* c, int64_t G) {
@@ -476,8 +483,16 @@ Tiles tiles_of(otsdb_ctx* c, int64_t G) {
   t.T = T;
   t.MG = MG;
   t.G = G;
+  t.max_chunks = c->max_chunks;
   return t;
 }
+
+// two-level ordered combine for groups of more than kCombineL1 chunks: the
+// single-level k_combine is one dependent chain of max_chunks loads per
+// (group, bucket) thread (C4: 1,953 chunks, 1.9 ms); first-level slices
+// cut it to ~max_chunks / kCombineSlices
+constexpr int64_t kCombineL1 = 128;
+constexpr int64_t kCombineSlices = 64;
 
 // Brackets a pipeline stage with HIP events when profiling is enabled.
 struct StageTimer {
@@ -528,6 +543,30 @@ bool bucketize_uses_ring(int code, int ds_agg) {
   return true;
 }
 
+template <class M>
+void launch_combine(otsdb_ctx* c, const Work& W, int64_t NB, int64_t n,
+                    const int64_t* g, const int64_t* t0, const int64_t* t1,
+                    double* out_val, uint8_t* out_emit, Packed* out_partial,
+                    bool two_level) {
+  hipStream_t st = c->stream;
+  if (!two_level) {
+    hipLaunchKernelGGL(k_combine<M>, dim3(blocks_for(n * NB, 256)), dim3(256),
+                       0, st, NB, n, g, t0, t1, (const Packed*)W.partial,
+                       (const uint8_t*)W.tile_emit, out_val, out_emit,
+                       out_partial, c->d_err, (int64_t)0);
+    return;
+  }
+  hipLaunchKernelGGL(k_combine_l1<M>,
+                     dim3(blocks_for(n * kCombineSlices * NB, 256)), dim3(256),
+                     0, st, NB, n, kCombineSlices, t0, t1,
+                     (const Packed*)W.partial, (const uint8_t*)W.tile_emit,
+                     W.comb, W.comb_emit);
+  hipLaunchKernelGGL(k_combine<M>, dim3(blocks_for(n * NB, 256)), dim3(256), 0,
+                     st, NB, n, g, t0, t1, (const Packed*)W.comb,
+                     (const uint8_t*)W.comb_emit, out_val, out_emit,
+                     out_partial, c->d_err, kCombineSlices);
+}
+
 // Everything up to dense (group, bucket) results / partials.
 // mode 0: final dense results; mode 1: per-group partials into `gpart/gemit`
 otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
@@ -571,6 +610,9 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
 
   // workspace
   const bool sel_large = is_selection(spec->agg_id) && (T.LG > 0 || mode == 2);
+  const int64_t n_comb = (mode == 1) ? G : T.MG;
+  const bool two_level = T.max_chunks > kCombineL1 &&
+                         (double)n_comb * kCombineSlices * NB * 33.0 < 2.0e9;
   auto carve = [&](char* base) {
     Carve cv{base};
     W.SM.lo = cv.take<int64_t>(S);
@@ -586,6 +628,10 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     W.out_val = cv.take<double>((size_t)G * NB);
     W.out_emit = cv.take<uint8_t>((size_t)G * NB);
     W.counts = cv.take<int64_t>(G + 1);
+    if (two_level) {
+      W.comb = cv.take<Packed>((size_t)n_comb * kCombineSlices * NB);
+      W.comb_emit = cv.take<uint8_t>((size_t)n_comb * kCombineSlices * NB);
+    }
     if (sel_large) {
       W.keys = cv.take<uint64_t>((size_t)goff.back() * NB);
       W.sel = cv.take<SelState>((size_t)T.LG * NB);
@@ -762,8 +808,20 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   }
   if (S > 0 && NB > 0) {
     StageTimer tm(c, 1);
-    hipLaunchKernelGGL(k_transform, dim3(blocks_for(S, 4)), dim3(256), 0, st,
-                       P, B, W.SM, W.R, c->d_err);
+    // rate rows of up to 2,048 buckets stay in registers between the two
+    // RateSpan passes (one row read, one write)
+    auto L = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(blocks_for(S, 4)), dim3(256), 0, st, P, B,
+                         W.SM, W.R, c->d_err);
+    };
+    static const int64_t reg_max = [] {
+      const char* e = getenv("OTSDB_TRANSFORM_REG_MAX");  // tuning knob
+      return e ? (int64_t)atoll(e) : (int64_t)0;
+    }();
+    if (!P.rate || NB > reg_max) L(k_transform<0>);
+    else if (NB <= 512) L(k_transform<8>);
+    else if (NB <= 1024) L(k_transform<16>);
+    else L(k_transform<32>);
   }
   if (G > 0 && NB > 0) {
     StageTimer tm(c, 2);
@@ -780,10 +838,8 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
                            T.single, d_members, W.R, W.partial, W.tile_emit,
                            W.out_val, W.out_emit, c->d_err, 0);
       if (T.MG > 0)
-        hipLaunchKernelGGL(k_combine<MC>, dim3(blocks_for(T.MG * NB, 256)),
-                           dim3(256), 0, st, NB, T.MG, T.mg, T.mt0, T.mt1,
-                           W.partial, W.tile_emit, W.out_val, W.out_emit,
-                           (Packed*)nullptr, c->d_err);
+        launch_combine<MC>(c, W, NB, T.MG, T.mg, T.mt0, T.mt1, W.out_val,
+                           W.out_emit, nullptr, two_level);
       if (mode == 2) {
         // cross-rank protocol: local counts + keys only (otsdb_sel_*)
         const int64_t M = goff.back();
@@ -810,19 +866,13 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         hipLaunchKernelGGL(k_sel_init, dim3(blocks_for(NSEG, 256)), dim3(256),
                            0, st, NB, T.LG, T.lg_g, (const double*)W.out_val,
                            (const uint8_t*)W.out_emit, W.sel, median, P.pct);
-        HIP_TRY(hipMemsetAsync(W.hist, 0, (size_t)NSEG * 512 * 4, st));
-        for (int pass = 0; pass < 8; ++pass) {
-          hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)(T.LGCH * NB)),
-                             dim3(256), 0, st, pass, NB, M, T.LG, T.lg_off,
-                             T.lg_k, T.lg_ch0, (const uint64_t*)W.keys,
-                             (const SelState*)W.sel, W.hist);
-          hipLaunchKernelGGL(k_radix_select, dim3(blocks_for(NSEG * 2, 256)),
-                             dim3(256), 0, st, pass, NSEG, W.hist, W.sel);
-        }
-        hipLaunchKernelGGL(k_sel_finish, dim3(blocks_for(NSEG, 256)),
-                           dim3(256), 0, st, NB, T.LG, T.lg_g,
-                           (const SelState*)W.sel, (const uint8_t*)W.out_emit,
-                           W.out_val, c->d_err, median, P.pct);
+        // one workgroup per (group, bucket) segment: min/max, 11-bit digit
+        // passes until <= SS_CAP candidates, LDS gather + count select
+        hipLaunchKernelGGL(k_seg_select, dim3((unsigned)NSEG), dim3(SS_THREADS),
+                           0, st, NB, M, T.LG, T.lg_g, T.lg_off, T.lg_k,
+                           (const uint64_t*)W.keys, (const SelState*)W.sel,
+                           (const uint8_t*)W.out_emit, W.out_val, c->d_err,
+                           median, P.pct);
       }
     } else {
       ok = with_monoid(spec->agg_id, [&](auto tag) {
@@ -834,15 +884,11 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
                              W.out_val, W.out_emit, c->d_err, mode);
         if (mode == 0) {
           if (T.MG > 0)
-            hipLaunchKernelGGL(k_combine<M>, dim3(blocks_for(T.MG * NB, 256)),
-                               dim3(256), 0, st, NB, T.MG, T.mg, T.mt0, T.mt1,
-                               W.partial, W.tile_emit, W.out_val, W.out_emit,
-                               (Packed*)nullptr, c->d_err);
+            launch_combine<M>(c, W, NB, T.MG, T.mg, T.mt0, T.mt1, W.out_val,
+                              W.out_emit, nullptr, two_level);
         } else {
-          hipLaunchKernelGGL(k_combine<M>, dim3(blocks_for(G * NB, 256)),
-                             dim3(256), 0, st, NB, G, T.ag, T.at0, T.at1,
-                             W.partial, W.tile_emit, W.out_val, gemit, gpart,
-                             c->d_err);
+          launch_combine<M>(c, W, NB, G, T.ag, T.at0, T.at1, W.out_val, gemit,
+                            gpart, two_level);
         }
       });
       if (!ok) return fail(OTSDB_E_NO_SUCH_ELEMENT, "aggregator %d", spec->agg_id);

@@ -261,43 +261,6 @@ DEV int bucket_narrow(const Params& P, int64_t ts) {
   return (int)q;
 }
 
-// Fast lane fold for lanes whose K points fall into at most two adjacent
-// buckets (the common case when buckets hold more than K points).  Points are
-// sorted by time, so only the first and last point need a bucket index: the
-// lane spans buckets k0..k1, and with k1 <= k0 + 1 every point before the
-// start of bucket k1 belongs to k0 (a prefix, the head run) and the rest to
-// k1.  Both runs accumulate branch free with masked pushes, in point order.
-// Returns false (nothing changed) when the lane spans three or more buckets.
-template <class M, int K, bool FLOATONLY>
-DEV bool fold_fast(const Params& P, const BatchDev& B, int sf, int64_t i0,
-                   const int64_t* t, const int64_t* v, int& nseg, int& cur_key,
-                   int& head_key, M& cur, M& head) {
-  const int k0 = bucket_narrow(P, t[0]), k1 = bucket_narrow(P, t[K - 1]);
-  if (k1 - k0 > 1) return false;
-  // start of bucket k1; INT64_MIN sends every point to the one run
-  const int64_t bnd =
-      (k1 == k0) ? INT64_MIN : P.gbase + (int64_t)k1 * P.interval;
-  M h = M::init(), c = M::init();
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const double x =
-        FLOATONLY ? bits_to_double(v[j]) : point_value(B, i0 + j, v[j], sf);
-    const bool inh = t[j] < bnd;
-    h.push_if(inh, x);
-    c.push_if(!inh, x);
-  }
-  head_key = k0;
-  cur_key = k1;
-  cur = c;
-  if (k0 == k1) {
-    nseg = 1;
-  } else {
-    nseg = 2;
-    head = h;
-  }
-  return true;
-}
-
 DEV void wait_vmcnt(int n) {
   // s_waitcnt vmcnt(n) (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14,
   // expcnt and lgkmcnt at their no-wait maxima)
@@ -358,6 +321,55 @@ DEV void sink_flush(RowSink& S, int64_t& flushed, int64_t limit) {
     }
   }
   if (limit > flushed) flushed = limit;
+}
+
+// Fast lane fold for lanes whose K points fall into at most three adjacent
+// buckets (the common case when buckets hold more than K/2 points; a 1 m
+// bucket of 10 s points puts a lane's 8 points in 2 or 3 buckets).  Points
+// are sorted by time, so only the first and last point need a bucket index:
+// the lane spans buckets k0..k1 (k1 <= k0 + 2), every point before the start
+// of bucket k0+1 belongs to k0 (the head run), every point from the start of
+// k1 on to k1 (the tail run) and the rest to k0+1, a bucket wholly inside
+// the lane that closes here.  All runs accumulate branch free with masked
+// pushes, in point order.  Returns false (nothing changed) when the lane
+// spans four or more buckets.
+template <class M, int K, bool FLOATONLY>
+DEV bool fold_fast(const Params& P, const BatchDev& B, int sf, int64_t i0,
+                   const int64_t* t, const int64_t* v, RowSink& S, int& err,
+                   int& nseg, int& cur_key, int& head_key, M& cur, M& head) {
+  const int k0 = bucket_narrow(P, t[0]), k1 = bucket_narrow(P, t[K - 1]);
+  if (k1 - k0 > 2) return false;
+  // starts of the tail bucket k1 and of the middle bucket k0+1 (INT64_MIN
+  // sends every point to the tail run)
+  const int64_t b_tail =
+      (k1 == k0) ? INT64_MIN : P.gbase + (int64_t)k1 * P.interval;
+  const int64_t b_mid =
+      (k1 == k0 + 2) ? P.gbase + (int64_t)(k0 + 1) * P.interval : b_tail;
+  M h = M::init(), m = M::init(), c = M::init();
+  bool any_mid = false;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const double x =
+        FLOATONLY ? bits_to_double(v[j]) : point_value(B, i0 + j, v[j], sf);
+    const bool inh = t[j] < b_mid;
+    const bool inc = t[j] >= b_tail;
+    const bool inm = !inh && !inc;
+    h.push_if(inh, x);
+    m.push_if(inm, x);
+    c.push_if(inc, x);
+    any_mid |= inm;
+  }
+  head_key = k0;
+  cur_key = k1;
+  cur = c;
+  if (k0 == k1) {
+    nseg = 1;
+  } else {
+    nseg = any_mid ? 3 : 2;
+    head = h;
+    if (any_mid) S.put(k0 + 1, m.finish(&err));
+  }
+  return true;
 }
 
 // Folds the K points of one lane in order: the first run (which may continue
@@ -449,9 +461,9 @@ DEV void reduce_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
     const bool fonly = !B.is_float && sf;
     bool done = false;
     if (P.narrow) {
-      done = fonly ? fold_fast<M, K, true>(P, B, sf, i0, t, v, nseg, cur_key,
-                                           head_key, cur, head)
-                   : fold_fast<M, K, false>(P, B, sf, i0, t, v, nseg,
+      done = fonly ? fold_fast<M, K, true>(P, B, sf, i0, t, v, S, err, nseg,
+                                           cur_key, head_key, cur, head)
+                   : fold_fast<M, K, false>(P, B, sf, i0, t, v, S, err, nseg,
                                             cur_key, head_key, cur, head);
     }
     if (!done) {
@@ -790,6 +802,16 @@ DEV double interp_value(int method, int64_t x, int64_t x0, double y0,
 //  * otherwise interpolation between the series' own points (:754-793),
 //    contributing iff first <= x <= last (or a point exists past the window).
 // ------------------------------------------------------------------------
+template <int NCH>
+__global__ __launch_bounds__(256) void k_transform(Params P, BatchDev B,
+                                                   SeriesMeta SM, Rows R,
+                                                   int* err_word);
+template <int NCH>
+DEV void transform_rate(const Params& P, const SeriesMeta& SM, int64_t s,
+                        double* rowv, uint8_t* rows, bool sent, bool fill,
+                        int64_t kf, int64_t kl, int* err_word);
+
+template <int NCH>
 __global__ __launch_bounds__(256) void k_transform(Params P, BatchDev B,
                                                    SeriesMeta SM, Rows R,
                                                    int* err_word) {
@@ -838,9 +860,15 @@ __global__ __launch_bounds__(256) void k_transform(Params P, BatchDev B,
     const bool of = SM.of_has[s] != 0;
     int64_t carry_idx = -1;
     double carry_val = 0.0;
+    // row values two chunks ahead: the chunk loop is a dependent chain, an
+    // unprefetched load per chunk costs a full HBM latency
+    double va = lane < nb ? rowv[lane] : 0.0;
+    double vn = lane + 64 < nb ? rowv[lane + 64] : 0.0;
     for (int64_t c0 = 0; c0 < nb; c0 += 64) {
       const int64_t b = c0 + lane;
-      const double vb = b < nb ? rowv[b] : 0.0;
+      const double vb = va;
+      va = vn;
+      vn = b + 128 < nb ? rowv[b + 128] : 0.0;
       const bool p = b < nb && real_at(b, vb);
       const double v = p ? vb : 0.0;
       if (sent && b < nb)  // every state of the row, written once
@@ -848,28 +876,33 @@ __global__ __launch_bounds__(256) void k_transform(Params P, BatchDev B,
                     : (((b > kf && b < kl) || (of && kf <= kl && b > kl))
                            ? ST_INTERP
                            : ST_ABSENT);
-      const int64_t incl = wave_incl_max(p ? b : -1);
-      int64_t prev = __shfl_up(incl, 1);
-      if (lane == 0) prev = -1;
-      prev = prev > carry_idx ? prev : carry_idx;
-      const double yp = __shfl(v, (int)((prev - c0) & 63));
-      const double yprev = prev >= c0 ? yp : carry_val;
+      // the real buckets of the chunk as a wave-uniform mask: each lane's
+      // previous real bucket is the highest set bit below it (else the
+      // carry), no cross-lane scan
+      const uint64_t rm = __ballot(p);
+      const uint64_t below = rm & ((1ULL << lane) - 1);
+      const int pl = below ? 63 - __builtin_clzll(below) : -1;
+      const int64_t prev = pl >= 0 ? c0 + pl : carry_idx;
       uint64_t gaps = __ballot(p && prev >= 0 && prev < b - 1);
-      while (gaps) {
-        const int g = __builtin_ctzll(gaps);
-        gaps &= gaps - 1;
-        const int64_t k0 = __shfl(prev, g), k1 = c0 + g;
-        const double y0 = __shfl(yprev, g), y1 = __shfl(v, g);
-        const int64_t x0 = bucket_ts(P, k0), x1 = bucket_ts(P, k1);
-        for (int64_t j = k0 + 1 + lane; j < k1; j += 64) {
-          rowv[j] = interp_value(P.interp, bucket_ts(P, j), x0, y0, x1, y1);
-          rows[j] = ST_INTERP;
+      if (gaps) {
+        const double yp = __shfl(v, pl >= 0 ? pl : 0);
+        const double yprev = pl >= 0 ? yp : carry_val;
+        while (gaps) {
+          const int g = __builtin_ctzll(gaps);
+          gaps &= gaps - 1;
+          const int64_t k0 = __shfl(prev, g), k1 = c0 + g;
+          const double y0 = __shfl(yprev, g), y1 = __shfl(v, g);
+          const int64_t x0 = bucket_ts(P, k0), x1 = bucket_ts(P, k1);
+          for (int64_t j = k0 + 1 + lane; j < k1; j += 64) {
+            rowv[j] = interp_value(P.interp, bucket_ts(P, j), x0, y0, x1, y1);
+            rows[j] = ST_INTERP;
+          }
         }
       }
-      const int64_t last = __shfl(incl, 63);
-      if (last >= 0) {
-        carry_val = __shfl(v, (int)((last - c0) & 63));
-        carry_idx = last;
+      if (rm) {
+        const int l = 63 - __builtin_clzll(rm);
+        carry_val = readlane_d(v, l);
+        carry_idx = c0 + l;
       }
     }
     if (SM.of_has[s] && carry_idx >= 0) {
@@ -883,32 +916,54 @@ __global__ __launch_bounds__(256) void k_transform(Params P, BatchDev B,
     return;
   }
 
-  // ---------------- rate: pass 1 computes the rate points ----------------
+  transform_rate<NCH>(P, SM, s, rowv, rows, sent, fill, kf, kl, err_word);
+}
+
+// RateSpan over the bucket points of one series and the contribution rule
+// of rate mode (AggregationIterator.java:448-459, :744-753).  Pass 1 computes
+// the rate points (the first one against (0, 0) or the FillingDownsampler
+// bucket before the grid), pass 2 writes each bucket's contribution: the
+// series' latest rate at or before it, from its first real rate on the junk
+// one.  NCH > 0: the row (<= 64*NCH buckets) stays in registers between the
+// passes and is written once; NCH == 0: pass 1 stores the rates and a
+// transient state in the row and pass 2 re-reads them.
+template <int NCH>
+DEV void transform_rate(const Params& P, const SeriesMeta& SM, int64_t s,
+                        double* rowv, uint8_t* rows, bool sent, bool fill,
+                        int64_t kf, int64_t kl, int* err_word) {
+  const int lane = LANE;
+  const int64_t nb = P.nb;
+  auto real_at = [&](int64_t b, double v) {
+    return sent ? (b >= kf && b <= kl && __double_as_longlong(v) != kAbsentBits)
+                : rows[b] == ST_REAL;
+  };
+  constexpr int NR = NCH > 0 ? NCH : 1;
+  double rreg[NR];
+  uint32_t kmask = 0;  // bit c: this lane's bucket of chunk c is a kept rate
   const double cmax_d = (double)P.counter_max;
-  // previous source point: the (0, 0) origin of RateSpan's first rate, or the
-  // FillingDownsampler bucket before the grid when start is unaligned
   int64_t carry_pts = P.rate_origin_ts;
   double carry_pv = P.rate_origin_val;
   int64_t r0_idx = -1, last_kept = -1;
   double r0_val = 0.0;
   int kept_count = 0;
   int bad_ts = 0;
-  for (int64_t c0 = 0; c0 < nb; c0 += 64) {
+  auto pass1 = [&](int64_t c0, int c, double vb) {
     const int64_t b = c0 + lane;
     const bool inb = b < nb;
-    const double vb = inb ? rowv[b] : 0.0;
     const uint8_t st = (inb && real_at(b, vb)) ? ST_REAL : 0;
     const bool pt = inb && (fill || st == ST_REAL);
     const double pv = (st == ST_REAL) ? vb : P.fill_value;
     const int64_t t = bucket_ts(P, b);
-    const int64_t incl = wave_incl_max(pt ? b : -1);
-    int64_t prev = __shfl_up(incl, 1);
-    if (lane == 0) prev = -1;
-    const double vp = __shfl(pv, (int)((prev - c0) & 63));
+    // previous source point of each lane: highest set bit below it in the
+    // chunk's point mask, else the carry
+    const uint64_t pm = __ballot(pt);
+    const uint64_t below = pm & ((1ULL << lane) - 1);
+    const int pl = below ? 63 - __builtin_clzll(below) : -1;
+    const double vp = __shfl(pv, pl >= 0 ? pl : 0);
     int64_t tprev;
     double vprev;
-    if (prev >= c0) {
-      tprev = bucket_ts(P, prev);
+    if (pl >= 0) {
+      tprev = bucket_ts(P, c0 + pl);
       vprev = vp;
     } else {
       tprev = carry_pts;
@@ -932,7 +987,10 @@ __global__ __launch_bounds__(256) void k_transform(Params P, BatchDev B,
         rate = diff / dt;
       }
     }
-    if (inb) {
+    if (NCH > 0) {
+      rreg[c] = rate;
+      if (pt && kept) kmask |= 1u << c;
+    } else if (inb) {
       if (pt && kept) {
         rowv[b] = rate;
         rows[b] = ST_KEPT;
@@ -951,10 +1009,30 @@ __global__ __launch_bounds__(256) void k_transform(Params P, BatchDev B,
       if (kept_count > 2) kept_count = 2;
       last_kept = c0 + 63 - __builtin_clzll(km);
     }
-    const int64_t lp = __shfl(incl, 63);
-    if (lp >= 0) {
-      carry_pts = bucket_ts(P, lp);
-      carry_pv = __shfl(pv, (int)((lp - c0) & 63));
+    if (pm) {
+      const int l = 63 - __builtin_clzll(pm);
+      carry_pts = bucket_ts(P, c0 + l);
+      carry_pv = readlane_d(pv, l);
+    }
+  };
+  if (NCH > 0) {
+    // the whole row first (every load in flight at once), then the chain
+#pragma unroll
+    for (int c = 0; c < NR; ++c) {
+      const int64_t b = (int64_t)c * 64 + lane;
+      rreg[c] = b < nb ? rowv[b] : 0.0;
+    }
+#pragma unroll
+    for (int c = 0; c < NR; ++c)
+      if ((int64_t)c * 64 < nb) pass1((int64_t)c * 64, c, rreg[c]);
+  } else {
+    double va = lane < nb ? rowv[lane] : 0.0;
+    double vn = lane + 64 < nb ? rowv[lane + 64] : 0.0;
+    for (int64_t c0 = 0; c0 < nb; c0 += 64) {
+      const double vb = va;
+      va = vn;
+      vn = c0 + 128 + lane < nb ? rowv[c0 + 128 + lane] : 0.0;
+      pass1(c0, 0, vb);
     }
   }
   if (__ballot(bad_ts) && lane == 0) atomicOr(err_word, ERR_RATE_TS);
@@ -966,33 +1044,65 @@ __global__ __launch_bounds__(256) void k_transform(Params P, BatchDev B,
   }
   const int total = kept_count + (of_kept ? 1 : 0);
 
-  // ---------------- rate: pass 2 writes contributions --------------------
   int64_t carry_k = -1;
   double carry_kv = 0.0;
-  for (int64_t c0 = 0; c0 < nb; c0 += 64) {
+  auto pass2 = [&](int64_t c0, int c, uint8_t st_in, double v_in) {
     const int64_t b = c0 + lane;
     const bool inb = b < nb;
-    const uint8_t st = inb ? rows[b] : 0;
-    const bool k = st == ST_KEPT;
-    const double kv = k ? rowv[b] : 0.0;
-    const int64_t incl = wave_incl_max(k ? b : -1);
-    const int64_t lk = incl > carry_k ? incl : carry_k;
-    const double lv = __shfl(kv, (int)((incl - c0) & 63));
-    const double held = incl >= c0 ? lv : (lk >= 0 ? carry_kv : r0_val);
+    bool k;
+    double kv;
+    if (NCH > 0) {
+      k = inb && ((kmask >> c) & 1u);
+      kv = k ? rreg[c] : 0.0;
+    } else {
+      k = inb && st_in == ST_KEPT;
+      kv = k ? v_in : 0.0;
+    }
+    // latest kept rate at or before each lane: highest set bit up to it
+    const uint64_t km = __ballot(k);
+    const uint64_t upto = km & ((2ULL << lane) - 1);
+    const int il = upto ? 63 - __builtin_clzll(upto) : -1;
+    const double lv = __shfl(kv, il >= 0 ? il : 0);
+    const double held = il >= 0 ? lv : (carry_k >= 0 ? carry_kv : r0_val);
     if (inb) {
       if (total < 2 || (b > last_kept && !of_kept)) {
         rows[b] = ST_ABSENT;
       } else if (k && b != r0_idx) {
+        if (NCH > 0) rowv[b] = kv;
         rows[b] = ST_REAL;
       } else {
         rowv[b] = held;
         rows[b] = ST_INTERP;
       }
     }
-    const int64_t lk63 = __shfl(incl, 63);
-    if (lk63 >= 0) {
-      carry_k = lk63;
-      carry_kv = __shfl(kv, (int)((lk63 - c0) & 63));
+    if (km) {
+      const int l = 63 - __builtin_clzll(km);
+      carry_k = c0 + l;
+      carry_kv = readlane_d(kv, l);
+    }
+  };
+  if (NCH > 0) {
+#pragma unroll
+    for (int c = 0; c < NR; ++c)
+      if ((int64_t)c * 64 < nb) pass2((int64_t)c * 64, c, 0, 0.0);
+  } else {
+    // pass 2 re-reads what pass 1 stored (KEPT flags and rates), two chunks
+    // ahead like pass 1
+    auto ld = [&](int64_t b, uint8_t& st, double& v) {
+      st = b < nb ? rows[b] : (uint8_t)0;
+      v = b < nb ? rowv[b] : 0.0;
+    };
+    uint8_t sa, sn;
+    double va, vn;
+    ld(lane, sa, va);
+    ld(lane + 64, sn, vn);
+    for (int64_t c0 = 0; c0 < nb; c0 += 64) {
+      const uint8_t sc = sa;
+      const double vc = va;
+      sa = sn;
+      va = vn;
+      ld(c0 + 128 + lane, sn, vn);
+      pass2(c0, 0, sc, vc);
     }
   }
 }
@@ -1065,14 +1175,66 @@ __global__ __launch_bounds__(256) void k_group(
   }
 }
 
-// merge the chunk partials of multi-chunk groups in chunk order
+// ordered fold of the chunk partials [t0, t1) of bucket b; loads issued in
+// batches of 8 ahead of the dependent combines (the chain is latency-bound)
+template <class M>
+DEV void fold_chunks(const Packed* __restrict__ partial,
+                     const uint8_t* __restrict__ tile_emit, int64_t nb,
+                     int64_t b, int64_t t0, int64_t t1, M& st, int& emit) {
+  int64_t t = t0;
+  for (; t + 8 <= t1; t += 8) {
+    Packed q[8];
+    uint8_t e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      q[j] = partial[(t + j) * nb + b];
+      e[j] = tile_emit[(t + j) * nb + b];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      st = M::combine(st, M::unpack(q[j]));
+      emit |= e[j];
+    }
+  }
+  for (; t < t1; ++t) {
+    st = M::combine(st, M::unpack(partial[t * nb + b]));
+    emit |= tile_emit[t * nb + b];
+  }
+}
+
+// first level of the ordered combine of groups with many chunks: slice s of
+// group i (chunks [t0 + s*L, t0 + (s+1)*L)) -> scratch row i*ns + s
+template <class M>
+__global__ __launch_bounds__(256) void k_combine_l1(
+    int64_t nb, int64_t n_groups, int64_t ns,
+    const int64_t* __restrict__ grp_t0, const int64_t* __restrict__ grp_t1,
+    const Packed* __restrict__ partial, const uint8_t* __restrict__ tile_emit,
+    Packed* __restrict__ scratch, uint8_t* __restrict__ scratch_emit) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = idx / nb;  // i * ns + s
+  if (row >= n_groups * ns) return;
+  const int64_t b = idx - row * nb;
+  const int64_t i = row / ns, sl = row - i * ns;
+  const int64_t t0 = grp_t0[i], t1 = grp_t1[i];
+  const int64_t L = (t1 - t0 + ns - 1) / ns;
+  const int64_t a = t0 + sl * L;
+  const int64_t e = a + L < t1 ? a + L : t1;
+  M st = M::init();
+  int emit = 0;
+  if (a < e) fold_chunks<M>(partial, tile_emit, nb, b, a, e, st, emit);
+  scratch[row * nb + b] = st.pack();
+  scratch_emit[row * nb + b] = (uint8_t)emit;
+}
+
+// merge the chunk partials of multi-chunk groups in chunk order (ns > 0:
+// the ns first-level slices of k_combine_l1, rows [i*ns, (i+1)*ns))
 template <class M>
 __global__ __launch_bounds__(256) void k_combine(
     int64_t nb, int64_t n_groups, const int64_t* __restrict__ grp_g,
     const int64_t* __restrict__ grp_t0, const int64_t* __restrict__ grp_t1,
     const Packed* __restrict__ partial, const uint8_t* __restrict__ tile_emit,
     double* __restrict__ out_val, uint8_t* __restrict__ out_emit,
-    Packed* __restrict__ out_partial, int* err_word) {
+    Packed* __restrict__ out_partial, int* err_word, int64_t ns) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t i = idx / nb;
   if (i >= n_groups) return;
@@ -1080,10 +1242,10 @@ __global__ __launch_bounds__(256) void k_combine(
   const int64_t g = grp_g[i];
   M st = M::init();
   int emit = 0;
-  for (int64_t t = grp_t0[i]; t < grp_t1[i]; ++t) {
-    st = M::combine(st, M::unpack(partial[t * nb + b]));
-    emit |= tile_emit[t * nb + b];
-  }
+  if (ns > 0)
+    fold_chunks<M>(partial, tile_emit, nb, b, i * ns, (i + 1) * ns, st, emit);
+  else
+    fold_chunks<M>(partial, tile_emit, nb, b, grp_t0[i], grp_t1[i], st, emit);
   const int64_t o = g * nb + b;
   if (out_partial) {
     out_partial[o] = st.pack();

@@ -46,12 +46,11 @@ __global__ __launch_bounds__(256) void k_keys_transpose(
     const int64_t m = m0 + mi, b = b0 + bi;
     uint64_t k = KEY_NONE;
     if (m < M && b < nb) {
+      // both loads unconditional: the 16 rows' loads all go out at once
       const int64_t off = members[m] * nb + b;
       const uint8_t st = R.state[off];
-      if (st) {
-        const double v = R.val[off];
-        if (!is_nan(v)) k = dkey(v);
-      }
+      const double v = R.val[off];
+      if (st && !is_nan(v)) k = dkey(v);
     }
     tile[mi][bi] = k;
   }
@@ -322,6 +321,197 @@ DEV double sel_value(int median, int64_t n, double pos, double lo, double hi) {
   if (median || n == 1) return lo;
   if (pos >= 1 && pos < (double)n) return lo + (pos - __builtin_floor(pos)) * (hi - lo);
   return lo;
+}
+
+// ------------------------------------------------------------------------
+// k_seg_select: the whole selection of one segment (large group, bucket) in
+// one workgroup, replacing k_radix_hist/k_radix_select's eight grid-wide
+// passes for rank-local groups.  (1) min / max key of the segment: bits above
+// the highest differing bit are common to every key and need no pass; (2)
+// 11-bit digit passes (2,048-bin LDS histograms per target) only while a
+// target still has more than SS_CAP candidates; (3) the <= SS_CAP candidates
+// of each target are gathered into LDS and the target's order statistic is
+// picked by counting.  Exact: the same keys, the same order statistics.
+// ------------------------------------------------------------------------
+constexpr int SS_BITS = 11;
+constexpr int SS_BINS = 1 << SS_BITS;
+constexpr int SS_CAP = 1024;
+constexpr int SS_THREADS = 256;
+
+DEV uint64_t block_min_max_u64(uint64_t v, bool is_max, uint64_t* red) {
+  // wave reduce then across the 4 waves of the block
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint64_t o = __shfl_xor(v, d);
+    v = is_max ? (o > v ? o : v) : (o < v ? o : v);
+  }
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if (LANE == 0) red[w] = v;
+  __syncthreads();
+  uint64_t r = red[0];
+  for (int j = 1; j < SS_THREADS / 64; ++j)
+    r = is_max ? (red[j] > r ? red[j] : r) : (red[j] < r ? red[j] : r);
+  return r;
+}
+
+__global__ __launch_bounds__(SS_THREADS) void k_seg_select(
+    int64_t nb, int64_t M, int64_t n_lg, const int64_t* __restrict__ lg_g,
+    const int64_t* __restrict__ lg_off, const int64_t* __restrict__ lg_k,
+    const uint64_t* __restrict__ keys, const SelState* __restrict__ sel,
+    const uint8_t* __restrict__ emit, double* __restrict__ out_val,
+    int* err_word, int median, double p) {
+  __shared__ uint32_t h[2][SS_BINS];
+  __shared__ uint64_t cand[2][SS_CAP];
+  __shared__ uint64_t red[SS_THREADS / 64];
+  __shared__ uint32_t s_nc[2];
+  __shared__ uint64_t s_pick[2];
+  __shared__ int s_digit[2];
+  __shared__ int64_t s_below[2], s_cnt[2];
+  const int tid = threadIdx.x;
+  const int64_t seg = blockIdx.x;
+  if (seg >= n_lg * nb) return;
+  const int64_t lg = seg / nb, b = seg - lg * nb;
+  const int64_t o = lg_g[lg] * nb + b;
+  if (!emit[o]) return;
+  const SelState s0 = sel[seg];
+  const int nt = s0.ntarget;
+  double r = qnan();
+  if (nt > 0) {
+    const uint64_t* col = keys + b * M + lg_off[lg];
+    const int64_t k = lg_k[lg];
+    // every key of the segment, 4 independent loads in flight per thread
+    auto for_keys = [&](auto&& f) {
+      int64_t i = tid;
+      for (; i + 3 * SS_THREADS < k; i += 4 * SS_THREADS) {
+        const uint64_t a0 = col[i], a1 = col[i + SS_THREADS],
+                       a2 = col[i + 2 * SS_THREADS],
+                       a3 = col[i + 3 * SS_THREADS];
+        f(a0);
+        f(a1);
+        f(a2);
+        f(a3);
+      }
+      for (; i < k; i += SS_THREADS) f(col[i]);
+    };
+    // (1) min / max over the non-NONE keys
+    uint64_t mn = ~0ULL, mx = 0;
+    for_keys([&](uint64_t key) {
+      if (key == KEY_NONE) return;
+      mn = key < mn ? key : mn;
+      mx = key > mx ? key : mx;
+    });
+    mn = block_min_max_u64(mn, false, red);
+    mx = block_min_max_u64(mx, true, red);
+    uint64_t prefix[2], mask[2];
+    int64_t rank[2], cnt[2];
+    int shift = 0;
+    if (mn != mx) shift = 64 - __builtin_clzll(mn ^ mx);  // bits left to resolve
+    for (int t = 0; t < 2; ++t) {
+      mask[t] = shift >= 64 ? 0ULL : ~0ULL << shift;
+      prefix[t] = mn & mask[t];
+      rank[t] = s0.rank[t];
+      cnt[t] = s0.n;
+    }
+    // (2) digit passes while some target has too many candidates
+    while (shift > 0 && (cnt[0] > SS_CAP || (nt == 2 && cnt[1] > SS_CAP))) {
+      const int w = shift < SS_BITS ? shift : SS_BITS;
+      shift -= w;
+      const uint32_t dm = (1u << w) - 1;
+      for (int j = tid; j < 2 * SS_BINS; j += SS_THREADS) (&h[0][0])[j] = 0;
+      __syncthreads();
+      for_keys([&](uint64_t key) {
+        if (key == KEY_NONE) return;
+        const uint32_t d = (uint32_t)(key >> shift) & dm;
+        if ((key & mask[0]) == prefix[0]) atomicAdd(&h[0][d], 1u);
+        if (nt == 2 && (key & mask[1]) == prefix[1]) atomicAdd(&h[1][d], 1u);
+      });
+      __syncthreads();
+      // per target: the digit whose cumulative count passes the rank (one
+      // wave per target scans its bins, 32 per lane)
+      const int wv = tid >> 6, lane = LANE;
+      if (wv < nt) {
+        const int per = SS_BINS / 64;
+        uint32_t sum = 0;
+        for (int j = 0; j < per; ++j) sum += h[wv][lane * per + j];
+        uint32_t incl = sum;
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t y = __shfl_up(incl, d);
+          if (lane >= d) incl += y;
+        }
+        const int64_t excl = (int64_t)incl - sum;
+        const int64_t rr = rank[wv];
+        if (rr >= excl && rr < (int64_t)incl) {
+          int64_t cum = excl;
+          int j = 0;
+          for (; j < per - 1; ++j) {
+            const uint32_t c = h[wv][lane * per + j];
+            if (rr < cum + c) break;
+            cum += c;
+          }
+          s_digit[wv] = lane * per + j;
+          s_below[wv] = cum;
+          s_cnt[wv] = h[wv][lane * per + j];
+        }
+      }
+      __syncthreads();
+      for (int t = 0; t < nt; ++t) {
+        prefix[t] |= (uint64_t)s_digit[t] << shift;
+        mask[t] |= (uint64_t)dm << shift;
+        rank[t] -= s_below[t];
+        cnt[t] = s_cnt[t];
+      }
+      __syncthreads();
+    }
+    // (3) both targets' candidates gathered in one pass over the keys, then
+    // each target's rank-th picked by counting
+    uint64_t val[2];
+    bool need[2] = {false, false};
+    for (int t = 0; t < nt; ++t) {
+      if (shift == 0) val[t] = prefix[t];  // every bit resolved
+      else need[t] = true;
+    }
+    if (need[0] || need[1]) {
+      if (tid < 2) s_nc[tid] = 0;
+      __syncthreads();
+      for_keys([&](uint64_t key) {
+        if (key == KEY_NONE) return;
+        for (int t = 0; t < 2; ++t) {
+          if (need[t] && (key & mask[t]) == prefix[t]) {
+            const uint32_t q = atomicAdd(&s_nc[t], 1u);
+            if (q < SS_CAP) cand[t][q] = key;
+          }
+        }
+      });
+      __syncthreads();
+      for (int t = 0; t < 2; ++t) {
+        if (!need[t]) continue;
+        const int nc = (int)(s_nc[t] < SS_CAP ? s_nc[t] : SS_CAP);
+        const int64_t rr = rank[t];
+        for (int j = tid; j < nc; j += SS_THREADS) {
+          const uint64_t x = cand[t][j];
+          int less = 0, eq = 0;
+          for (int q = 0; q < nc; ++q) {
+            less += cand[t][q] < x;
+            eq += cand[t][q] == x;
+          }
+          if (rr >= less && rr < less + eq) s_pick[t] = x;  // ties: same key
+        }
+      }
+      __syncthreads();
+      for (int t = 0; t < 2; ++t)
+        if (need[t]) val[t] = s_pick[t];
+    }
+    if (nt == 1) val[1] = val[0];
+    // PercentileAgg / Median estimator over the order statistics
+    double pos = 0.0;
+    int64_t r0, r1;
+    sel_ranks(median, p, s0.n, &r0, &r1, &pos);
+    r = sel_value(median, s0.n, pos, key_value(val[0]), key_value(val[1]));
+  }
+  if (tid == 0) {
+    if (is_inf(r)) atomicOr(err_word, ERR_INFINITY);
+    out_val[o] = r;
+  }
 }
 
 // ------------------------------------------------------------------------

@@ -224,14 +224,31 @@ def test_big_groups_chunked(engine):
         check(engine, spec, b, agg in ORDER_FREE, scale=100.0, where="big/" + agg)
 
 
-@pytest.mark.parametrize("n_series", [45, 300])
-def test_percentiles_large_groups(engine, n_series):
-    """median / percentiles over groups above the LDS-sort limit: radix
-    select over transposed keys (exact: selection + the reference's
-    estimator arithmetic)."""
+def test_huge_group_two_level_combine(engine):
+    """One group of > 128 chunks (36k series): the ordered two-level chunk
+    combine (k_combine_l1 + k_combine) — exact for order-free aggregators,
+    1e-12 otherwise."""
+    b = datasets.random_batch(73, n_series=36000, big_group=True,
+                              span_ms=600 * 1000, cadence_ms=30000,
+                              empty_frac=0.01)
+    for agg in ("sum", "zimsum", "avg", "dev", "min", "mimmax", "count",
+                "first", "last", "diff", "none"):
+        spec = _spec(agg, "max", end=datasets.T0 + 600 * 1000)
+        check(engine, spec, b, agg in ORDER_FREE, scale=100.0,
+              where="huge/" + agg)
+
+
+@pytest.mark.parametrize("n_series,kind", [(45, "float"), (300, "float"),
+                                           (5000, "float"), (5000, "int")])
+def test_percentiles_large_groups(engine, n_series, kind):
+    """median / percentiles over groups above the LDS-sort limit: per-segment
+    select over transposed keys — direct gather below SS_CAP candidates,
+    11-bit digit passes above it, ties from integer data (exact: selection
+    + the reference's estimator arithmetic)."""
     b = datasets.random_batch(77, n_series=n_series, big_group=True,
                               span_ms=3600 * 1000, cadence_ms=30000,
-                              nan_frac=0.05)
+                              nan_frac=0.05 if kind == "float" else 0.0,
+                              value_kind=kind)
     for agg in ("median", "p50", "p75", "p99", "p999", "ep95r3", "ep50r7"):
         for fill in ("none", "nan"):
             spec = _spec(agg, "max", fill, end=datasets.T0 + 3600 * 1000)
