@@ -35,7 +35,43 @@ def parse():
                     help="series per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-decode", action="store_true",
+                    help="skip the secondary compacted-cell decode figure")
     return ap.parse_args()
+
+
+def decode_figure(eng, config, n_series, reps=5):
+    """Secondary figure: the compacted-cell decode of the same
+    workload's series at whole-second resolution (2-byte qualifiers, 8-byte
+    doubles + meta byte per hour row, the format a scan returns): cells are
+    encoded in HBM (otsdb_encode_cells_device), then otsdb_decode_cells_device
+    (validate/count, scan, write) is timed end to end."""
+    import torch
+    from opentsdb_amd import workload
+    g = workload.gen_spec(config)
+    g.flags = 1
+    db = workload.generate_device(eng, g, 0, n_series, config=config)
+    n = db.n_points_total
+    cells = workload.encode_cells_device(eng, db)
+    del db
+    torch.cuda.empty_cache()
+    workload.decode_cells_device(eng, cells, capacity=n)  # warm-up
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        out = workload.decode_cells_device(eng, cells, capacity=n)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t) / reps
+    cb = cells.n_bytes
+    del out, cells
+    torch.cuda.empty_cache()
+    return {"kernel": "k_decode (count + scan + write)",
+            "points": n, "ms": dt * 1e3, "value": n / dt,
+            "unit": "data points/s",
+            "compacted_bytes": cb, "compacted_bytes_per_point": cb / n,
+            "achieved_GBs": (cb + 17 * n) / dt / 1e9,
+            "note": "reads the compacted cells, writes ts/val/is_float "
+                    "(17 B/point); not part of the headline value"}
 
 
 def cpu_baseline(config, target_s):
@@ -194,6 +230,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.config, args.cpu_seconds)
 
+    n_groups, n_buckets = db.n_groups, int(sz.n_buckets)
+    decode = None
+    if world == 1 and not args.no_decode and args.config == "C2":
+        del db, res
+        torch.cuda.empty_cache()
+        decode = decode_figure(eng, args.config, n_series)
+
     if rank == 0:
         line = {
             "metric": "data points aggregated/sec (node) for 1m-avg "
@@ -218,8 +261,8 @@ def main():
                                 (cfg["group"] or "") + "=*" if cfg["group"]
                                 else "", n_series, cfg["days"]),
                 "points_per_gpu": n_points,
-                "groups_per_gpu": db.n_groups,
-                "buckets": int(sz.n_buckets),
+                "groups_per_gpu": n_groups,
+                "buckets": n_buckets,
                 "output_points_per_gpu": out_points,
                 "parallelism": "series-sharded dp%d%s" % (
                     world, " + RCCL exchange" if sharded else ""),
@@ -240,6 +283,7 @@ def main():
                 "algorithmic_bytes_per_launch": BYTES_PER_POINT * n_points,
             },
             "cpu_baseline": cpu,
+            "decode": decode,
         }
         print(json.dumps(line), flush=True)
     if dist:

@@ -324,6 +324,34 @@ otsdb_status otsdb_decode_cells_device(otsdb_ctx* ctx, const otsdb_cells* cells,
                                        uint8_t* is_float, int64_t capacity,
                                        void* hip_stream);
 
+/* Test / bench infrastructure (not the query path): encodes a columnar
+ * DEVICE batch into compacted RowSeq columns, the layout the write path and
+ * compaction produce and otsdb_decode_cells_device reads (one row per
+ * (series, hour); 2-byte qualifiers for whole seconds, 4-byte ms qualifiers
+ * otherwise; doubles in 8 bytes, longs in the smallest of 1/2/4/8; the meta
+ * byte on multi-value columns; Internal.java:848-863, TSDB.java:1051-1147,
+ * CompactionQueue.java:594-616).  Two calls: with cells == NULL it writes
+ * per-series counts (rows, qualifier bytes, value bytes) into series_rows /
+ * series_qbytes / series_vbytes [S]; then, with those arrays turned into
+ * exclusive prefix sums by the caller, it writes the cells (qual_off[R] and
+ * val_off[R] are the caller's totals).  Values are typed by
+ * batch->series_float (NULL = doubles).                                    */
+typedef struct {
+  int64_t* row_series;  /* [R] */
+  int64_t* row_base_s;  /* [R] */
+  int64_t* qual_off;    /* [R+1] */
+  uint8_t* qual;
+  int64_t* val_off;     /* [R+1] */
+  uint8_t* val;
+} otsdb_cells_out;
+
+otsdb_status otsdb_encode_cells_device(otsdb_ctx* ctx, const otsdb_batch* batch,
+                                       int64_t* series_rows,
+                                       int64_t* series_qbytes,
+                                       int64_t* series_vbytes,
+                                       const otsdb_cells_out* cells,
+                                       void* hip_stream);
+
 /* ---- stage timing (bench roofline) ------------------------------------- */
 /* When enabled, every query records HIP events around its pipeline stages
  * on the query's stream.  otsdb_prof_read returns, per stage, the summed
@@ -344,7 +372,7 @@ typedef struct {
   int64_t duration_ms;    /* 86400000 / 604800000                            */
   int64_t cadence_ms;     /* 10000                                           */
   int32_t kind;           /* 0 = gauge f64, 1 = gauge int64, 2 = counter int64 */
-  int32_t _pad;
+  int32_t flags;          /* 1 = whole-second phases (2-byte qualifiers)     */
 } otsdb_gen_spec;
 
 otsdb_status otsdb_gen_counts_device(otsdb_ctx* ctx, const otsdb_gen_spec* g,

@@ -97,6 +97,12 @@ class Cells(C.Structure):
     ]
 
 
+class CellsOut(C.Structure):
+    _fields_ = [("row_series", C.c_void_p), ("row_base_s", C.c_void_p),
+                ("qual_off", C.c_void_p), ("qual", C.c_void_p),
+                ("val_off", C.c_void_p), ("val", C.c_void_p)]
+
+
 class GenSpec(C.Structure):
     _fields_ = [
         ("seed", C.c_uint64),
@@ -104,7 +110,7 @@ class GenSpec(C.Structure):
         ("duration_ms", C.c_int64),
         ("cadence_ms", C.c_int64),
         ("kind", C.c_int32),
-        ("_pad", C.c_int32),
+        ("flags", C.c_int32),
     ]
 
 
@@ -117,6 +123,7 @@ EXPORTS = [
     "otsdb_gen_fill_device", "otsdb_prof_enable", "otsdb_prof_read",
     "otsdb_decode_cells_device", "otsdb_sel_prepare_device",
     "otsdb_sel_hist_device", "otsdb_sel_finish_device",
+    "otsdb_encode_cells_device",
 ]
 
 _lib = None
@@ -180,6 +187,9 @@ def load(path=None):
     lib.otsdb_sel_hist_device.restype = C.c_int
     lib.otsdb_sel_finish_device.argtypes = [vp, vp, PR, vp]
     lib.otsdb_sel_finish_device.restype = C.c_int
+    lib.otsdb_encode_cells_device.argtypes = [vp, PB, vp, vp, vp,
+                                              C.POINTER(CellsOut), vp]
+    lib.otsdb_encode_cells_device.restype = C.c_int
     lib.otsdb_prof_enable.argtypes = [vp, C.c_int]
     lib.otsdb_prof_enable.restype = C.c_int
     lib.otsdb_prof_read.argtypes = [vp, vp, vp, C.c_int, C.c_int]

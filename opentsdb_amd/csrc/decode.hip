@@ -37,11 +37,113 @@ DEV int fmap_compose(int g, int f) {  // g o f
   return fmap_apply(g, f & 1) | (fmap_apply(g, (f >> 1) & 1) << 1);
 }
 
+// The first vl (1..8) bytes at a, big-endian, from two aligned 8-byte loads
+// (values sit at any byte offset: one meta byte per multi-value column);
+// byte loads within 16 bytes of the end of the value buffer.
+DEV uint64_t load_be(const uint8_t* base, int64_t a, int vl, int64_t vend) {
+  const int64_t al = a & ~(int64_t)7;
+  uint64_t w;
+  if (((uintptr_t)base & 7) == 0 && al + 16 <= vend) {
+    const uint64_t lo = *reinterpret_cast<const uint64_t*>(base + al);
+    const uint64_t hi = *reinterpret_cast<const uint64_t*>(base + al + 8);
+    const int sh = (int)(a - al) * 8;
+    w = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;  // bytes a.. a+7, LE
+  } else {
+    w = 0;
+    for (int i = 0; i < vl; ++i) w |= (uint64_t)base[a + i] << (8 * i);
+  }
+  return __builtin_bswap64(w) >> (64 - 8 * vl);
+}
+
+// RowSeq value bits of a point: big-endian signed 1/2/4/8-byte longs
+// (RowSeq.java:233-245), 4-byte floats widened, 8-byte doubles (:256-266)
+DEV int64_t value_bits(uint64_t x, int vl, int fl) {
+  if (fl) return vl == 4 ? __double_as_longlong((double)__uint_as_float((uint32_t)x))
+                         : (int64_t)x;
+  switch (vl) {
+    case 1: return (int8_t)x;
+    case 2: return (int16_t)x;
+    case 4: return (int32_t)x;
+    default: return (int64_t)x;
+  }
+}
+
+// Fast path of one column whose qualifiers all have the width of the first
+// (the common case: no MS_MIXED_COMPACT) — point i's qualifier is at
+// qw * i, no start-recurrence scan — and, for the write, whose values all
+// have one length (point i's value at vl * i).  Same checks and results as
+// the generic walk below; returns false (nothing done) when the column is
+// not uniform.  mode 0: count + validate, records uniformity in fast[r];
+// mode 1: writes.
+DEV bool decode_uniform(const CellsDev& C, int64_t r, int mode,
+                        const uint8_t* q, int64_t qlen, int64_t vbase,
+                        int64_t vlen, int64_t base_ms, int64_t* row_count,
+                        const int64_t* row_out, uint8_t* fast, int64_t cap,
+                        int64_t* ts, int64_t* val, uint8_t* isf, int& bad) {
+  const int lane = LANE;
+  if (mode == 1 && !fast[r]) return false;
+  const int qw = ((q[0] & 0xF0) == 0xF0) ? 4 : 2;
+  if (qlen % qw || ((uintptr_t)q & 1)) return false;
+  const int64_t n = qlen / qw;
+  auto qual_at = [&](int64_t i) -> uint32_t {
+    const uint16_t* h = reinterpret_cast<const uint16_t*>(q + qw * i);
+    const uint32_t a = __builtin_bswap16(h[0]);
+    return qw == 2 ? a : (a << 16) | __builtin_bswap16(h[1]);
+  };
+  if (mode == 0) {
+    const int v0 = (int)(qual_at(0) & 0x7) + 1;  // same address: broadcast
+    int consistent = 1, diff = 0;
+    int64_t vsum = 0;
+    for (int64_t i0 = 0; i0 < n; i0 += 64) {
+      const int64_t i = i0 + lane;
+      if (i < n) {
+        const uint32_t qv = qual_at(i);
+        const int mk = (((qv >> (qw == 2 ? 8 : 24)) & 0xF0) == 0xF0);
+        consistent &= (qw == 4) == (mk != 0);
+        const int vl = (int)(qv & 0x7) + 1;
+        if (qv & 0x8) bad |= !(vl == 4 || vl == 8);
+        else bad |= !(vl == 1 || vl == 2 || vl == 4 || vl == 8);
+        diff |= vl != v0;
+        vsum += vl;
+      }
+    }
+    if (__ballot(!consistent)) return false;
+    for (int d = 32; d >= 1; d >>= 1) vsum += __shfl_xor(vsum, d);
+    const int64_t meta = n > 1 ? 1 : 0;
+    if (vsum + meta != vlen) bad = 1;
+    const bool one_len = __ballot(diff) == 0;  // every lane votes
+    if (lane == 0) {
+      row_count[r] = n;
+      fast[r] = one_len ? 1 : 0;
+    }
+    return true;
+  }
+  // mode 1, one value length
+  const int vl = (int)(qual_at(0) & 0x7) + 1;
+  const int64_t vend = C.val_off[C.R];
+  const int64_t out0 = row_out[r];
+  for (int64_t i0 = 0; i0 < n; i0 += 64) {
+    const int64_t i = i0 + lane;
+    if (i >= n) break;
+    const uint32_t qv = qual_at(i);
+    const int64_t o = out0 + i;
+    if (o >= cap) continue;
+    const int fl = (qv & 0x8) != 0;
+    const uint64_t x = load_be(C.val, vbase + vl * i, vl, vend);
+    ts[o] = qw == 4 ? base_ms + (int64_t)((qv & 0x0FFFFFC0u) >> 6)
+                    : base_ms + (int64_t)((qv & 0xFFFFu) >> 4) * 1000;
+    val[o] = value_bits(x, vl, fl);
+    isf[o] = (uint8_t)fl;
+  }
+  return true;
+}
+
 // one wavefront per row; mode 0 counts (and validates), mode 1 writes
 __global__ __launch_bounds__(256) void k_decode(
     CellsDev C, int mode, int64_t* __restrict__ row_count,
-    const int64_t* __restrict__ row_out, int64_t cap, int64_t* __restrict__ ts,
-    int64_t* __restrict__ val, uint8_t* __restrict__ isf, int* err_word) {
+    const int64_t* __restrict__ row_out, uint8_t* __restrict__ fast,
+    int64_t cap, int64_t* __restrict__ ts, int64_t* __restrict__ val,
+    uint8_t* __restrict__ isf, int* err_word) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= C.R) return;
@@ -51,9 +153,21 @@ __global__ __launch_bounds__(256) void k_decode(
   const int64_t vlen = C.val_off[r + 1] - C.val_off[r];
   const int64_t base_ms = C.row_base_s[r] * 1000;
   if (qlen & 1) {  // not a data-point column (Internal.java:262-264)
-    if (mode == 0 && lane == 0) row_count[r] = 0;
+    if (mode == 0 && lane == 0) {
+      row_count[r] = 0;
+      fast[r] = 0;
+    }
     return;
   }
+  if (qlen > 0) {
+    int fbad = 0;
+    if (decode_uniform(C, r, mode, q, qlen, C.val_off[r], vlen, base_ms,
+                       row_count, row_out, fast, cap, ts, val, isf, fbad)) {
+      if (__ballot(fbad) && lane == 0) atomicOr(err_word, ERR_CORRUPT_CELL);
+      return;
+    }
+  }
+  if (mode == 0 && lane == 0) fast[r] = 0;
   const int64_t units = qlen >> 1;
   int carry_start = 1;
   int64_t carry_n = 0, carry_voff = 0;
@@ -144,6 +258,150 @@ __global__ __launch_bounds__(256) void k_decode(
     if (lane == 0) row_count[r] = carry_n;
   }
   if (__ballot(bad) && lane == 0) atomicOr(err_word, ERR_CORRUPT_CELL);
+}
+
+// ------------------------------------------------------------------------
+// k_encode: the inverse — columnar series -> compacted RowSeq columns, the
+// layout the write path + compaction produce (test/bench infrastructure, the
+// device twin of tests/cells.py): one row per (series, hour), a 2-byte
+// qualifier for whole-second offsets and a 4-byte ms qualifier otherwise
+// (Internal.buildQualifier, Internal.java:848-863), doubles as 8 bytes, longs
+// in the smallest of 1/2/4/8 bytes (TSDB.addPoint, TSDB.java:1051-1147), and
+// the trailing meta byte (bit0 = mixed s/ms) on multi-value columns
+// (CompactionQueue.buildCompactedColumn, CompactionQueue.java:594-616).
+// One wavefront per series; rows are runs of consecutive points with the
+// same hour, so every offset is a prefix sum inside the series (64-bit
+// masks for the in-chunk parts, carries across chunks).  mode 0 counts
+// rows / qualifier bytes / value bytes per series, mode 1 writes them at
+// the per-series bases the caller scanned.
+// ------------------------------------------------------------------------
+DEV int enc_long_len(int64_t v) {
+  if (v >= -128 && v <= 127) return 1;
+  if (v >= -32768 && v <= 32767) return 2;
+  if (v >= INT32_MIN && v <= INT32_MAX) return 4;
+  return 8;
+}
+
+// lanes [a, b] (a <= b) of a 64-bit mask
+DEV uint64_t lane_range(int a, int b) {
+  const uint64_t hi = b >= 63 ? ~0ULL : ((1ULL << (b + 1)) - 1);
+  return hi & ~((1ULL << a) - 1);
+}
+
+__global__ __launch_bounds__(256) void k_encode(
+    int64_t S, const int64_t* __restrict__ offsets,
+    const int64_t* __restrict__ ts, const int64_t* __restrict__ val,
+    const uint8_t* __restrict__ series_float, int mode,
+    int64_t* __restrict__ s_rows, int64_t* __restrict__ s_qb,
+    int64_t* __restrict__ s_vb, int64_t* __restrict__ row_series,
+    int64_t* __restrict__ row_base_s, int64_t* __restrict__ qual_off,
+    int64_t* __restrict__ val_off, uint8_t* __restrict__ qual,
+    uint8_t* __restrict__ vbytes) {
+  const int lane = LANE;
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= S) return;
+  const int64_t p0 = offsets[s], p1 = offsets[s + 1];
+  const int fl = series_float ? (int)series_float[s] : 1;
+  int64_t row = mode ? s_rows[s] : 0, qo = mode ? s_qb[s] : 0,
+          vo = mode ? s_vb[s] : 0;
+  const int64_t row0 = row, qo0 = qo, vo0 = vo;
+  // the row open at the chunk start: its start is before the chunk
+  int64_t prev_hour = INT64_MIN;
+  int carry_ms = 0, carry_s = 0;  // the open row has 4- / 2-byte qualifiers
+  for (int64_t c0 = p0; c0 < p1; c0 += 64) {
+    const int64_t p = c0 + lane;
+    const bool in = p < p1;
+    const int64_t t = in ? ts[p] : 0;
+    const int64_t v = in ? val[p] : 0;
+    const int64_t sec = t / 1000;
+    const int64_t hour = sec - sec % 3600;
+    const int64_t off_ms = t - hour * 1000;
+    const int ms = in && (off_ms % 1000 != 0);
+    const int qlen = in ? (ms ? 4 : 2) : 0;
+    const int vlen = in ? (fl ? 8 : enc_long_len(v)) : 0;
+    int64_t ph = __shfl_up(hour, 1);
+    if (lane == 0) ph = prev_hour;
+    const bool rs = in && hour != ph;            // row starts here
+    const int64_t nh = __shfl_down(hour, 1);
+    const bool next_in = (p + 1 < p1);
+    const bool re = in && (!next_in || (lane < 63 ? nh != hour
+                                                  : ts[p + 1] / 1000 -
+                                                        (ts[p + 1] / 1000) % 3600 !=
+                                                        hour));
+    const uint64_t rsm = __ballot(rs), msm = __ballot(ms), inm = __ballot(in);
+    // this lane's row inside the chunk: from its start lane (or the chunk
+    // start when the row began earlier) to here
+    const uint64_t below = rsm & lane_range(0, lane);
+    const int st_l = below ? 63 - __builtin_clzll(below) : -1;
+    const int a = st_l >= 0 ? st_l : 0;
+    const uint64_t span = lane_range(a, lane) & inm;
+    const bool open_row = st_l < 0;  // continues the row of the last chunk
+    const int any_ms = ((msm & span) != 0) || (open_row && carry_ms);
+    const int any_s = ((~msm & span) != 0) || (open_row && carry_s);
+    // a row has more than one point iff its end is not also its start, or
+    // it continues from the previous chunk
+    const bool single = rs && re;
+    const int meta = (re && !single) ? 1 : 0;
+    // prefix sums of qualifier and value bytes (meta bytes included)
+    int qe = qlen, ve = vlen + meta;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(qe, d), z = __shfl_up(ve, d);
+      if (lane >= d) {
+        qe += y;
+        ve += z;
+      }
+    }
+    const int64_t q_at = qo + qe - qlen;
+    const int64_t v_at = vo + ve - vlen - meta;
+    const int64_t r_at = row + __popcll(rsm & ((1ULL << lane) - 1));
+    if (mode == 1 && in) {
+      const int flags = fl ? (0x8 | 7) : (vlen - 1);
+      if (ms) {
+        const uint32_t q = 0xF0000000u | ((uint32_t)off_ms << 6) | (uint32_t)flags;
+        qual[q_at] = (uint8_t)(q >> 24);
+        qual[q_at + 1] = (uint8_t)(q >> 16);
+        qual[q_at + 2] = (uint8_t)(q >> 8);
+        qual[q_at + 3] = (uint8_t)q;
+      } else {
+        const uint32_t q = ((uint32_t)(off_ms / 1000) << 4) | (uint32_t)flags;
+        qual[q_at] = (uint8_t)(q >> 8);
+        qual[q_at + 1] = (uint8_t)q;
+      }
+      const uint64_t x = (uint64_t)v;  // doubles: their bits; longs: two's
+      for (int i = 0; i < vlen; ++i)
+        vbytes[v_at + i] = (uint8_t)(x >> (8 * (vlen - 1 - i)));
+      if (meta) vbytes[v_at + vlen] = (any_ms && any_s) ? 1 : 0;
+      if (rs) {
+        row_series[r_at] = s;
+        row_base_s[r_at] = hour;
+        qual_off[r_at] = q_at;
+        val_off[r_at] = v_at;
+      }
+    }
+    // carries: the row open at the chunk end
+    const int last = 63 - __builtin_clzll(inm);
+    const uint64_t lb = rsm & lane_range(0, last);
+    const int ls = lb ? 63 - __builtin_clzll(lb) : -1;
+    const uint64_t tail = lane_range(ls >= 0 ? ls : 0, last) & inm;
+    const int tail_ms = (msm & tail) != 0, tail_s = (~msm & tail) != 0;
+    if (ls >= 0) {
+      carry_ms = tail_ms;
+      carry_s = tail_s;
+    } else {
+      carry_ms |= tail_ms;
+      carry_s |= tail_s;
+    }
+    prev_hour = __shfl(hour, last);
+    row += __popcll(rsm);
+    qo += __shfl(qe, last);
+    vo += __shfl(ve, last);
+  }
+  if (mode == 0 && lane == 0) {
+    s_rows[s] = row - row0;
+    s_qb[s] = qo - qo0;
+    s_vb[s] = vo - vo0;
+  }
 }
 
 // series point offsets from per-row output offsets (rows sorted by series)

@@ -17,6 +17,7 @@
 #include <type_traits>
 #include <vector>
 
+#include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_segmented_radix_sort.hpp>
 
 #include "../../include/otsdb_agg.h"
@@ -694,7 +695,8 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         case 80: case 40: case 97: case 85: case 89: case 49: case 82: case 42: case 96:
         case 201: case 202: case 203: case 204: case 205: case 206:
         case 401: case 402: case 403: case 404: case 405: case 406:
-        case 407: case 408: case 409:
+        case 407: case 408: case 409: case 410: case 411: case 412:
+        case 413: case 414: case 415:
           if constexpr (std::is_same<M, MSum<1>>::value) {
             const int v = c->bucketize_k;
             Params P0 = P;  // 80/40: the generic (branchy) fold only
@@ -726,6 +728,24 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
                                  grid, blk, 0, st, P, B, W.SM, W.R);
             } else if (v == 409) {
               hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 512, 256>),
+                                 grid, blk, 0, st, P, B, W.SM, W.R);
+            } else if (v == 410) {  // production + next-step prefetch
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 1, 0, 1, 0, 1, 256, 64>),
+                                 grid, blk, 0, st, P, B, W.SM, W.R);
+            } else if (v == 411) {  // prefetch + 4 KiB flushes
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 1, 0, 1, 0, 1, 1024, 512>),
+                                 grid, blk, 0, st, P, B, W.SM, W.R);
+            } else if (v == 413) {  // production, >= 5 waves / SIMD
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 5, 0, 1, 256, 64>),
+                                 grid, blk, 0, st, P, B, W.SM, W.R);
+            } else if (v == 414) {  // production, >= 6 waves / SIMD
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 6, 0, 1, 256, 64>),
+                                 grid, blk, 0, st, P, B, W.SM, W.R);
+            } else if (v == 415) {  // prefetch, >= 4 waves / SIMD
+              hipLaunchKernelGGL((k_bucketize_k<M, 8, 1, 0, 4, 0, 1, 256, 64>),
+                                 grid, blk, 0, st, P, B, W.SM, W.R);
+            } else if (v == 412) {  // K=4 + prefetch
+              hipLaunchKernelGGL((k_bucketize_k<M, 4, 1, 0, 1, 0, 1, 256, 64>),
                                  grid, blk, 0, st, P, B, W.SM, W.R);
             } else if (v >= 201 && v <= 206) {  // LDS-DMA staged variants
               auto L = [&](auto kern, int wpb) {
@@ -1578,21 +1598,33 @@ otsdb_status otsdb_decode_cells_device(otsdb_ctx* c, const otsdb_cells* cells,
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   const int64_t R = cells->n_rows, S = n_series;
   if (R < 0 || S < 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
-  // workspace: row counts + row output offsets
-  otsdb_status rc = ensure(&c->dec_ws, &c->dec_ws_cap, (size_t)(2 * R + 2) * 8);
+  // workspace: row counts, row output offsets, uniform-column flags and the
+  // device scan's temporary storage
+  size_t scan_tmp = 0;
+  HIP_TRY(rocprim::exclusive_scan(nullptr, scan_tmp, (const int64_t*)nullptr,
+                                  (int64_t*)nullptr, (int64_t)0,
+                                  (size_t)(R + 1), rocprim::plus<int64_t>(),
+                                  st));
+  const size_t ws_need = (size_t)(2 * R + 2) * 8 + (size_t)R + 64 + scan_tmp;
+  otsdb_status rc = ensure(&c->dec_ws, &c->dec_ws_cap, ws_need);
   if (rc) return rc;
   int64_t* row_count = (int64_t*)c->dec_ws;
   int64_t* row_out = row_count + (R + 1);
+  uint8_t* fast = (uint8_t*)(row_out + (R + 1));
+  void* tmp = (void*)(((uintptr_t)(fast + R) + 63) & ~(uintptr_t)63);
   CellsDev C{R, cells->row_series, cells->row_base_s, cells->qual_off,
              cells->qual, cells->val_off, cells->val};
   HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), st));
   if (R > 0) {
     hipLaunchKernelGGL(k_decode, dim3(blocks_for(R, 4)), dim3(256), 0, st, C,
-                       0, row_count, (const int64_t*)nullptr, (int64_t)0,
+                       0, row_count, (const int64_t*)nullptr, fast, (int64_t)0,
                        (int64_t*)nullptr, (int64_t*)nullptr,
                        (uint8_t*)nullptr, c->d_err);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, R,
-                       (const int64_t*)row_count, row_out);
+    // row_count[R] = 0, so row_out[R] = the total
+    HIP_TRY(hipMemsetAsync(row_count + R, 0, 8, st));
+    HIP_TRY(rocprim::exclusive_scan(tmp, scan_tmp, (const int64_t*)row_count,
+                                    row_out, (int64_t)0, (size_t)(R + 1),
+                                    rocprim::plus<int64_t>(), st));
   } else {
     HIP_TRY(hipMemsetAsync(row_out, 0, 8, st));
   }
@@ -1614,8 +1646,34 @@ otsdb_status otsdb_decode_cells_device(otsdb_ctx* c, const otsdb_cells* cells,
                 (long long)capacity, (long long)total);
   if (R > 0)
     hipLaunchKernelGGL(k_decode, dim3(blocks_for(R, 4)), dim3(256), 0, st, C,
-                       1, row_count, (const int64_t*)row_out, capacity, ts_ms,
-                       val, is_float, c->d_err);
+                       1, row_count, (const int64_t*)row_out, fast, capacity,
+                       ts_ms, val, is_float, c->d_err);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(st));
+  return OTSDB_OK;
+}
+
+otsdb_status otsdb_encode_cells_device(otsdb_ctx* c, const otsdb_batch* b,
+                                       int64_t* series_rows,
+                                       int64_t* series_qbytes,
+                                       int64_t* series_vbytes,
+                                       const otsdb_cells_out* o,
+                                       void* hip_stream) {
+  if (!c || !b || !series_rows || !series_qbytes || !series_vbytes)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  if (b->is_float)
+    return fail(OTSDB_E_UNSUPPORTED, "per-point value types: use series_float");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  const int64_t S = b->n_series;
+  if (S > 0)
+    hipLaunchKernelGGL(k_encode, dim3(blocks_for(S, 4)), dim3(256), 0, st, S,
+                       b->offsets, b->ts_ms, b->val, b->series_float,
+                       o ? 1 : 0, series_rows, series_qbytes, series_vbytes,
+                       o ? o->row_series : nullptr, o ? o->row_base_s : nullptr,
+                       o ? o->qual_off : nullptr, o ? o->val_off : nullptr,
+                       o ? o->qual : nullptr, o ? o->val : nullptr);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(st));
   return OTSDB_OK;
@@ -1662,7 +1720,7 @@ otsdb_status otsdb_gen_counts_device(otsdb_ctx* c, const otsdb_gen_spec* g,
   if (g->cadence_ms <= 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "cadence");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
-  GenP gp{g->seed, g->t0_ms, g->duration_ms, g->cadence_ms, g->kind};
+  GenP gp{g->seed, g->t0_ms, g->duration_ms, g->cadence_ms, g->kind, g->flags};
   if (n_series > 0)
     hipLaunchKernelGGL(k_gen_counts, dim3(blocks_for(n_series, 4)), dim3(256),
                        0, st, gp, series0, n_series, counts);
@@ -1679,7 +1737,7 @@ otsdb_status otsdb_gen_fill_device(otsdb_ctx* c, const otsdb_gen_spec* g,
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
-  GenP gp{g->seed, g->t0_ms, g->duration_ms, g->cadence_ms, g->kind};
+  GenP gp{g->seed, g->t0_ms, g->duration_ms, g->cadence_ms, g->kind, g->flags};
   if (n_series > 0)
     hipLaunchKernelGGL(k_gen_fill, dim3(blocks_for(n_series, 4)), dim3(256),
                        0, st, gp, series0, n_series, offsets, ts_ms, val);

@@ -1461,6 +1461,7 @@ struct GenP {
   uint64_t seed;
   int64_t t0_ms, duration_ms, cadence_ms;
   int kind;
+  int flags;  // otsdb_gen_spec.flags: 1 = whole-second phases
 };
 
 DEV GenSeries gen_params(const GenP& g, int64_t s) {
@@ -1472,6 +1473,7 @@ DEV GenSeries gen_params(const GenP& g, int64_t s) {
   p.key = key;
   p.n = g.duration_ms / g.cadence_ms;
   p.phase = (int64_t)(r[0] % (uint64_t)g.cadence_ms);
+  if (g.flags & 1) p.phase -= p.phase % 1000;
   p.first = 0;
   p.last = p.n;
   if (p.n > 1 && (r[1] % 100) < 5) {

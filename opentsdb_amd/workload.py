@@ -162,3 +162,79 @@ def generate_device(engine, gspec, series0, n_series, group_size=None,
                      torch.from_numpy(members).to(device), None, sf)
     db.n_points_total = N
     return db
+
+
+class DeviceCells:
+    """Compacted RowSeq columns in HBM (otsdb_cells), kept alive with their
+    torch tensors."""
+
+    def __init__(self, t, n_series):
+        self.t = t
+        self.n_series = n_series
+        self.n_rows = t["row_series"].numel()
+        self.n_bytes = (t["qual"].numel() + t["val"].numel() +
+                        16 * self.n_rows)
+
+    def as_abi(self):
+        t = self.t
+        return abi.Cells(self.n_rows, t["row_series"].data_ptr(),
+                         t["row_base_s"].data_ptr(), t["qual_off"].data_ptr(),
+                         t["qual"].data_ptr(), t["val_off"].data_ptr(),
+                         t["val"].data_ptr())
+
+
+def encode_cells_device(engine, db):
+    """The columnar DeviceBatch db as compacted cells in HBM
+    (otsdb_encode_cells_device: count, scan, fill)."""
+    import ctypes as C
+    import torch
+    dev = db.ts.device
+    S = db.n_series
+    cnt = [torch.zeros(S, dtype=torch.int64, device=dev) for _ in range(3)]
+    b = db.as_abi()
+    engine._check(engine.lib.otsdb_encode_cells_device(
+        engine.ctx, C.byref(b), cnt[0].data_ptr(), cnt[1].data_ptr(),
+        cnt[2].data_ptr(), None, None))
+    tot = [int(c.sum().item()) for c in cnt]
+    base = [torch.cumsum(c, 0) - c for c in cnt]  # exclusive prefix sums
+    R, Q, V = tot
+    t = dict(row_series=torch.empty(max(R, 1), dtype=torch.int64, device=dev),
+             row_base_s=torch.empty(max(R, 1), dtype=torch.int64, device=dev),
+             qual_off=torch.empty(R + 1, dtype=torch.int64, device=dev),
+             val_off=torch.empty(R + 1, dtype=torch.int64, device=dev),
+             qual=torch.zeros(Q + 16, dtype=torch.uint8, device=dev),
+             val=torch.zeros(V + 16, dtype=torch.uint8, device=dev))
+    out = abi.CellsOut(t["row_series"].data_ptr(), t["row_base_s"].data_ptr(),
+                       t["qual_off"].data_ptr(), t["qual"].data_ptr(),
+                       t["val_off"].data_ptr(), t["val"].data_ptr())
+    engine._check(engine.lib.otsdb_encode_cells_device(
+        engine.ctx, C.byref(b), base[0].data_ptr(), base[1].data_ptr(),
+        base[2].data_ptr(), C.byref(out), None))
+    t["qual_off"][R] = Q
+    t["val_off"][R] = V
+    t["row_series"] = t["row_series"][:R]
+    t["row_base_s"] = t["row_base_s"][:R]
+    torch.cuda.synchronize()
+    return DeviceCells(t, S)
+
+
+def decode_cells_device(engine, cells, capacity=None):
+    """otsdb_decode_cells_device -> (offsets, ts, val, is_float) tensors."""
+    import ctypes as C
+    import torch
+    dev = cells.t["qual"].device
+    S = cells.n_series
+    offsets = torch.zeros(S + 1, dtype=torch.int64, device=dev)
+    c = cells.as_abi()
+    if capacity is None:
+        engine._check(engine.lib.otsdb_decode_cells_device(
+            engine.ctx, C.byref(c), S, offsets.data_ptr(), None, None, None,
+            0, None))
+        capacity = int(offsets[-1].item())
+    ts = torch.empty(max(capacity, 2), dtype=torch.int64, device=dev)
+    val = torch.empty_like(ts)
+    isf = torch.empty(max(capacity, 2), dtype=torch.uint8, device=dev)
+    engine._check(engine.lib.otsdb_decode_cells_device(
+        engine.ctx, C.byref(c), S, offsets.data_ptr(), ts.data_ptr(),
+        val.data_ptr(), isf.data_ptr(), capacity, None))
+    return offsets, ts[:capacity], val[:capacity], isf[:capacity]

@@ -1374,6 +1374,7 @@ static void gen_params(const otsdb_gen_spec* g, int64_t s, gen_series* p) {
   p->key = key;
   p->n = g->duration_ms / g->cadence_ms;
   p->phase = (int64_t)(r[0] % (uint64_t)g->cadence_ms);
+  if (g->flags & 1) p->phase -= p->phase % 1000;
   p->first = 0;
   p->last = p->n;
   if (p->n > 1 && (r[1] % 100) < 5) {

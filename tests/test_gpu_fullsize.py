@@ -1,0 +1,142 @@
+"""Parity at the BASELINE configurations' full per-GPU sizes.
+
+The batch is the bench's own (SURVEY §8d generator, generated in HBM, every
+series of the configuration: C2 100k series x 7 days = 5.7 G points) and the
+whole query runs on it.  The oracle cannot finish a full 5.7 G-point query in
+test time, so parity is checked where it is size independent: groups are
+independent, so a sample of whole groups (C1/C2/C3: the configuration's own
+groups; C4/C5, one group of every series: a seeded random subset of
+full-length series made its own group, the rest another) is copied back and
+run through the oracle, bit-exact for order-free results and within 1e-12
+relative for sums / averages / deviations.  Every group's timestamps must
+increase, stay on the grid and inside the window.
+"""
+import numpy as np
+import pytest
+
+from opentsdb_amd import workload
+from opentsdb_amd.batch import HostBatch, groups_from_ids
+from opentsdb_amd.engine import DataPoints, DeviceResult, run_device
+from oracle import pyoracle
+from tests.test_gpu_parity import compare, engine  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+
+def _series_to_host(db, series, group_ids):
+    """HostBatch of the given series (device batch slices, one D2H copy),
+    grouped by group_ids (one per series, dense)."""
+    import torch
+    offs = db.offsets.cpu().numpy()
+    lens = offs[series + 1] - offs[series]
+    idx = torch.cat([torch.arange(int(offs[s]), int(offs[s + 1]),
+                                  device=db.ts.device) for s in series])
+    ts = db.ts[idx].cpu().numpy()
+    val = db.val[idx].cpu().numpy()
+    sf = db.series_float[torch.as_tensor(series, device=db.ts.device)]
+    ho = np.zeros(len(series) + 1, np.int64)
+    np.cumsum(lens, out=ho[1:])
+    g_off, members = groups_from_ids(np.asarray(group_ids, np.int64))
+    return HostBatch(ho, ts, val, None, sf.cpu().numpy(), g_off, members)
+
+
+def _result_groups(res, groups):
+    offs = res.offsets.cpu().numpy()
+    out = []
+    for g in groups:
+        a, b = int(offs[g]), int(offs[g + 1])
+        out.append(DataPoints(res.ts[a:b].cpu().numpy(),
+                              res.val[a:b].cpu().numpy(),
+                              res.is_int[a:b].cpu().numpy()))
+    return out
+
+
+def _check_grid(res, spec, nb):
+    """Every group: strictly increasing timestamps on the downsample grid,
+    inside the window, at most nb points."""
+    offs = res.offsets.cpu().numpy()
+    ts = res.ts[:int(offs[-1])].cpu().numpy()
+    cnt = np.diff(offs)
+    assert (cnt <= nb).all()
+    if len(ts):
+        assert ts.min() >= spec.start_ms - spec.ds_interval_ms
+        assert ts.max() <= spec.end_ms
+        assert ((ts - ts.min()) % spec.ds_interval_ms == 0).all()
+        d = np.diff(ts)
+        starts = offs[1:-1][(offs[1:-1] > 0) & (offs[1:-1] < len(ts))]
+        d[starts - 1] = 1  # group boundaries
+        assert (d > 0).all()
+
+
+def _run(eng, spec, db):
+    import torch
+    sz = eng.plan(spec, db)
+    res = DeviceResult(torch, db.n_groups, int(sz.max_out_points), "cuda")
+    run_device(eng, spec, db, res)
+    torch.cuda.synchronize()
+    return res, int(sz.n_buckets)
+
+
+def _free():
+    import gc
+    import torch
+    gc.collect()
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("config,n_check", [("C1", 100), ("C2", 40),
+                                            ("C3", 2)])
+def test_full_size_own_groups(engine, config, n_check):  # noqa: F811
+    """The configuration's own groups ({host=*} / {dc=*}): a seeded sample
+    of whole groups against the oracle."""
+    n = workload.default_series_per_gpu(config)
+    g = workload.gen_spec(config)
+    db = workload.generate_device(engine, g, 0, n, config=config)
+    spec = workload.query_spec(config)
+    res, nb = _run(engine, spec, db)
+    _check_grid(res, spec, nb)
+    G = db.n_groups
+    rng = np.random.default_rng(7)
+    pick = np.sort(rng.choice(G, size=min(n_check, G), replace=False))
+    goff = db.group_offsets.cpu().numpy()
+    mem = db.group_members.cpu().numpy()
+    series, gid = [], []
+    for j, gg in enumerate(pick):
+        m = mem[goff[gg]:goff[gg + 1]]
+        series.extend(m.tolist())
+        gid.extend([j] * len(m))
+    hb = _series_to_host(db, np.asarray(series, np.int64), gid)
+    ref = pyoracle.group_by(spec, hb)
+    got = _result_groups(res, pick)
+    compare(got, ref, False, scale=100.0, where="%s-full" % config)
+    del db, res
+    _free()
+
+
+@pytest.mark.parametrize("config,n_sub", [("C4", 1500), ("C5", 3000)])
+def test_full_size_subset_group(engine, config, n_sub):  # noqa: F811
+    """One-group configurations: every series of the configuration is
+    aggregated; a seeded random subset of full-length series forms group 0
+    (checked against the oracle), the rest group 1."""
+    import torch
+    n = workload.default_series_per_gpu(config)
+    g = workload.gen_spec(config)
+    db = workload.generate_device(engine, g, 0, n, config=config)
+    rng = np.random.default_rng(11)
+    sub = np.sort(rng.choice(n, size=n_sub, replace=False))
+    gid = np.ones(n, np.int64)
+    gid[sub] = 0
+    g_off, members = groups_from_ids(gid)
+    db.group_offsets = torch.from_numpy(g_off).cuda()
+    db.group_members = torch.from_numpy(members).cuda()
+    spec = workload.query_spec(config)
+    res, nb = _run(engine, spec, db)
+    _check_grid(res, spec, nb)
+    hb = _series_to_host(db, sub, np.zeros(n_sub, np.int64))
+    ref = pyoracle.group_by(spec, hb)
+    got = _result_groups(res, [0])
+    # C5's p99 selects among 1m-avg values, whose sums the GPU associates
+    # differently (lane tree): within 1e-12, not bit-exact
+    compare(got, ref, False, scale=100.0, where="%s-full" % config)
+    del db, res
+    _free()
