@@ -53,7 +53,7 @@ def decode_figure(eng, config, n_series, reps=5):
     db = workload.generate_device(eng, g, 0, n_series, config=config)
     n = db.n_points_total
     cells = workload.encode_cells_device(eng, db)
-    del db
+    db.ts = db.val = None  # keep the group arrays only
     torch.cuda.empty_cache()
     workload.decode_cells_device(eng, cells, capacity=n)  # warm-up
     torch.cuda.synchronize()
@@ -63,7 +63,29 @@ def decode_figure(eng, config, n_series, reps=5):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t) / reps
     cb = cells.n_bytes
-    del out, cells
+    del out
+    torch.cuda.empty_cache()
+    # the whole query straight from the cells: decode fused into the
+    # downsample (otsdb_agg_run_cells_device)
+    from opentsdb_amd.engine import DeviceResult
+    spec = workload.query_spec(config)
+    res = DeviceResult(torch, db.n_groups, db.n_groups * 2100, "cuda")
+    workload.run_cells_device(eng, spec, cells, db, res)  # warm-up
+    eng.lib.otsdb_prof_enable(eng.ctx, 1)
+    eng.lib.otsdb_prof_read(eng.ctx, None, None, 0, 1)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        workload.run_cells_device(eng, spec, cells, db, res)
+    torch.cuda.synchronize()
+    dq = (time.perf_counter() - t) / reps
+    import ctypes as C
+    ms = (C.c_double * 8)()
+    nn = (C.c_int64 * 8)()
+    eng.lib.otsdb_prof_read(eng.ctx, ms, nn, 8, 1)
+    eng.lib.otsdb_prof_enable(eng.ctx, 0)
+    kb = ms[0] / max(nn[0], 1) / 1e3
+    del cells, res, db
     torch.cuda.empty_cache()
     return {"kernel": "k_decode (count + scan + write)",
             "points": n, "ms": dt * 1e3, "value": n / dt,
@@ -71,7 +93,15 @@ def decode_figure(eng, config, n_series, reps=5):
             "compacted_bytes": cb, "compacted_bytes_per_point": cb / n,
             "achieved_GBs": (cb + 17 * n) / dt / 1e9,
             "note": "reads the compacted cells, writes ts/val/is_float "
-                    "(17 B/point); not part of the headline value"}
+                    "(17 B/point); not part of the headline value",
+            "fused_query": {
+                "what": "the same C2 query straight from the cells, decode "
+                        "fused into the downsample (k_bucketize_cells)",
+                "value": n / dq, "unit": "data points/s",
+                "ms_per_query": dq * 1e3,
+                "k_bucketize_cells_ms": kb * 1e3,
+                "achieved_GBs_compacted": cb / kb / 1e9 if kb else None,
+                "frac_of_8TBs": cb / kb / 8e12 if kb else None}}
 
 
 def cpu_baseline(config, target_s):

@@ -352,6 +352,20 @@ otsdb_status otsdb_encode_cells_device(otsdb_ctx* ctx, const otsdb_batch* batch,
                                        const otsdb_cells_out* cells,
                                        void* hip_stream);
 
+/* The query straight from compacted columns (DEVICE pointers): the decode
+ * runs fused into the downsample (no columnar copy).
+ * `batch` supplies n_series and the groups only (its point arrays are not
+ * read); series s owns the rows with row_series == s.  A corrupt column is
+ * OTSDB_E_ILLEGAL_DATA.  Queries the fused path does not cover (raw
+ * group-by, median / percentile or "all" downsampling, columns mixing 2-
+ * and 4-byte qualifiers) are decoded into a context-owned columnar buffer
+ * first and run through the columnar pipeline — same results.           */
+otsdb_status otsdb_agg_run_cells_device(otsdb_ctx* ctx,
+                                        const otsdb_query_spec* spec,
+                                        const otsdb_cells* cells,
+                                        const otsdb_batch* batch,
+                                        otsdb_result* out, void* hip_stream);
+
 /* ---- stage timing (bench roofline) ------------------------------------- */
 /* When enabled, every query records HIP events around its pipeline stages
  * on the query's stream.  otsdb_prof_read returns, per stage, the summed

@@ -123,7 +123,7 @@ EXPORTS = [
     "otsdb_gen_fill_device", "otsdb_prof_enable", "otsdb_prof_read",
     "otsdb_decode_cells_device", "otsdb_sel_prepare_device",
     "otsdb_sel_hist_device", "otsdb_sel_finish_device",
-    "otsdb_encode_cells_device",
+    "otsdb_encode_cells_device", "otsdb_agg_run_cells_device",
 ]
 
 _lib = None
@@ -190,6 +190,9 @@ def load(path=None):
     lib.otsdb_encode_cells_device.argtypes = [vp, PB, vp, vp, vp,
                                               C.POINTER(CellsOut), vp]
     lib.otsdb_encode_cells_device.restype = C.c_int
+    lib.otsdb_agg_run_cells_device.argtypes = [vp, PS, C.POINTER(Cells), PB,
+                                               PR, vp]
+    lib.otsdb_agg_run_cells_device.restype = C.c_int
     lib.otsdb_prof_enable.argtypes = [vp, C.c_int]
     lib.otsdb_prof_enable.restype = C.c_int
     lib.otsdb_prof_read.argtypes = [vp, vp, vp, C.c_int, C.c_int]

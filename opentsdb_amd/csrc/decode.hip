@@ -404,6 +404,310 @@ __global__ __launch_bounds__(256) void k_encode(
   }
 }
 
+// ------------------------------------------------------------------------
+// k_bucketize_cells: decode fused into the downsample.
+// One wavefront per series walks its compacted columns in row order and
+// feeds the decoded points straight into k_bucketize_k's reduction
+// (reduce_step): the compacted bytes (10 B / point for seconds + doubles)
+// are read once and no columnar copy is written.  Each step of 64*K points
+// stages the step's qualifier bytes, then its value bytes, through the
+// wave's LDS with aligned 16-byte loads (the columns sit at any byte offset
+// and a lane's values are 8 bytes apart: direct loads would touch eight
+// times the cache lines); values may have any legal length per point (long
+// counters are stored in 1/2/4/8 bytes) — their offsets are a wave prefix
+// sum of the lengths.  What k_prep derives from columnar timestamps is
+// derived from the cells: the SpanGroup.add filter from the series' first
+// and last point, the seek / stop window per step, and the first bucket
+// past the window (lane 0 walks its points in order, as k_prep does).
+// Closed buckets go straight to the row with their state byte.  Columns
+// must have one qualifier width (no MS_MIXED_COMPACT; the write path emits
+// one per resolution): a series holding a mixed column raises
+// ERR_CELLS_GENERIC and the host decodes instead.  Corrupt columns (illegal
+// value lengths, value bytes that do not add up) raise ERR_CORRUPT_CELL
+// (Internal.extractDataPoints, Internal.java:307-321).
+// ------------------------------------------------------------------------
+enum : int { ERR_CELLS_GENERIC = 1 << 20 };
+
+struct CellRow {
+  const uint8_t* q;
+  int64_t n, vbase, vlen, base_ms;
+  int qw;
+  bool ok;
+};
+
+DEV CellRow cell_row(const CellsDev& C, int64_t r) {
+  CellRow w;
+  const int64_t qo = C.qual_off[r], qlen = C.qual_off[r + 1] - qo;
+  w.q = C.qual + qo;
+  w.vbase = C.val_off[r];
+  w.vlen = C.val_off[r + 1] - w.vbase;
+  w.base_ms = C.row_base_s[r] * 1000;
+  w.qw = (qlen > 0 && (w.q[0] & 0xF0) == 0xF0) ? 4 : 2;
+  w.n = qlen / w.qw;
+  w.ok = qlen > 0 && qlen % w.qw == 0 && !((uintptr_t)w.q & 1);
+  return w;
+}
+
+DEV uint32_t cell_qual(const CellRow& w, int64_t i) {
+  const uint16_t* h = reinterpret_cast<const uint16_t*>(w.q + w.qw * i);
+  const uint32_t a = __builtin_bswap16(h[0]);
+  return w.qw == 2 ? a : (a << 16) | __builtin_bswap16(h[1]);
+}
+
+DEV int64_t qual_ts(int64_t base_ms, int qw, uint32_t qv) {
+  return qw == 4 ? base_ms + (int64_t)((qv & 0x0FFFFFC0u) >> 6)
+                 : base_ms + (int64_t)((qv & 0xFFFFu) >> 4) * 1000;
+}
+
+// the folded double of a value (RowSeq longValue/doubleValue -> toDouble,
+// RowSeq.java:552-643)
+DEV int64_t dbits_of(uint64_t x, int vl, int fl) {
+  const int64_t bits = value_bits(x, vl, fl);
+  return fl ? bits : __double_as_longlong((double)bits);
+}
+
+DEV void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// copies bytes [src, src + n) into lds with aligned 16-byte loads (whole
+// 16-byte blocks around the range: never past a page); returns where src's
+// first byte landed
+DEV int stage16(uint8_t* lds, const uint8_t* src, int64_t n) {
+  const uintptr_t a = (uintptr_t)src, al = a & ~(uintptr_t)15;
+  const int sh = (int)(a - al);
+  const int nch = (int)((sh + n + 15) >> 4);
+  for (int c = LANE; c < nch; c += 64)
+    *reinterpret_cast<uint4*>(lds + 16 * c) =
+        *reinterpret_cast<const uint4*>(al + 16 * (uintptr_t)c);
+  wave_lds_fence();
+  return sh;
+}
+
+DEV uint64_t lds_be(const uint8_t* lds, int o, int vl) {
+  const int al = o & ~7;
+  const uint64_t lo = *reinterpret_cast<const uint64_t*>(lds + al);
+  const uint64_t hi = *reinterpret_cast<const uint64_t*>(lds + al + 8);
+  const int sh = (o - al) * 8;
+  const uint64_t w = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+  return __builtin_bswap64(w) >> (64 - 8 * vl);
+}
+
+__global__ void k_series_rows(int64_t R, int64_t S,
+                              const int64_t* __restrict__ row_series,
+                              int64_t* __restrict__ series_row) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > R) return;
+  const int64_t prev = r == 0 ? -1 : row_series[r - 1];
+  const int64_t cur = r == R ? S : row_series[r];
+  for (int64_t s = prev + 1; s <= cur && s <= S; ++s) series_row[s] = r;
+}
+
+template <class M, int K>
+__global__ __launch_bounds__(256) void k_bucketize_cells(
+    Params P, CellsDev C, const int64_t* __restrict__ series_row, int64_t S,
+    SeriesMeta SM, Rows R, int* err_word) {
+  static_assert(K % 2 == 0, "K");
+  constexpr int PTS = 64 * K;
+  __shared__ __attribute__((aligned(16))) uint8_t lq_all[4][PTS * 4 + 32];
+  __shared__ __attribute__((aligned(16))) uint8_t lv_all[4][PTS * 8 + 32];
+  const int lane = LANE;
+  const int wv = threadIdx.x >> 6;
+  const int64_t s = (int64_t)blockIdx.x * 4 + wv;
+  if (s >= S) return;
+  uint8_t* lq = lq_all[wv];
+  uint8_t* lv = lv_all[wv];
+  const int64_t r0 = series_row[s], r1 = series_row[s + 1];
+  auto meta = [&](bool keep, uint8_t of_has, int64_t of_ts, double of_val) {
+    if (lane == 0) {
+      SM.keep[s] = keep;
+      SM.lo[s] = 0;
+      SM.hi[s] = 0;
+      SM.of_has[s] = of_has;
+      SM.of_ts[s] = of_ts;
+      SM.of_val[s] = of_val;
+    }
+  };
+  // SpanGroup.add filter (SpanGroup.java:321-338) from the first and last
+  // point of the series
+  bool keep = r0 < r1;
+  if (keep) {
+    const CellRow a = cell_row(C, r0), z = cell_row(C, r1 - 1);
+    if (!a.ok || !z.ok) {
+      if (lane == 0) atomicOr(err_word, ERR_CELLS_GENERIC);
+      meta(false, 0, 0, 0.0);
+      return;
+    }
+    const int64_t t_first = qual_ts(a.base_ms, a.qw, cell_qual(a, 0));
+    const int64_t t_last = qual_ts(z.base_ms, z.qw, cell_qual(z, z.n - 1));
+    keep = t_first <= P.end_ms && t_last >= P.start_ms;
+  }
+  if (!keep) {
+    meta(false, 0, 0, 0.0);
+    return;
+  }
+  BatchDev Bd{0, nullptr, nullptr, nullptr, nullptr, nullptr};
+  RowSink Sk{R.val + s * P.nb, R.state + s * P.nb, nullptr, 0, 1, 1, 0, 0};
+  int err = 0, carry_key = INT32_MIN;
+  M carry = M::init();
+  int64_t stop_r = -1, stop_i = 0;  // first point at or past stop_ts
+  int generic = 0, corrupt = 0;
+  for (int64_t r = r0; r < r1 && stop_r < 0; ++r) {
+    const CellRow w = cell_row(C, r);
+    if (w.base_ms + 3600000 <= P.seek_ts) continue;  // hour row before seek
+    if (!w.ok) {
+      generic = 1;
+      break;
+    }
+    int64_t vpos = 0;  // value bytes of the row consumed so far
+    for (int64_t st0 = 0; st0 < w.n; st0 += PTS) {
+      const int n_st = (int)(w.n - st0 < PTS ? w.n - st0 : PTS);
+      // qualifiers of the step -> LDS -> K per lane
+      const int sq = stage16(lq, w.q + w.qw * st0, (int64_t)w.qw * n_st);
+      uint32_t qv[K];
+      int vl[K], lsum = 0, odd = 0, bad = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const int i = K * lane + j;
+        qv[j] = 0;
+        vl[j] = 0;
+        if (i < n_st) {
+          const uint16_t* h =
+              reinterpret_cast<const uint16_t*>(lq + sq + w.qw * i);
+          const uint32_t a = __builtin_bswap16(h[0]);
+          qv[j] = w.qw == 2 ? a : (a << 16) | __builtin_bswap16(h[1]);
+          const int mk = ((qv[j] >> (w.qw == 2 ? 8 : 24)) & 0xF0) == 0xF0;
+          odd |= (w.qw == 4) != (mk != 0);
+          vl[j] = (int)(qv[j] & 0x7) + 1;
+          if (qv[j] & 0x8) bad |= !(vl[j] == 4 || vl[j] == 8);
+          else bad |= !(vl[j] == 1 || vl[j] == 2 || vl[j] == 4 || vl[j] == 8);
+          lsum += vl[j];
+        }
+      }
+      generic |= __ballot(odd) != 0;
+      corrupt |= __ballot(bad) != 0;
+      if (generic || corrupt) break;
+      // value offsets: exclusive wave scan of the lanes' byte counts
+      int incl = lsum;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d);
+        if (lane >= d) incl += y;
+      }
+      const int step_bytes = __shfl(incl, 63);
+      if (vpos + step_bytes > w.vlen) {
+        corrupt = 1;
+        break;
+      }
+      const int sv = stage16(lv, C.val + w.vbase + vpos, step_bytes);
+      int off = sv + incl - lsum;
+      int64_t t[K], v[K];
+      int lt_seek = 0, lt_stop = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const int i = K * lane + j;
+        if (i < n_st) {
+          t[j] = qual_ts(w.base_ms, w.qw, qv[j]);
+          v[j] = dbits_of(lds_be(lv, off, vl[j]), vl[j], (qv[j] & 0x8) != 0);
+          off += vl[j];
+          lt_seek += t[j] < P.seek_ts;
+          lt_stop += t[j] < P.stop_ts;
+        } else {
+          t[j] = 0;
+          v[j] = 0;
+        }
+      }
+      vpos += step_bytes;
+      // valid points of the step are [lo, hi) in row indices (ts increase)
+      int sum_seek = lt_seek, sum_stop = lt_stop;
+      for (int d = 32; d >= 1; d >>= 1) {
+        sum_seek += __shfl_xor(sum_seek, d);
+        sum_stop += __shfl_xor(sum_stop, d);
+      }
+      const int64_t lo = st0 + sum_seek, hi = st0 + sum_stop;
+      if (hi > lo)
+        reduce_step<M, K, 1>(P, Bd, 1, lo, hi, st0, st0 + (int64_t)K * lane,
+                             t, v, Sk, err, carry_key, carry);
+      if (hi < st0 + n_st) {  // reached stop_ts inside this row
+        stop_r = r;
+        stop_i = hi;
+        break;
+      }
+      // LDS reuse by the next step: every lane is done reading
+      wave_lds_fence();
+    }
+    if (generic || corrupt) break;
+    // every value byte of the column used, the meta byte aside
+    if (stop_r < 0 && vpos + (w.n > 1 ? 1 : 0) != w.vlen) {
+      corrupt = 1;
+      break;
+    }
+  }
+  if (generic || corrupt) {
+    // a mixed column is parsed by the generic decode, which also judges
+    // whether it is corrupt
+    if (lane == 0)
+      atomicOr(err_word, generic ? ERR_CELLS_GENERIC : ERR_CORRUPT_CELL);
+    meta(false, 0, 0, 0.0);
+    return;
+  }
+  if (carry_key >= 0 && carry_key < P.nb && lane == 0)
+    Sk.put(carry_key, carry.finish(&err));
+  // the first bucket past the window (k_prep's of_val): lane 0 folds its
+  // points in order, across rows (NONE fill only, like k_prep)
+  uint8_t of_has = 0;
+  int64_t of_ts = 0;
+  double of_val = 0.0;
+  if (!P.run_all && P.fill == 0 && stop_r >= 0 && lane == 0) {
+    CellRow w = cell_row(C, stop_r);
+    // value offset of point stop_i: the lengths of the points before it
+    int64_t voff = 0;
+    for (int64_t i = 0; i < stop_i; ++i) voff += (cell_qual(w, i) & 0x7) + 1;
+    const int64_t vend = C.val_off[C.R];
+    const int64_t t = qual_ts(w.base_ms, w.qw, cell_qual(w, stop_i));
+    int64_t e;
+    bool ok = true;
+    if (P.cal) {
+      const int64_t k = cal_bucket(P, t);
+      ok = k >= P.cal_lo && k + 1 < P.cal_n;
+      of_ts = ok ? P.cal[k] : 0;
+      e = ok ? P.cal[k + 1] : 0;
+    } else {
+      of_ts = align_ts(t, P.interval);
+      e = of_ts + P.interval;
+    }
+    if (!ok) {
+      atomicOr(err_word, ERR_CAL_RANGE);
+    } else {
+      M st = M::init();
+      int64_t r = stop_r, i = stop_i;
+      while (r < r1) {
+        if (i >= w.n) {
+          if (++r >= r1) break;
+          w = cell_row(C, r);
+          if (!w.ok) break;
+          i = 0;
+          voff = 0;
+          continue;
+        }
+        const uint32_t q = cell_qual(w, i);
+        if (qual_ts(w.base_ms, w.qw, q) >= e) break;
+        const int l = (int)(q & 0x7) + 1;
+        st.push(bits_to_double(dbits_of(
+            load_be(C.val, w.vbase + voff, l, vend), l, (q & 0x8) != 0)));
+        voff += l;
+        ++i;
+      }
+      int e2 = 0;
+      of_val = st.finish(&e2);
+      of_has = 1;
+    }
+  }
+  if (__ballot(err) && lane == 0) atomicOr(err_word, err);
+  meta(true, of_has, of_ts, of_val);
+}
+
 // series point offsets from per-row output offsets (rows sorted by series)
 __global__ void k_series_offsets(int64_t R, int64_t S,
                                  const int64_t* __restrict__ row_series,

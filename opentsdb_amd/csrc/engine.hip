@@ -169,6 +169,10 @@ struct otsdb_ctx {
   size_t ev_used = 0;
   double prof_ms[8] = {0};
   int64_t prof_n[8] = {0};
+  void* cells_ws = nullptr;  // cells query: series row / point offsets
+  size_t cells_ws_cap = 0;
+  void* cells_col = nullptr;  // cells query fallback: decoded columns
+  size_t cells_col_cap = 0;
   void* cal = nullptr;  // calendar bucket edges of the current query
   size_t cal_cap = 0;
   int bucketize_k = 0;  // k_bucketize variant (OTSDB_BUCKETIZE_K; 0 = production)
@@ -570,10 +574,14 @@ void launch_combine(otsdb_ctx* c, const Work& W, int64_t NB, int64_t n,
 
 // Everything up to dense (group, bucket) results / partials.
 // mode 0: final dense results; mode 1: per-group partials into `gpart/gemit`
+// cells != null: the series come as compacted columns (k_bucketize_cells
+// decodes them inside the downsample; B carries only S)
 otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
                           const BatchDev& B, const int64_t* d_members,
                           std::vector<int64_t>& goff, Params& P, Work& W,
-                          int mode, Packed* gpart, uint8_t* gemit) {
+                          int mode, Packed* gpart, uint8_t* gemit,
+                          const CellsDev* cells = nullptr,
+                          const int64_t* series_row = nullptr) {
   hipStream_t st = c->stream;
   const int64_t S = B.S;
   const int64_t G = (int64_t)goff.size() - 1;
@@ -584,7 +592,8 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
 
   // grid trimming for very wide windows (NONE fill only): the rows span only
   // the buckets that hold data
-  if (!P.run_all && !P.fill && !P.cal && (double)S * (double)nb > 4.0e9) {
+  if (!cells && !P.run_all && !P.fill && !P.cal &&
+      (double)S * (double)nb > 4.0e9) {
     unsigned long long init[2] = {~0ULL, 0ULL};
     HIP_TRY(hipMemcpyAsync(c->d_mm, init, 16, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_bounds, dim3(blocks_for(S, 256)), dim3(256), 0, st, P,
@@ -655,12 +664,23 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   // an A/B compares kernels over the same workspace placement
   if (const char* k = getenv("OTSDB_BUCKETIZE_K")) c->bucketize_k = atoi(k);
 #endif
-  P.sentinel = !P.ds_sel && bucketize_uses_ring(c->bucketize_k, spec->ds_agg_id);
+  P.sentinel = !cells && !P.ds_sel &&
+               bucketize_uses_ring(c->bucketize_k, spec->ds_agg_id);
   if (S > 0 && NB > 0 && !P.sentinel)
     HIP_TRY(hipMemsetAsync(W.R.state, 0, (size_t)S * NB, st));
 
   bool ok = true;
-  if (S > 0 && NB > 0 && P.ds_sel) {
+  if (cells && S > 0 && NB > 0) {
+    // decode fused into the downsample (decode.hip)
+    ok = with_monoid(spec->ds_agg_id, [&](auto tag) {
+      using M = decltype(tag);
+      StageTimer tm(c, 0);
+      hipLaunchKernelGGL((k_bucketize_cells<M, 8>), dim3(blocks_for(S, 4)),
+                         dim3(256), 0, st, P, *cells, series_row, S, W.SM, W.R,
+                         c->d_err);
+    });
+    if (!ok) return fail(OTSDB_E_UNSUPPORTED, "downsampler %d", spec->ds_agg_id);
+  } else if (S > 0 && NB > 0 && P.ds_sel) {
     // median / percentile downsampling: per-bucket selection
     {
       StageTimer tm(c, 3);
@@ -1174,6 +1194,142 @@ otsdb_status run_device_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
   return finish(c, G, out);
 }
 
+// otsdb_decode_cells_device without the lock (also the fallback of the
+// fused cells query)
+otsdb_status decode_impl(otsdb_ctx* c, const otsdb_cells* cells,
+                         int64_t n_series, int64_t* offsets, int64_t* ts_ms,
+                         int64_t* val, uint8_t* is_float, int64_t capacity,
+                         hipStream_t st) {
+  const int64_t R = cells->n_rows, S = n_series;
+  if (R < 0 || S < 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
+  // workspace: row counts, row output offsets, uniform-column flags and the
+  // device scan's temporary storage
+  size_t scan_tmp = 0;
+  HIP_TRY(rocprim::exclusive_scan(nullptr, scan_tmp, (const int64_t*)nullptr,
+                                  (int64_t*)nullptr, (int64_t)0,
+                                  (size_t)(R + 1), rocprim::plus<int64_t>(),
+                                  st));
+  const size_t ws_need = (size_t)(2 * R + 2) * 8 + (size_t)R + 64 + scan_tmp;
+  otsdb_status rc = ensure(&c->dec_ws, &c->dec_ws_cap, ws_need);
+  if (rc) return rc;
+  int64_t* row_count = (int64_t*)c->dec_ws;
+  int64_t* row_out = row_count + (R + 1);
+  uint8_t* fast = (uint8_t*)(row_out + (R + 1));
+  void* tmp = (void*)(((uintptr_t)(fast + R) + 63) & ~(uintptr_t)63);
+  CellsDev C{R, cells->row_series, cells->row_base_s, cells->qual_off,
+             cells->qual, cells->val_off, cells->val};
+  HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), st));
+  if (R > 0) {
+    hipLaunchKernelGGL(k_decode, dim3(blocks_for(R, 4)), dim3(256), 0, st, C,
+                       0, row_count, (const int64_t*)nullptr, fast, (int64_t)0,
+                       (int64_t*)nullptr, (int64_t*)nullptr,
+                       (uint8_t*)nullptr, c->d_err);
+    // row_count[R] = 0, so row_out[R] = the total
+    HIP_TRY(hipMemsetAsync(row_count + R, 0, 8, st));
+    HIP_TRY(rocprim::exclusive_scan(tmp, scan_tmp, (const int64_t*)row_count,
+                                    row_out, (int64_t)0, (size_t)(R + 1),
+                                    rocprim::plus<int64_t>(), st));
+  } else {
+    HIP_TRY(hipMemsetAsync(row_out, 0, 8, st));
+  }
+  hipLaunchKernelGGL(k_series_offsets, dim3(blocks_for(R + 1, 256)), dim3(256),
+                     0, st, R, S, cells->row_series, (const int64_t*)row_out,
+                     offsets);
+  HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
+                         hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_small[1], row_out + R, 8, hipMemcpyDeviceToHost,
+                         st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (c->h_small[0] & ERR_CORRUPT_CELL)
+    return fail(OTSDB_E_ILLEGAL_DATA,
+                "Corrupted value: couldn't break down into individual values");
+  const int64_t total = c->h_small[1];
+  if (!ts_ms) return OTSDB_OK;
+  if (total > capacity)
+    return fail(OTSDB_E_CAPACITY, "decode capacity %lld < %lld points",
+                (long long)capacity, (long long)total);
+  if (R > 0)
+    hipLaunchKernelGGL(k_decode, dim3(blocks_for(R, 4)), dim3(256), 0, st, C,
+                       1, row_count, (const int64_t*)row_out, fast, capacity,
+                       ts_ms, val, is_float, c->d_err);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(st));
+  return OTSDB_OK;
+}
+
+// Query straight from compacted columns: the fused decode + downsample when
+// the query and the columns allow it, else decode -> columnar -> pipeline.
+otsdb_status run_cells_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
+                            const otsdb_cells* cells, const otsdb_batch* b,
+                            otsdb_result* out, std::vector<int64_t>& goff) {
+  otsdb_status rc = check_spec(spec);
+  if (rc) return rc;
+  hipStream_t st = c->stream;
+  const int64_t S = b->n_series, R = cells->n_rows;
+  if (S < 0 || R < 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
+  const bool ds = spec->ds_interval_ms > 0 || spec->run_all;
+  Params P;
+  rc = make_params(spec, &P, c);
+  if (rc) return rc;
+  CellsDev C{R, cells->row_series, cells->row_base_s, cells->qual_off,
+             cells->qual, cells->val_off, cells->val};
+  if (ds && !P.ds_sel && !P.run_all) {
+    rc = ensure(&c->cells_ws, &c->cells_ws_cap, (size_t)(S + 1) * 8);
+    if (rc) return rc;
+    int64_t* series_row = (int64_t*)c->cells_ws;
+    hipLaunchKernelGGL(k_series_rows, dim3(blocks_for(R + 1, 256)), dim3(256),
+                       0, st, R, S, cells->row_series, series_row);
+    BatchDev B{S, nullptr, nullptr, nullptr, nullptr, nullptr};
+    Work W;
+    rc = run_pipeline(c, spec, B, b->group_members, goff, P, W, 0, nullptr,
+                      nullptr, &C, series_row);
+    if (rc) return rc;
+    // a column the fused path does not take (ERR_CELLS_GENERIC): re-run
+    // through the decode below
+    HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const int e = (int)(c->h_small[0] & 0xFFFFFFFF);
+    if (e & ERR_CORRUPT_CELL)
+      return fail(OTSDB_E_ILLEGAL_DATA,
+                  "Corrupted value: couldn't break down into individual values");
+    if (!(e & ERR_CELLS_GENERIC)) {
+      const int64_t G = (int64_t)goff.size() - 1;
+      rc = compact(c, P, G, W.out_val, W.out_emit, W.counts, out);
+      if (rc) return rc;
+      return finish(c, G, out);
+    }
+  }
+  // decode to a columnar batch in the context's own buffer, then the
+  // columnar pipeline (raw group-by, median/percentile or "all" downsampling,
+  // mixed-width columns)
+  rc = ensure(&c->cells_ws, &c->cells_ws_cap, (size_t)(S + 1) * 8 + 64);
+  if (rc) return rc;
+  int64_t* offs = (int64_t*)c->cells_ws;
+  rc = decode_impl(c, cells, S, offs, nullptr, nullptr, nullptr, 0, st);
+  if (rc) return rc;
+  int64_t N = 0;
+  HIP_TRY(hipMemcpyAsync(&N, offs + S, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const size_t col = ((size_t)std::max<int64_t>(N, 2) * 8 + 255) & ~(size_t)255;
+  rc = ensure(&c->cells_col, &c->cells_col_cap,
+              2 * col + (size_t)std::max<int64_t>(N, 2) + 256);
+  if (rc) return rc;
+  int64_t* ts = (int64_t*)c->cells_col;
+  int64_t* vv = (int64_t*)((char*)c->cells_col + col);
+  uint8_t* isf = (uint8_t*)((char*)c->cells_col + 2 * col);
+  rc = decode_impl(c, cells, S, offs, ts, vv, isf, N, st);
+  if (rc) return rc;
+  otsdb_batch cb = *b;
+  cb.n_points = N;
+  cb.offsets = offs;
+  cb.ts_ms = ts;
+  cb.val = vv;
+  cb.is_float = isf;
+  cb.series_float = nullptr;
+  return run_device_impl(c, spec, &cb, out, goff);
+}
+
 }  // namespace
 
 // =========================================================================
@@ -1215,6 +1371,8 @@ void otsdb_ctx_destroy(otsdb_ctx* c) {
   if (c->dec_ws) hipFree(c->dec_ws);
   if (c->ws2) hipFree(c->ws2);
   if (c->cal) hipFree(c->cal);
+  if (c->cells_ws) hipFree(c->cells_ws);
+  if (c->cells_col) hipFree(c->cells_col);
   if (c->d_tiles) hipFree(c->d_tiles);
   if (c->d_err) hipFree(c->d_err);
   for (auto e : c->ev_pool) hipEventDestroy(e);
@@ -1277,6 +1435,24 @@ otsdb_status otsdb_agg_run_device(otsdb_ctx* c, const otsdb_query_spec* spec,
   std::vector<int64_t> goff;
   otsdb_status rc = read_goff(c, b, true, goff);
   if (!rc) rc = run_device_impl(c, spec, b, out, goff);
+  c->stream = saved;
+  return rc;
+}
+
+otsdb_status otsdb_agg_run_cells_device(otsdb_ctx* c,
+                                        const otsdb_query_spec* spec,
+                                        const otsdb_cells* cells,
+                                        const otsdb_batch* b,
+                                        otsdb_result* out, void* hip_stream) {
+  if (!c || !spec || !cells || !b || !out)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t saved = c->stream;
+  if (hip_stream) c->stream = (hipStream_t)hip_stream;
+  std::vector<int64_t> goff;
+  otsdb_status rc = read_goff(c, b, true, goff);
+  if (!rc) rc = run_cells_impl(c, spec, cells, b, out, goff);
   c->stream = saved;
   return rc;
 }
@@ -1596,61 +1772,8 @@ otsdb_status otsdb_decode_cells_device(otsdb_ctx* c, const otsdb_cells* cells,
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
-  const int64_t R = cells->n_rows, S = n_series;
-  if (R < 0 || S < 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
-  // workspace: row counts, row output offsets, uniform-column flags and the
-  // device scan's temporary storage
-  size_t scan_tmp = 0;
-  HIP_TRY(rocprim::exclusive_scan(nullptr, scan_tmp, (const int64_t*)nullptr,
-                                  (int64_t*)nullptr, (int64_t)0,
-                                  (size_t)(R + 1), rocprim::plus<int64_t>(),
-                                  st));
-  const size_t ws_need = (size_t)(2 * R + 2) * 8 + (size_t)R + 64 + scan_tmp;
-  otsdb_status rc = ensure(&c->dec_ws, &c->dec_ws_cap, ws_need);
-  if (rc) return rc;
-  int64_t* row_count = (int64_t*)c->dec_ws;
-  int64_t* row_out = row_count + (R + 1);
-  uint8_t* fast = (uint8_t*)(row_out + (R + 1));
-  void* tmp = (void*)(((uintptr_t)(fast + R) + 63) & ~(uintptr_t)63);
-  CellsDev C{R, cells->row_series, cells->row_base_s, cells->qual_off,
-             cells->qual, cells->val_off, cells->val};
-  HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), st));
-  if (R > 0) {
-    hipLaunchKernelGGL(k_decode, dim3(blocks_for(R, 4)), dim3(256), 0, st, C,
-                       0, row_count, (const int64_t*)nullptr, fast, (int64_t)0,
-                       (int64_t*)nullptr, (int64_t*)nullptr,
-                       (uint8_t*)nullptr, c->d_err);
-    // row_count[R] = 0, so row_out[R] = the total
-    HIP_TRY(hipMemsetAsync(row_count + R, 0, 8, st));
-    HIP_TRY(rocprim::exclusive_scan(tmp, scan_tmp, (const int64_t*)row_count,
-                                    row_out, (int64_t)0, (size_t)(R + 1),
-                                    rocprim::plus<int64_t>(), st));
-  } else {
-    HIP_TRY(hipMemsetAsync(row_out, 0, 8, st));
-  }
-  hipLaunchKernelGGL(k_series_offsets, dim3(blocks_for(R + 1, 256)), dim3(256),
-                     0, st, R, S, cells->row_series, (const int64_t*)row_out,
-                     offsets);
-  HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
-                         hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(&c->h_small[1], row_out + R, 8, hipMemcpyDeviceToHost,
-                         st));
-  HIP_TRY(hipStreamSynchronize(st));
-  if (c->h_small[0] & ERR_CORRUPT_CELL)
-    return fail(OTSDB_E_ILLEGAL_DATA,
-                "Corrupted value: couldn't break down into individual values");
-  const int64_t total = c->h_small[1];
-  if (!ts_ms) return OTSDB_OK;
-  if (total > capacity)
-    return fail(OTSDB_E_CAPACITY, "decode capacity %lld < %lld points",
-                (long long)capacity, (long long)total);
-  if (R > 0)
-    hipLaunchKernelGGL(k_decode, dim3(blocks_for(R, 4)), dim3(256), 0, st, C,
-                       1, row_count, (const int64_t*)row_out, fast, capacity,
-                       ts_ms, val, is_float, c->d_err);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(st));
-  return OTSDB_OK;
+  return decode_impl(c, cells, n_series, offsets, ts_ms, val, is_float,
+                     capacity, st);
 }
 
 otsdb_status otsdb_encode_cells_device(otsdb_ctx* c, const otsdb_batch* b,

@@ -333,11 +333,24 @@ DEV void sink_flush(RowSink& S, int64_t& flushed, int64_t limit) {
 // the lane that closes here.  All runs accumulate branch free with masked
 // pushes, in point order.  Returns false (nothing changed) when the lane
 // spans four or more buckets.
+// nv < K: only the first nv points are in range (the step reaches past the
+// end of the series / window); nv == 0 leaves the lane empty (nseg = 0).
 template <class M, int K, bool FLOATONLY>
 DEV bool fold_fast(const Params& P, const BatchDev& B, int sf, int64_t i0,
                    const int64_t* t, const int64_t* v, RowSink& S, int& err,
-                   int& nseg, int& cur_key, int& head_key, M& cur, M& head) {
-  const int k0 = bucket_narrow(P, t[0]), k1 = bucket_narrow(P, t[K - 1]);
+                   int& nseg, int& cur_key, int& head_key, M& cur, M& head,
+                   int nv = K) {
+  if (nv <= 0) {
+    nseg = 0;
+    return true;
+  }
+  int64_t tl = t[K - 1];
+  if (nv < K) {
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      if (j == nv - 1) tl = t[j];
+  }
+  const int k0 = bucket_narrow(P, t[0]), k1 = bucket_narrow(P, tl);
   if (k1 - k0 > 2) return false;
   // starts of the tail bucket k1 and of the middle bucket k0+1 (INT64_MIN
   // sends every point to the tail run)
@@ -351,9 +364,10 @@ DEV bool fold_fast(const Params& P, const BatchDev& B, int sf, int64_t i0,
   for (int j = 0; j < K; ++j) {
     const double x =
         FLOATONLY ? bits_to_double(v[j]) : point_value(B, i0 + j, v[j], sf);
-    const bool inh = t[j] < b_mid;
-    const bool inc = t[j] >= b_tail;
-    const bool inm = !inh && !inc;
+    const bool vj = j < nv;
+    const bool inh = vj && t[j] < b_mid;
+    const bool inc = vj && t[j] >= b_tail;
+    const bool inm = vj && !inh && !inc;
     h.push_if(inh, x);
     m.push_if(inm, x);
     c.push_if(inc, x);
@@ -457,23 +471,32 @@ DEV void reduce_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
   // last step; no per-point type test for all-double series)
   int nseg = 0, cur_key = 0, head_key = 0;
   M cur = M::init(), head = M::init();
-  if (base >= lo && base + PTS <= hi) {
+  const bool full = base >= lo && base + PTS <= hi;
+  // a step that only runs past hi (the last one): the fast fold still
+  // applies, each lane to its in-range prefix
+  const bool tail = !full && base >= lo && P.narrow;
+  if (full || tail) {
     const bool fonly = !B.is_float && sf;
     bool done = false;
+    const int64_t nr = hi - i0;
+    const int nv = full ? K : (int)(nr < 0 ? 0 : (nr > K ? K : nr));
     if (P.narrow) {
       done = fonly ? fold_fast<M, K, true>(P, B, sf, i0, t, v, S, err, nseg,
-                                           cur_key, head_key, cur, head)
+                                           cur_key, head_key, cur, head, nv)
                    : fold_fast<M, K, false>(P, B, sf, i0, t, v, S, err, nseg,
-                                            cur_key, head_key, cur, head);
+                                            cur_key, head_key, cur, head, nv);
     }
     if (!done) {
-      if (fonly)
+      if (full && fonly)
         fold_lane<M, K, true, false>(P, B, sf, i0, lo, hi, t, v, S,
                                      err, nseg, cur_key, head_key, cur, head);
-      else
+      else if (full)
         fold_lane<M, K, false, false>(P, B, sf, i0, lo, hi, t, v, S,
                                       err, nseg, cur_key, head_key, cur,
                                       head);
+      else
+        fold_lane<M, K, false, true>(P, B, sf, i0, lo, hi, t, v, S,
+                                     err, nseg, cur_key, head_key, cur, head);
     }
   } else {
     fold_lane<M, K, false, true>(P, B, sf, i0, lo, hi, t, v, S,

@@ -238,3 +238,20 @@ def decode_cells_device(engine, cells, capacity=None):
         engine.ctx, C.byref(c), S, offsets.data_ptr(), ts.data_ptr(),
         val.data_ptr(), isf.data_ptr(), capacity, None))
     return offsets, ts[:capacity], val[:capacity], isf[:capacity]
+
+
+def run_cells_device(engine, spec, cells, db_groups, result):
+    """otsdb_agg_run_cells_device: the query straight from compacted columns
+    (decode fused into the downsample).  db_groups: a DeviceBatch-like object
+    supplying n_series and the group arrays."""
+    import ctypes as C
+    b = abi.Batch()
+    b.n_series = cells.n_series
+    b.n_points = 0
+    b.n_groups = db_groups.n_groups
+    b.group_offsets = db_groups.group_offsets.data_ptr()
+    b.group_members = db_groups.group_members.data_ptr()
+    c = cells.as_abi()
+    r = result.as_abi()
+    engine._check(engine.lib.otsdb_agg_run_cells_device(
+        engine.ctx, C.byref(spec), C.byref(c), C.byref(b), C.byref(r), None))

@@ -165,3 +165,81 @@ def test_full_size_cells_roundtrip(engine, flags):
     del db, dc, offs, ts, val, isf
     gc.collect()
     torch.cuda.empty_cache()
+
+
+def _result_points(res, G):
+    from opentsdb_amd.engine import DataPoints
+    offs = res.offsets.cpu().numpy()
+    return [DataPoints(res.ts[offs[g]:offs[g + 1]].cpu().numpy(),
+                       res.val[offs[g]:offs[g + 1]].cpu().numpy(),
+                       res.is_int[offs[g]:offs[g + 1]].cpu().numpy())
+            for g in range(G)]
+
+
+FUSED = [("sum", "1m-avg", False), ("zimsum", "5m-sum", False),
+         ("avg", "10m-max", False), ("dev", "1m-min", False),
+         ("count", "2m-count", False), ("max", "1m-first-nan", False),
+         ("min", "1m-last-zero", False), ("p99", "1m-avg", False),
+         ("mimmax", "30s-max", False), ("sum", "1m-sum", True),
+         ("sum", "1hc-avg", False)]
+
+
+@pytest.mark.parametrize("agg,ds,rate", FUSED,
+                         ids=["%s:%s%s" % (a, d, ":rate" if r else "")
+                              for a, d, r in FUSED])
+@pytest.mark.parametrize("kind,seconds", [("float", True), ("int", True),
+                                          ("float", False)])
+def test_fused_cells_query(engine, agg, ds, rate, kind, seconds):
+    """otsdb_agg_run_cells_device (decode fused into the downsample) against
+    the oracle on the same points: timestamps and emission exact, values
+    bit-exact for order-free functions, 1e-12 otherwise."""
+    import torch
+    from opentsdb_amd import workload
+    from opentsdb_amd.engine import DeviceResult
+    from tests.test_gpu_parity import compare
+    hb = datasets.random_batch(29, n_series=40, n_groups=4, span_ms=4 * 3600000,
+                               value_kind=kind, counter=rate,
+                               cadence_ms=10000 if seconds else 7001)
+    if seconds:
+        hb.ts[:] = hb.ts - hb.ts % 1000
+        # keep the series strictly increasing after flooring
+        for s in range(hb.n_series):
+            a, b = hb.offsets[s], hb.offsets[s + 1]
+            assert (np.diff(hb.ts[a:b]) > 0).all()
+    isf = 1 if (kind == "float" and not rate) else 0
+    hb.is_float = np.full(len(hb.ts), isf, np.uint8)
+    db = _device_batch(hb, "float" if isf else "int")
+    cells_d = workload.encode_cells_device(engine, db)
+    d = core.DownsamplingSpecification(ds)
+    ro = core.RateOptions(True, core.LONG_MAX, 0) if rate else None
+    t0, t1 = datasets.T0 + 600000, datasets.T0 + 3 * 3600000
+    spec = core.make_spec(t0, t1, core.Aggregators.get(agg), d, t0, t1, rate,
+                          ro)
+    ref = pyoracle.group_by(spec, hb)
+    res = DeviceResult(torch, db.n_groups, 4 * len(hb.ts) + 64, "cuda")
+    workload.run_cells_device(engine, spec, cells_d, db, res)
+    got = _result_points(res, db.n_groups)
+    fn = ds.split("-")[1]
+    exact = fn in ("max", "min", "count", "first", "last") and agg in (
+        "max", "min", "count", "mimmax", "p99") and not rate
+    compare(got, ref, exact, scale=1e4, where="fused/%s/%s" % (agg, ds))
+
+
+def test_fused_cells_corrupt_column(engine):
+    """A column whose value bytes do not match its qualifiers:
+    IllegalDataException, as the decode (Internal.java:307-321)."""
+    import torch
+    from opentsdb_amd import workload
+    from opentsdb_amd.engine import DeviceResult
+    hb = datasets.random_batch(31, n_series=6, n_groups=1, span_ms=3600000)
+    hb.ts[:] = hb.ts - hb.ts % 1000
+    db = _device_batch(hb, "float")
+    cd = workload.encode_cells_device(engine, db)
+    # drop the last value byte of row 1: every later offset shifts
+    cd.t["val_off"][2:] -= 1
+    spec = core.make_spec(datasets.T0, datasets.T0 + 3600000,
+                          core.Aggregators.SUM,
+                          core.DownsamplingSpecification("1m-avg"))
+    res = DeviceResult(torch, db.n_groups, 4096, "cuda")
+    with pytest.raises(core.IllegalDataException):
+        workload.run_cells_device(engine, spec, cd, db, res)
