@@ -510,14 +510,15 @@ __global__ __launch_bounds__(256) void k_bucketize_cells(
     SeriesMeta SM, Rows R, int* err_word) {
   static_assert(K % 2 == 0, "K");
   constexpr int PTS = 64 * K;
-  __shared__ __attribute__((aligned(16))) uint8_t lq_all[4][PTS * 4 + 32];
-  __shared__ __attribute__((aligned(16))) uint8_t lv_all[4][PTS * 8 + 32];
+  constexpr int QB = PTS * 4 + 32, VB = PTS * 8 + 64;
+  // two buffers per wave: row r is read from one while row r + 1 lands in
+  // the other (LDS-DMA, no VGPRs in flight)
+  __shared__ __attribute__((aligned(16))) uint8_t lq_all[4][2][QB];
+  __shared__ __attribute__((aligned(16))) uint8_t lv_all[4][2][VB];
   const int lane = LANE;
   const int wv = threadIdx.x >> 6;
   const int64_t s = (int64_t)blockIdx.x * 4 + wv;
   if (s >= S) return;
-  uint8_t* lq = lq_all[wv];
-  uint8_t* lv = lv_all[wv];
   const int64_t r0 = series_row[s], r1 = series_row[s + 1];
   auto meta = [&](bool keep, uint8_t of_has, int64_t of_ts, double of_val) {
     if (lane == 0) {
@@ -553,18 +554,60 @@ __global__ __launch_bounds__(256) void k_bucketize_cells(
   M carry = M::init();
   int64_t stop_r = -1, stop_i = 0;  // first point at or past stop_ts
   int generic = 0, corrupt = 0;
-  for (int64_t r = r0; r < r1 && stop_r < 0; ++r) {
-    const CellRow w = cell_row(C, r);
-    if (w.base_ms + 3600000 <= P.seek_ts) continue;  // hour row before seek
+  // a row fits the prefetch buffers when it has <= PTS points; its whole
+  // qualifier and value byte ranges then go to LDS by DMA, issued while the
+  // previous row is being reduced
+  auto fits = [&](const CellRow& w) {
+    return w.ok && w.n <= PTS && w.vlen + 16 <= VB && w.qw * w.n + 16 <= QB;
+  };
+  auto prefetch = [&](const CellRow& w, int buf) -> int {  // DMA instrs
+    int k = 0;
+    const uintptr_t qa = (uintptr_t)w.q, qal = qa & ~(uintptr_t)15;
+    const int nq = (int)(((qa - qal) + w.qw * w.n + 15) >> 4);
+    for (int c0 = 0; c0 < nq; c0 += 64, ++k)
+      if (c0 + lane < nq)
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(qal + 16 * (uintptr_t)(c0 + lane)),
+            (void*)&lq_all[wv][buf][16 * c0], 16, 0, 0);
+    const uintptr_t va = (uintptr_t)(C.val + w.vbase),
+                    val_ = va & ~(uintptr_t)15;
+    const int nvb = (int)(((va - val_) + w.vlen + 15) >> 4);
+    for (int c0 = 0; c0 < nvb; c0 += 64, ++k)
+      if (c0 + lane < nvb)
+        __builtin_amdgcn_global_load_lds(
+            (const void*)(val_ + 16 * (uintptr_t)(c0 + lane)),
+            (void*)&lv_all[wv][buf][16 * c0], 16, 0, 0);
+    return k;
+  };
+  int64_t r = r0;
+  while (r < r1 && cell_row(C, r).base_ms + 3600000 <= P.seek_ts) ++r;
+  int buf = 0;
+  CellRow wn = r < r1 ? cell_row(C, r) : CellRow{};
+  if (r < r1 && fits(wn)) prefetch(wn, 0);
+  for (; r < r1 && stop_r < 0; ++r, buf ^= 1) {
+    const CellRow w = wn;
     if (!w.ok) {
       generic = 1;
       break;
+    }
+    const bool pre = fits(w);  // this row already sits in buffer buf
+    int n_next = 0;
+    if (r + 1 < r1) {
+      wn = cell_row(C, r + 1);
+      if (fits(wn)) n_next = prefetch(wn, buf ^ 1);
+    }
+    uint8_t* lq = lq_all[wv][buf];
+    uint8_t* lv = lv_all[wv][buf];
+    if (pre) {
+      wait_vmcnt(n_next);  // this row's DMA done, the next row's may fly
+      wave_lds_fence();
     }
     int64_t vpos = 0;  // value bytes of the row consumed so far
     for (int64_t st0 = 0; st0 < w.n; st0 += PTS) {
       const int n_st = (int)(w.n - st0 < PTS ? w.n - st0 : PTS);
       // qualifiers of the step -> LDS -> K per lane
-      const int sq = stage16(lq, w.q + w.qw * st0, (int64_t)w.qw * n_st);
+      const int sq = pre ? (int)((uintptr_t)w.q & 15)
+                         : stage16(lq, w.q + w.qw * st0, (int64_t)w.qw * n_st);
       uint32_t qv[K];
       int vl[K], lsum = 0, odd = 0, bad = 0;
 #pragma unroll
@@ -600,7 +643,8 @@ __global__ __launch_bounds__(256) void k_bucketize_cells(
         corrupt = 1;
         break;
       }
-      const int sv = stage16(lv, C.val + w.vbase + vpos, step_bytes);
+      const int sv = pre ? (int)((uintptr_t)(C.val + w.vbase) & 15)
+                         : stage16(lv, C.val + w.vbase + vpos, step_bytes);
       int off = sv + incl - lsum;
       int64_t t[K], v[K];
       int lt_seek = 0, lt_stop = 0;
@@ -634,7 +678,7 @@ __global__ __launch_bounds__(256) void k_bucketize_cells(
         stop_i = hi;
         break;
       }
-      // LDS reuse by the next step: every lane is done reading
+      // LDS reuse by the next step / row: every lane is done reading
       wave_lds_fence();
     }
     if (generic || corrupt) break;
@@ -644,6 +688,9 @@ __global__ __launch_bounds__(256) void k_bucketize_cells(
       break;
     }
   }
+  // no LDS-DMA may still be landing when the wave (and its block's LDS)
+  // goes away
+  wait_vmcnt(0);
   if (generic || corrupt) {
     // a mixed column is parsed by the generic decode, which also judges
     // whether it is corrupt
