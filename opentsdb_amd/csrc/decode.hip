@@ -525,6 +525,8 @@ __global__ __launch_bounds__(256) void k_bucketize_cells(
       SM.keep[s] = keep;
       SM.lo[s] = 0;
       SM.hi[s] = 0;
+      SM.kf[s] = 0;
+      SM.kl[s] = -1;
       SM.of_has[s] = of_has;
       SM.of_ts[s] = of_ts;
       SM.of_val[s] = of_val;

@@ -629,6 +629,8 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     W.SM.hi = cv.take<int64_t>(S);
     W.SM.of_ts = cv.take<int64_t>(S);
     W.SM.of_val = cv.take<double>(S);
+    W.SM.kf = cv.take<int32_t>(S);
+    W.SM.kl = cv.take<int32_t>(S);
     W.SM.keep = cv.take<uint8_t>(S);
     W.SM.of_has = cv.take<uint8_t>(S);
     W.R.val = cv.take<double>((size_t)S * NB);
@@ -846,7 +848,12 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     });
     if (!ok) return fail(OTSDB_E_UNSUPPORTED, "downsampler %d", spec->ds_agg_id);
   }
-  if (S > 0 && NB > 0) {
+  // constant interpolation, NONE fill, no rate, sentinel rows: k_group
+  // derives each contribution itself and k_transform is not needed
+  const bool direct = P.sentinel && !P.rate && !P.fill && !P.run_all &&
+                      (P.interp == 1 || P.interp == 2 || P.interp == 3) &&
+                      !is_selection(spec->agg_id);
+  if (S > 0 && NB > 0 && !direct) {
     StageTimer tm(c, 1);
     // rate rows of up to 2,048 buckets stay in registers between the two
     // RateSpan passes (one row read, one write)
@@ -917,7 +924,13 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     } else {
       ok = with_monoid(spec->agg_id, [&](auto tag) {
         using M = decltype(tag);
-        if (T.T > 0)
+        if (T.T > 0 && direct)
+          hipLaunchKernelGGL(k_group_direct<M>, dim3(blocks_for(T.T * NB, 256)),
+                             dim3(256), 0, st, P, NB, T.T, T.tg, T.tm0, T.tm1,
+                             T.single, d_members, W.SM, W.R, W.partial,
+                             W.tile_emit, W.out_val, W.out_emit, c->d_err,
+                             mode);
+        else if (T.T > 0)
           hipLaunchKernelGGL(k_group<M>, dim3(blocks_for(T.T * NB, 256)),
                              dim3(256), 0, st, NB, T.T, T.tg, T.tm0, T.tm1,
                              T.single, d_members, W.R, W.partial, W.tile_emit,

@@ -94,6 +94,8 @@ struct BatchDev {
 struct SeriesMeta {
   int64_t* lo;
   int64_t* hi;
+  int32_t* kf;  // bucket of the first / last point in [lo, hi) (kf > kl:
+  int32_t* kl;  // none) — the span sentinel rows are written over
   uint8_t* keep;
   uint8_t* of_has;
   int64_t* of_ts;

@@ -82,12 +82,15 @@ DEV int64_t wave_incl_max(int64_t x) {
 // interpolate up to end_time, AggregationIterator.java:760-775).
 // One thread per series.
 // ------------------------------------------------------------------------
-DEV void k_prep_store(SeriesMeta SM, int64_t s, bool keep, int64_t lo,
-                      int64_t hi, uint8_t of_has, int64_t of_ts,
-                      double of_val) {
+DEV void k_prep_store(const Params& P, const BatchDev& B, SeriesMeta SM,
+                      int64_t s, bool keep, int64_t lo, int64_t hi,
+                      uint8_t of_has, int64_t of_ts, double of_val) {
   SM.keep[s] = keep;
   SM.lo[s] = lo;
   SM.hi[s] = hi;
+  const bool any = keep && lo < hi;
+  SM.kf[s] = any ? (int32_t)bucket_of(P, B.ts[lo]) : 0;
+  SM.kl[s] = any ? (int32_t)bucket_of(P, B.ts[hi - 1]) : -1;
   SM.of_has[s] = of_has;
   SM.of_ts[s] = of_ts;
   SM.of_val[s] = of_val;
@@ -115,7 +118,7 @@ __global__ void k_prep(Params P, BatchDev B, SeriesMeta SM, int* err_word) {
         const int64_t k = cal_bucket(P, t);
         if (k < P.cal_lo || k + 1 >= P.cal_n) {
           atomicOr(err_word, ERR_CAL_RANGE);
-          k_prep_store(SM, s, keep, lo, hi, 0, 0, 0.0);
+          k_prep_store(P, B, SM, s, keep, lo, hi, 0, 0, 0.0);
           return;
         }
         of_ts = P.cal[k];
@@ -132,7 +135,7 @@ __global__ void k_prep(Params P, BatchDev B, SeriesMeta SM, int* err_word) {
       of_has = 1;
     }
   }
-  k_prep_store(SM, s, keep, lo, hi, of_has, of_ts, of_val);
+  k_prep_store(P, B, SM, s, keep, lo, hi, of_has, of_ts, of_val);
 }
 
 // ------------------------------------------------------------------------
@@ -853,11 +856,7 @@ __global__ __launch_bounds__(256) void k_transform(Params P, BatchDev B,
   const bool fill = P.fill != 0 && !P.run_all;
   // sentinel rows: buckets [kf, kl] (first / last point's bucket) hold a
   // value or kAbsentBits, the others are absent
-  int64_t kf = 0, kl = -1;
-  if (sent && SM.lo[s] < SM.hi[s]) {
-    kf = bucket_of(P, B.ts[SM.lo[s]]);
-    kl = bucket_of(P, B.ts[SM.hi[s] - 1]);
-  }
+  const int64_t kf = sent ? SM.kf[s] : 0, kl = sent ? SM.kl[s] : -1;
   auto real_at = [&](int64_t b, double v) {
     return sent ? (b >= kf && b <= kl && __double_as_longlong(v) != kAbsentBits)
                 : rows[b] == ST_REAL;
@@ -1180,6 +1179,78 @@ __global__ __launch_bounds__(256) void k_group(
       st.push(R.val[off]);
       emit |= sv == ST_REAL;
     }
+  }
+  if (tile_single[t] && !always_partial) {
+    const int64_t o = tile_g[t] * nb + b;
+    double r = 0.0;
+    if (emit) {
+      int e = 0;
+      r = st.finish(&e);
+      if (is_inf(r)) e |= ERR_INFINITY;
+      if (e) atomicOr(err_word, e);
+    }
+    out_val[o] = r;
+    out_emit[o] = (uint8_t)emit;
+  } else {
+    partial[t * nb + b] = st.pack();
+    tile_emit[t * nb + b] = (uint8_t)emit;
+  }
+}
+
+// k_group over sentinel rows without k_transform, for queries whose
+// interpolation is a constant (ZIM -> 0, MAX / MIN -> +-Double.MAX_VALUE,
+// AggregationIterator.java:782-789), NONE fill and no rate: what the
+// transform would derive per (series, bucket) is local — a real point iff
+// the bucket lies in the series' [kf, kl] and does not hold the absent
+// sentinel; otherwise the constant iff it lies strictly inside (kf, kl) or
+// past kl with a point past the window; else nothing.  Saves the row sweep
+// and the state bytes.
+template <class M>
+__global__ __launch_bounds__(256) void k_group_direct(
+    Params P, int64_t nb, int64_t n_tiles, const int64_t* __restrict__ tile_g,
+    const int64_t* __restrict__ tile_m0, const int64_t* __restrict__ tile_m1,
+    const uint8_t* __restrict__ tile_single, const int64_t* __restrict__ members,
+    SeriesMeta SM, Rows R, Packed* __restrict__ partial,
+    uint8_t* __restrict__ tile_emit, double* __restrict__ out_val,
+    uint8_t* __restrict__ out_emit, int* err_word, int always_partial) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t t = idx / nb;
+  if (t >= n_tiles) return;
+  const int64_t b = idx - t * nb;
+  const int64_t m0 = tile_m0[t], m1 = tile_m1[t];
+  const double cst = P.interp == 1 ? 0.0 : (P.interp == 2 ? kDoubleMax : -kDoubleMax);
+  M st = M::init();
+  int emit = 0;
+  auto one = [&](int64_t sidx, double v, int32_t kf, int32_t kl, uint8_t of) {
+    const bool in = b >= kf && b <= kl;
+    if (in && __double_as_longlong(v) != kAbsentBits) {
+      st.push(v);
+      emit = 1;
+    } else if ((b > kf && b < kl) || (of && kf <= kl && b > kl)) {
+      st.push(cst);
+    }
+  };
+  int64_t m = m0;
+  for (; m + 4 <= m1; m += 4) {
+    int64_t sx[4];
+    double v[4];
+    int32_t kf[4], kl[4];
+    uint8_t of[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) sx[u] = members[m + u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      kf[u] = SM.kf[sx[u]];
+      kl[u] = SM.kl[sx[u]];
+      of[u] = SM.of_has[sx[u]];
+      v[u] = R.val[sx[u] * nb + b];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) one(sx[u], v[u], kf[u], kl[u], of[u]);
+  }
+  for (; m < m1; ++m) {
+    const int64_t sx = members[m];
+    one(sx, R.val[sx * nb + b], SM.kf[sx], SM.kl[sx], SM.of_has[sx]);
   }
   if (tile_single[t] && !always_partial) {
     const int64_t o = tile_g[t] * nb + b;
