@@ -494,6 +494,72 @@ DEV uint64_t lds_be(const uint8_t* lds, int o, int vl) {
   return __builtin_bswap64(w) >> (64 - 8 * vl);
 }
 
+// Big-endian fields of W bytes each, N consecutive ones from LDS byte o on
+// (o any byte offset; the lane's N*W bytes are read as whole dwords and the
+// fields cut out with byte-align funnels)
+template <int W, int N>
+DEV void lds_be_run(const uint8_t* lds, int o, uint32_t* out) {
+  constexpr int ND = (W * N + 3) / 4 + 1;
+  const int a = o & ~3, sh = o & 3;
+  uint32_t d[ND + 1];
+#pragma unroll
+  for (int i = 0; i < ND; ++i)
+    d[i] = *reinterpret_cast<const uint32_t*>(lds + a + 4 * i);
+  d[ND] = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const int b = W * j;  // compile-time byte offset of field j
+    // bytes sh + b .. : dword (b >> 2) + carry, shift ((b & 3) + sh) & 3
+    const int r = (b & 3) + sh;
+    const int i0 = b >> 2;
+    const uint32_t lo = r >= 4 ? d[i0 + 1] : d[i0];
+    const uint32_t hi = r >= 4 ? d[i0 + 2] : d[i0 + 1];
+    const uint32_t x = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(r & 3));
+    out[j] = W == 2 ? (((x & 0xFF) << 8) | ((x >> 8) & 0xFF))
+                    : __builtin_bswap32(x);
+  }
+}
+
+// N consecutive values of VL bytes (one length and type for all of them,
+// fl: floating point) from LDS byte o on -> the folded double's bits
+// (RowSeq extractIntegerValue / extractFloatingPointValue, toDouble)
+template <int VL, int N, int FL>
+DEV void lds_values(const uint8_t* lds, int o, int64_t* v) {
+  constexpr int ND = (VL * N + 3) / 4 + 1;
+  const int a = o & ~3;
+  const uint32_t sh = (uint32_t)(o & 3);
+  uint32_t d[ND + 1];
+#pragma unroll
+  for (int i = 0; i < ND; ++i)
+    d[i] = *reinterpret_cast<const uint32_t*>(lds + a + 4 * i);
+  d[ND] = 0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    if (VL == 8) {
+      const uint32_t lo = __builtin_amdgcn_alignbyte(d[2 * j + 1], d[2 * j], sh);
+      const uint32_t hi = __builtin_amdgcn_alignbyte(d[2 * j + 2], d[2 * j + 1], sh);
+      const int64_t x = (int64_t)(((uint64_t)__builtin_bswap32(lo) << 32) |
+                                  __builtin_bswap32(hi));
+      v[j] = FL ? x : __double_as_longlong((double)x);
+    } else if (VL == 4) {
+      const uint32_t x = __builtin_bswap32(
+          __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh));
+      v[j] = __double_as_longlong(FL ? (double)__uint_as_float(x)
+                                     : (double)(int32_t)x);
+    } else {
+      const int b = VL * j;
+      const int r = (b & 3) + (int)sh;
+      const int i0 = b >> 2;
+      const uint32_t lo = r >= 4 ? d[i0 + 1] : d[i0];
+      const uint32_t hi = r >= 4 ? d[i0 + 2] : d[i0 + 1];
+      const uint32_t x = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(r & 3));
+      const int32_t iv = VL == 2 ? (int32_t)(int16_t)(((x & 0xFF) << 8) | ((x >> 8) & 0xFF))
+                                 : (int32_t)(int8_t)(x & 0xFF);
+      v[j] = __double_as_longlong((double)iv);
+    }
+  }
+}
+
 __global__ void k_series_rows(int64_t R, int64_t S,
                               const int64_t* __restrict__ row_series,
                               int64_t* __restrict__ series_row) {
@@ -581,10 +647,42 @@ __global__ __launch_bounds__(256) void k_bucketize_cells(
             (void*)&lv_all[wv][buf][16 * c0], 16, 0, 0);
     return k;
   };
+  // Row metadata (column offsets, base time, qualifier width) for 64 rows at
+  // a time, one row per lane: one parallel load round trip per 64 rows
+  // instead of two dependent ones (offsets, then the first qualifier byte)
+  // in front of every row's prefetch.
+  int64_t mb = INT64_MIN, m_qo = 0, m_vo = 0, m_bms = 0, m_ql = 0, m_vl = 0;
+  int m_q0 = 0;
+  auto row_at = [&](int64_t rr) -> CellRow {
+    if (rr < mb || rr >= mb + 64) {  // wave-uniform
+      mb = rr;
+      const int64_t x = rr + lane;
+      if (x < r1) {
+        m_qo = C.qual_off[x];
+        m_ql = C.qual_off[x + 1] - m_qo;
+        m_vo = C.val_off[x];
+        m_vl = C.val_off[x + 1] - m_vo;
+        m_bms = C.row_base_s[x] * 1000;
+        m_q0 = m_ql > 0 ? C.qual[m_qo] : 0;
+      }
+    }
+    const int j = (int)(rr - mb);
+    CellRow w;
+    const int64_t qo = readlane_l(m_qo, j), qlen = readlane_l(m_ql, j);
+    w.q = C.qual + qo;
+    w.vbase = readlane_l(m_vo, j);
+    w.vlen = readlane_l(m_vl, j);
+    w.base_ms = readlane_l(m_bms, j);
+    const int q0 = __builtin_amdgcn_readlane(m_q0, j);
+    w.qw = (qlen > 0 && (q0 & 0xF0) == 0xF0) ? 4 : 2;
+    w.n = qlen / w.qw;
+    w.ok = qlen > 0 && qlen % w.qw == 0 && !((uintptr_t)w.q & 1);
+    return w;
+  };
   int64_t r = r0;
-  while (r < r1 && cell_row(C, r).base_ms + 3600000 <= P.seek_ts) ++r;
+  while (r < r1 && row_at(r).base_ms + 3600000 <= P.seek_ts) ++r;
   int buf = 0;
-  CellRow wn = r < r1 ? cell_row(C, r) : CellRow{};
+  CellRow wn = r < r1 ? row_at(r) : CellRow{};
   if (r < r1 && fits(wn)) prefetch(wn, 0);
   for (; r < r1 && stop_r < 0; ++r, buf ^= 1) {
     const CellRow w = wn;
@@ -595,7 +693,7 @@ __global__ __launch_bounds__(256) void k_bucketize_cells(
     const bool pre = fits(w);  // this row already sits in buffer buf
     int n_next = 0;
     if (r + 1 < r1) {
-      wn = cell_row(C, r + 1);
+      wn = row_at(r + 1);
       if (fits(wn)) n_next = prefetch(wn, buf ^ 1);
     }
     uint8_t* lq = lq_all[wv][buf];
@@ -611,65 +709,115 @@ __global__ __launch_bounds__(256) void k_bucketize_cells(
       const int sq = pre ? (int)((uintptr_t)w.q & 15)
                          : stage16(lq, w.q + w.qw * st0, (int64_t)w.qw * n_st);
       uint32_t qv[K];
-      int vl[K], lsum = 0, odd = 0, bad = 0;
+      if (w.qw == 2) lds_be_run<2, K>(lq, sq + 2 * K * lane, qv);
+      else lds_be_run<4, K>(lq, sq + 4 * K * lane, qv);
+      // one flags nibble for every point of the step (what compaction of
+      // one series' same-typed values writes) -> value length and type are
+      // wave-uniform: no length scan, no per-point type dispatch
+      const uint32_t f0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(qv[0] & 0xF));
+      int vl[K], lsum = 0, odd = 0, bad = 0, mixed = 0;
 #pragma unroll
       for (int j = 0; j < K; ++j) {
         const int i = K * lane + j;
-        qv[j] = 0;
         vl[j] = 0;
         if (i < n_st) {
-          const uint16_t* h =
-              reinterpret_cast<const uint16_t*>(lq + sq + w.qw * i);
-          const uint32_t a = __builtin_bswap16(h[0]);
-          qv[j] = w.qw == 2 ? a : (a << 16) | __builtin_bswap16(h[1]);
           const int mk = ((qv[j] >> (w.qw == 2 ? 8 : 24)) & 0xF0) == 0xF0;
           odd |= (w.qw == 4) != (mk != 0);
+          mixed |= (qv[j] & 0xF) != f0;
           vl[j] = (int)(qv[j] & 0x7) + 1;
-          if (qv[j] & 0x8) bad |= !(vl[j] == 4 || vl[j] == 8);
-          else bad |= !(vl[j] == 1 || vl[j] == 2 || vl[j] == 4 || vl[j] == 8);
           lsum += vl[j];
         }
       }
       generic |= __ballot(odd) != 0;
-      corrupt |= __ballot(bad) != 0;
-      if (generic || corrupt) break;
-      // value offsets: exclusive wave scan of the lanes' byte counts
-      int incl = lsum;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(incl, d);
-        if (lane >= d) incl += y;
-      }
-      const int step_bytes = __shfl(incl, 63);
-      if (vpos + step_bytes > w.vlen) {
-        corrupt = 1;
-        break;
-      }
-      const int sv = pre ? (int)((uintptr_t)(C.val + w.vbase) & 15)
-                         : stage16(lv, C.val + w.vbase + vpos, step_bytes);
-      int off = sv + incl - lsum;
+      if (generic) break;
+      const bool uni = __ballot(mixed) == 0;
       int64_t t[K], v[K];
-      int lt_seek = 0, lt_stop = 0;
+      int step_bytes, sv;
+      if (uni) {
+        const int vlu = (int)(f0 & 0x7) + 1, flu = (f0 & 0x8) != 0;
+        corrupt |= flu ? !(vlu == 4 || vlu == 8)
+                       : !(vlu == 1 || vlu == 2 || vlu == 4 || vlu == 8);
+        step_bytes = vlu * n_st;
+        if (corrupt || vpos + step_bytes > w.vlen) {
+          corrupt = 1;
+          break;
+        }
+        sv = pre ? (int)((uintptr_t)(C.val + w.vbase) & 15)
+                 : stage16(lv, C.val + w.vbase + vpos, step_bytes);
+        const int o = sv + vlu * K * lane;
+        switch (vlu + 16 * flu) {
+          case 8 + 16: lds_values<8, K, 1>(lv, o, v); break;
+          case 4 + 16: lds_values<4, K, 1>(lv, o, v); break;
+          case 8: lds_values<8, K, 0>(lv, o, v); break;
+          case 4: lds_values<4, K, 0>(lv, o, v); break;
+          case 2: lds_values<2, K, 0>(lv, o, v); break;
+          default: lds_values<1, K, 0>(lv, o, v); break;
+        }
+      } else {
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const int i = K * lane + j;
-        if (i < n_st) {
-          t[j] = qual_ts(w.base_ms, w.qw, qv[j]);
+        for (int j = 0; j < K; ++j) {
+          if (K * lane + j < n_st) {
+            if (qv[j] & 0x8) bad |= !(vl[j] == 4 || vl[j] == 8);
+            else bad |= !(vl[j] == 1 || vl[j] == 2 || vl[j] == 4 || vl[j] == 8);
+          }
+        }
+        corrupt |= __ballot(bad) != 0;
+        if (corrupt) break;
+        // value offsets: exclusive wave scan of the lanes' byte counts
+        int incl = lsum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const int y = __shfl_up(incl, d);
+          if (lane >= d) incl += y;
+        }
+        step_bytes = __shfl(incl, 63);
+        if (vpos + step_bytes > w.vlen) {
+          corrupt = 1;
+          break;
+        }
+        sv = pre ? (int)((uintptr_t)(C.val + w.vbase) & 15)
+                 : stage16(lv, C.val + w.vbase + vpos, step_bytes);
+        int off = sv + incl - lsum;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
           v[j] = dbits_of(lds_be(lv, off, vl[j]), vl[j], (qv[j] & 0x8) != 0);
           off += vl[j];
-          lt_seek += t[j] < P.seek_ts;
-          lt_stop += t[j] < P.stop_ts;
-        } else {
-          t[j] = 0;
-          v[j] = 0;
+        }
+      }
+      // the step's points are [lo, hi) in row indices (timestamps increase):
+      // counted against the seek / stop bounds unless the whole row lies
+      // inside them (offsets < 2^22 ms)
+      const bool inside =
+          w.base_ms >= P.seek_ts && w.base_ms + (1 << 22) <= P.stop_ts;
+      // (points past n_st keep whatever the LDS held: reduce_step only
+      // reads the step's [lo, hi))
+      int lt_seek = 0, lt_stop = 0;
+      if (w.qw == 2) {
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          t[j] = w.base_ms + (int64_t)(((qv[j] & 0xFFFFu) >> 4) * 1000u);
+      } else {
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+          t[j] = w.base_ms + (int64_t)((qv[j] & 0x0FFFFFC0u) >> 6);
+      }
+      if (!inside) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const bool in = K * lane + j < n_st;
+          lt_seek += in && t[j] < P.seek_ts;
+          lt_stop += in && t[j] < P.stop_ts;
         }
       }
       vpos += step_bytes;
-      // valid points of the step are [lo, hi) in row indices (ts increase)
-      int sum_seek = lt_seek, sum_stop = lt_stop;
-      for (int d = 32; d >= 1; d >>= 1) {
-        sum_seek += __shfl_xor(sum_seek, d);
-        sum_stop += __shfl_xor(sum_stop, d);
+      int sum_seek = 0, sum_stop = n_st;
+      if (!inside) {
+        sum_seek = lt_seek;
+        sum_stop = lt_stop;
+        for (int d = 32; d >= 1; d >>= 1) {
+          sum_seek += __shfl_xor(sum_seek, d);
+          sum_stop += __shfl_xor(sum_stop, d);
+        }
       }
       const int64_t lo = st0 + sum_seek, hi = st0 + sum_stop;
       if (hi > lo)

@@ -677,7 +677,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     ok = with_monoid(spec->ds_agg_id, [&](auto tag) {
       using M = decltype(tag);
       StageTimer tm(c, 0);
-      hipLaunchKernelGGL((k_bucketize_cells<M, 8>), dim3(blocks_for(S, 4)),
+      hipLaunchKernelGGL((k_bucketize_cells<M, 6>), dim3(blocks_for(S, 4)),
                          dim3(256), 0, st, P, *cells, series_row, S, W.SM, W.R,
                          c->d_err);
     });

@@ -363,18 +363,32 @@ DEV bool fold_fast(const Params& P, const BatchDev& B, int sf, int64_t i0,
       (k1 == k0 + 2) ? P.gbase + (int64_t)(k0 + 1) * P.interval : b_tail;
   M h = M::init(), m = M::init(), c = M::init();
   bool any_mid = false;
+  if (__ballot(k1 == k0 + 2) == 0) {
+    // no lane of the wave spans three buckets (buckets of more than K
+    // points): two runs, head and tail
 #pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const double x =
-        FLOATONLY ? bits_to_double(v[j]) : point_value(B, i0 + j, v[j], sf);
-    const bool vj = j < nv;
-    const bool inh = vj && t[j] < b_mid;
-    const bool inc = vj && t[j] >= b_tail;
-    const bool inm = vj && !inh && !inc;
-    h.push_if(inh, x);
-    m.push_if(inm, x);
-    c.push_if(inc, x);
-    any_mid |= inm;
+    for (int j = 0; j < K; ++j) {
+      const double x =
+          FLOATONLY ? bits_to_double(v[j]) : point_value(B, i0 + j, v[j], sf);
+      const bool vj = j < nv;
+      const bool inh = vj && t[j] < b_tail;
+      h.push_if(inh, x);
+      c.push_if(vj && !inh, x);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const double x =
+          FLOATONLY ? bits_to_double(v[j]) : point_value(B, i0 + j, v[j], sf);
+      const bool vj = j < nv;
+      const bool inh = vj && t[j] < b_mid;
+      const bool inc = vj && t[j] >= b_tail;
+      const bool inm = vj && !inh && !inc;
+      h.push_if(inh, x);
+      m.push_if(inm, x);
+      c.push_if(inc, x);
+      any_mid |= inm;
+    }
   }
   head_key = k0;
   cur_key = k1;

@@ -218,22 +218,29 @@ def encode_cells_device(engine, db):
     return DeviceCells(t, S)
 
 
-def decode_cells_device(engine, cells, capacity=None):
-    """otsdb_decode_cells_device -> (offsets, ts, val, is_float) tensors."""
+def decode_cells_device(engine, cells, capacity=None, out=None):
+    """otsdb_decode_cells_device -> (offsets, ts, val, is_float) tensors.
+    out: preallocated (offsets, ts, val, is_float) to decode into (the
+    bench times the decode without the allocation)."""
     import ctypes as C
     import torch
     dev = cells.t["qual"].device
     S = cells.n_series
-    offsets = torch.zeros(S + 1, dtype=torch.int64, device=dev)
     c = cells.as_abi()
+    if out is not None:
+        offsets, ts, val, isf = out
+        capacity = int(ts.numel())
+    else:
+        offsets = torch.zeros(S + 1, dtype=torch.int64, device=dev)
     if capacity is None:
         engine._check(engine.lib.otsdb_decode_cells_device(
             engine.ctx, C.byref(c), S, offsets.data_ptr(), None, None, None,
             0, None))
         capacity = int(offsets[-1].item())
-    ts = torch.empty(max(capacity, 2), dtype=torch.int64, device=dev)
-    val = torch.empty_like(ts)
-    isf = torch.empty(max(capacity, 2), dtype=torch.uint8, device=dev)
+    if out is None:
+        ts = torch.empty(max(capacity, 2), dtype=torch.int64, device=dev)
+        val = torch.empty_like(ts)
+        isf = torch.empty(max(capacity, 2), dtype=torch.uint8, device=dev)
     engine._check(engine.lib.otsdb_decode_cells_device(
         engine.ctx, C.byref(c), S, offsets.data_ptr(), ts.data_ptr(),
         val.data_ptr(), isf.data_ptr(), capacity, None))

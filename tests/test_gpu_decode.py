@@ -243,3 +243,77 @@ def test_fused_cells_corrupt_column(engine):
     res = DeviceResult(torch, db.n_groups, 4096, "cuda")
     with pytest.raises(core.IllegalDataException):
         workload.run_cells_device(engine, spec, cd, db, res)
+
+
+# (name, value kind, int range or None, float4 fraction, ms fraction): cell
+# layouts the device encoder does not write — 4-byte floats, 1/2/4/8-byte
+# longs of one width per column (the fused kernel's wave-uniform decode),
+# mixed widths (its per-point decode), 4-byte ms qualifiers
+HOST_FORMATS = [("f8", "float", None, 0.0, 0.0), ("f4", "float", None, 1.0, 0.0),
+                ("f4f8", "float", None, 0.5, 0.0), ("i1", "int", (-120, 120), 0, 0),
+                ("i2", "int", (-30000, 30000), 0, 0),
+                ("i4", "int", (1 << 20, 1 << 30), 0, 0),
+                ("i8", "int", (1 << 40, 1 << 50), 0, 0),
+                ("imix", "int", (-(1 << 40), 1 << 40), 0, 0),
+                ("f8ms", "float", None, 0.0, 1.0), ("i2ms", "int", (300, 30000), 0, 1.0)]
+
+
+@pytest.mark.parametrize("name,kind,rng_i,f4,ms", HOST_FORMATS,
+                         ids=[f[0] for f in HOST_FORMATS])
+@pytest.mark.parametrize("agg,ds", [("sum", "1m-avg"), ("max", "5m-max")])
+def test_fused_cells_host_formats(engine, name, kind, rng_i, f4, ms, agg, ds):
+    """The fused cells query over host-encoded columns of every value width
+    and qualifier width against the oracle run on the points RowSeq
+    decodes from the same columns."""
+    import torch
+    from opentsdb_amd import workload
+    from opentsdb_amd.batch import HostBatch
+    from opentsdb_amd.engine import DeviceResult
+    from tests.test_gpu_parity import compare
+    rng = np.random.default_rng(11)
+    b = datasets.random_batch(17, n_series=24, n_groups=3, value_kind=kind,
+                              cadence_ms=7000 if ms else 10000)
+    if ms:
+        b.ts = b.ts + rng.integers(0, 999, len(b.ts))
+        for s in range(b.n_series):
+            a, z = b.offsets[s], b.offsets[s + 1]
+            b.ts[a:z] = np.sort(b.ts[a:z])
+    else:
+        b.ts = b.ts - b.ts % 1000
+    if rng_i is not None:
+        b.val = rng.integers(rng_i[0], rng_i[1], len(b.ts)).astype(np.int64)
+        b.is_float = np.zeros(len(b.ts), np.uint8)
+    else:
+        b.is_float = np.ones(len(b.ts), np.uint8)
+    enc = cells.encode_batch(b, rng, f4, ms)
+    # the reference points: RowSeq.Iterator over every row
+    ts, bits, isint = [], [], []
+    for s in range(b.n_series):
+        for r in np.nonzero(enc["row_series"] == s)[0]:
+            q = enc["qual"][enc["qual_off"][r]:enc["qual_off"][r + 1]]
+            v = enc["val"][enc["val_off"][r]:enc["val_off"][r + 1]]
+            p = pyoracle.decode_row(q.tobytes(), v.tobytes(),
+                                    enc["row_base_s"][r])
+            ts.append(p["ts"])
+            bits.append(p["bits"])
+            isint.append(p["is_int"])
+    cat = lambda xs, dt: (np.concatenate(xs).astype(dt) if xs  # noqa
+                          else np.zeros(0, dt))
+    rts, rbits = cat(ts, np.int64), cat(bits, np.int64)
+    risf = (cat(isint, np.uint8) == 0).astype(np.uint8)
+    assert len(rts) == len(b.ts)
+    hb = HostBatch(b.offsets, rts, rbits, risf, None, b.group_offsets,
+                   b.group_members)
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda()
+         for k, v in enc.items()}
+    dc = workload.DeviceCells(d, b.n_series)
+    db = _device_batch(hb, kind)
+    t0, t1 = datasets.T0 + 600000, datasets.T0 + 3 * 3600000
+    spec = core.make_spec(t0, t1, core.Aggregators.get(agg),
+                          core.DownsamplingSpecification(ds), t0, t1)
+    ref = pyoracle.group_by(spec, hb)
+    res = DeviceResult(torch, db.n_groups, 4 * len(hb.ts) + 64, "cuda")
+    workload.run_cells_device(engine, spec, dc, db, res)
+    got = _result_points(res, db.n_groups)
+    compare(got, ref, agg == "max", scale=1e4,
+            where="fused-host/%s/%s/%s" % (name, agg, ds))
