@@ -140,6 +140,7 @@ struct Work {
   uint32_t* hist = nullptr;
   Packed* comb = nullptr;      // two-level combine: first-level slices
   uint8_t* comb_emit = nullptr;
+  uint8_t* redo = nullptr;     // fused-rate series handed back (Params.redo)
 };
 
 }  // namespace
@@ -633,6 +634,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     W.SM.kl = cv.take<int32_t>(S);
     W.SM.keep = cv.take<uint8_t>(S);
     W.SM.of_has = cv.take<uint8_t>(S);
+    W.redo = cv.take<uint8_t>(S);
     W.R.val = cv.take<double>((size_t)S * NB);
     W.R.state = cv.take<uint8_t>((size_t)S * NB);
     W.partial = cv.take<Packed>((size_t)T.T * NB);
@@ -670,6 +672,14 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
                bucketize_uses_ring(c->bucketize_k, spec->ds_agg_id);
   if (S > 0 && NB > 0 && !P.sentinel)
     HIP_TRY(hipMemsetAsync(W.R.state, 0, (size_t)S * NB, st));
+  // RateSpan inside k_bucketize (NONE fill; the FillingDownsampler's rate
+  // origin and fill points stay with k_transform)
+  static const bool rate_fuse_on = [] {
+    const char* e = getenv("OTSDB_RATE_FUSED");  // A/B knob
+    return !(e && e[0] == '0');
+  }();
+  const bool rate_fused = rate_fuse_on && P.sentinel && P.rate && !P.fill &&
+                          !P.run_all && c->bucketize_k == 0;
 
   bool ok = true;
   if (cells && S > 0 && NB > 0) {
@@ -842,8 +852,22 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
                              W.SM, W.R);
           break;
         default:  // production: LDS ring sink, sentinel rows, DPP scan
-          hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 256>), grid,
-                             blk, 0, st, P, B, W.SM, W.R);
+          if (rate_fused) {
+            // RateSpan fused into the ring flush (1,024-bucket ring: a step
+            // hands its series back only across a gap of ~1,000 buckets);
+            // then the plain kernel for the series handed back
+            Params PF = P;
+            PF.redo = W.redo;
+            hipLaunchKernelGGL(
+                (k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 1024, 512, 1>), grid, blk,
+                0, st, PF, B, W.SM, W.R);
+            PF.only_redo = 1;
+            hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 256>), grid,
+                               blk, 0, st, PF, B, W.SM, W.R);
+          } else {
+            hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 256>), grid,
+                               blk, 0, st, P, B, W.SM, W.R);
+          }
       }
     });
     if (!ok) return fail(OTSDB_E_UNSUPPORTED, "downsampler %d", spec->ds_agg_id);
@@ -865,7 +889,12 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       const char* e = getenv("OTSDB_TRANSFORM_REG_MAX");  // tuning knob
       return e ? (int64_t)atoll(e) : (int64_t)0;
     }();
-    if (!P.rate || NB > reg_max) L(k_transform<0>);
+    if (rate_fused) {  // only the series the fused kernel handed back
+      P.redo = W.redo;
+      P.only_redo = 1;
+      L(k_transform<0>);
+      P.only_redo = 0;
+    } else if (!P.rate || NB > reg_max) L(k_transform<0>);
     else if (NB <= 512) L(k_transform<8>);
     else if (NB <= 1024) L(k_transform<16>);
     else L(k_transform<32>);

@@ -75,6 +75,13 @@ struct Params {
   // the table starts before the grid's first bucket); null = fixed interval
   const int64_t* cal;
   int64_t cal_lo, cal_n;
+  // rate queries with the RateSpan pass fused into k_bucketize's ring
+  // flush: series the fused kernel hands back (a gap wider than its ring
+  // inside one step) get redo[s] = 1; the fallback kernels, launched with
+  // only_redo, skip every other series
+  uint8_t* redo;
+  int32_t only_redo;
+  int32_t _pad3;
 };
 
 // value bits of an absent bucket in sentinel rows: a signalling NaN, which

@@ -280,6 +280,18 @@ DEV void wait_vmcnt(int n) {
   }
 }
 
+DEV double readlane_d(double x, int l) {
+  const int64_t b = __builtin_bit_cast(int64_t, x);
+  const int32_t lo = __builtin_amdgcn_readlane((int32_t)(uint32_t)b, l);
+  const int32_t hi = __builtin_amdgcn_readlane((int32_t)(b >> 32), l);
+  return __builtin_bit_cast(double, (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+DEV int64_t readlane_l(int64_t b, int l) {
+  const int32_t lo = __builtin_amdgcn_readlane((int32_t)(uint32_t)b, l);
+  const int32_t hi = __builtin_amdgcn_readlane((int32_t)(b >> 32), l);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
 // Where closed buckets go.  Directly (one scattered 8-B value store and one
 // 1-B state store per closing lane), or through a per-wavefront LDS ring of
 // WIN bucket values that sink_flush drains in runs of 64 consecutive buckets,
@@ -310,9 +322,112 @@ struct RowSink {
 
 DEV double absent_value() { return __longlong_as_double(kAbsentBits); }
 
-// drains the ring's buckets [flushed, limit) (all final) to the row
-DEV void sink_flush(RowSink& S, int64_t& flushed, int64_t limit) {
+// RateSpan over a series' bucket points, carried across ring flushes
+// (k_transform's two passes, transform_rate, folded into the flush of each
+// run of 64 final buckets): the previous point of pass 1, the first kept
+// rate (the junk one), and the latest kept rate pass 2 holds.
+struct RateState {
+  int64_t carry_pts;   // last real bucket (pass 1's previous point)
+  double carry_pv;
+  int64_t r0_idx;      // first kept rate
+  double r0_val;
+  int64_t last_kept;
+  int64_t carry_k;     // latest kept rate
+  double carry_kv;
+  int kept_count;      // capped at 2
+  int bad;             // non-increasing timestamps (fallback reports it)
+};
+
+// One run of final buckets [f, min(f + 64, limit)) of the ring through
+// RateSpan (RateSpan.java:103-180) and the rate-mode contribution rule
+// (AggregationIterator.java:448-459, :744-753): each bucket gets its rate
+// (ST_REAL) or the latest kept rate at or before it (ST_INTERP), exactly as
+// transform_rate's passes; what depends on the whole series (buckets before
+// the first kept rate, after the last one, fewer than two rates) is fixed
+// by rate_finish.
+DEV void rate_flush(const Params& P, RowSink& S, RateState& R, int64_t f,
+                    int64_t limit) {
   const int lane = LANE;
+  const int64_t b = f + lane;
+  const bool inb = b < limit;
+  double v = 0.0;
+  if (inb) {
+    const int i = (int)(b & S.mask);
+    v = S.rv[i];
+    S.rv[i] = absent_value();
+  }
+  const bool p = inb && __double_as_longlong(v) != kAbsentBits;
+  const int64_t t = inb ? bucket_ts(P, b) : 0;
+  const uint64_t pm = __ballot(p);
+  const uint64_t below = pm & ((1ULL << lane) - 1);
+  const int pl = below ? 63 - __builtin_clzll(below) : -1;
+  const double vp = __shfl(v, pl >= 0 ? pl : 0);
+  const int64_t tprev = pl >= 0 ? bucket_ts(P, f + pl) : R.carry_pts;
+  const double vprev = pl >= 0 ? vp : R.carry_pv;
+  bool kept = false;
+  double rate = 0.0;
+  if (p) {
+    if (t <= tprev) R.bad = 1;
+    const double dt = (double)(t - tprev) / 1000.0;
+    double diff = v - vprev;
+    if (P.counter && diff < 0) {
+      if (!P.drop_resets) {
+        kept = true;
+        diff = (double)P.counter_max - vprev + v;
+        const double r = diff / dt;
+        rate = (P.reset_value > 0 && r > (double)P.reset_value) ? 0.0 : r;
+      }
+    } else {
+      kept = true;
+      rate = diff / dt;
+    }
+  }
+  const bool k = p && kept;
+  const uint64_t km = __ballot(k);
+  if (km) {
+    const int f0 = __builtin_ctzll(km);
+    const double rf = __shfl(rate, f0);
+    if (R.r0_idx < 0) {
+      R.r0_idx = f + f0;
+      R.r0_val = rf;
+    }
+    R.kept_count += __popcll(km);
+    if (R.kept_count > 2) R.kept_count = 2;
+    R.last_kept = f + 63 - __builtin_clzll(km);
+  }
+  if (pm) {
+    const int l = 63 - __builtin_clzll(pm);
+    R.carry_pts = bucket_ts(P, f + l);
+    R.carry_pv = readlane_d(v, l);
+  }
+  // pass 2: latest kept rate at or before each bucket
+  const double kv = k ? rate : 0.0;
+  const uint64_t upto = km & ((2ULL << lane) - 1);
+  const int il = upto ? 63 - __builtin_clzll(upto) : -1;
+  const double lv = __shfl(kv, il >= 0 ? il : 0);
+  const double held = il >= 0 ? lv : (R.carry_k >= 0 ? R.carry_kv : R.r0_val);
+  if (inb) {
+    const bool real = k && b != R.r0_idx;
+    S.rowv[b] = real ? kv : held;
+    S.rows[b] = real ? ST_REAL : ST_INTERP;
+  }
+  if (km) {
+    const int l = 63 - __builtin_clzll(km);
+    R.carry_k = f + l;
+    R.carry_kv = readlane_d(kv, l);
+  }
+}
+
+// drains the ring's buckets [flushed, limit) (all final) to the row
+template <int RATE = 0>
+DEV void sink_flush(RowSink& S, int64_t& flushed, int64_t limit,
+                    const Params* P = nullptr, RateState* R = nullptr) {
+  const int lane = LANE;
+  if (RATE) {
+    for (int64_t f = flushed; f < limit; f += 64) rate_flush(*P, S, *R, f, limit);
+    if (limit > flushed) flushed = limit;
+    return;
+  }
   for (int64_t f = flushed; f < limit; f += 64) {
     const int64_t b = f + lane;
     if (b < limit) {
@@ -461,18 +576,6 @@ DEV void seg_scan_dpp(int key, M& st) {
   seg_step_dpp<0x142, 0xA>(key, st);  // row_bcast:15 -> rows 1, 3
   seg_step_dpp<0x143, 0xC>(key, st);  // row_bcast:31 -> rows 2, 3
 }
-DEV double readlane_d(double x, int l) {
-  const int64_t b = __builtin_bit_cast(int64_t, x);
-  const int32_t lo = __builtin_amdgcn_readlane((int32_t)(uint32_t)b, l);
-  const int32_t hi = __builtin_amdgcn_readlane((int32_t)(b >> 32), l);
-  return __builtin_bit_cast(double, (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
-}
-DEV int64_t readlane_l(int64_t b, int l) {
-  const int32_t lo = __builtin_amdgcn_readlane((int32_t)(uint32_t)b, l);
-  const int32_t hi = __builtin_amdgcn_readlane((int32_t)(b >> 32), l);
-  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-
 // One step of the bucket reduction over the K consecutive points t[], v[]
 // of every lane (points i0 .. i0+K-1 of the series, step base `base`):
 // lane-local fold, the previous step's open bucket, the segmented wave scan
@@ -593,11 +696,13 @@ DEV int64_t step_last_key(const Params& P, const BatchDev& B, int64_t base,
   return bucket_of(P, B.ts[e]);
 }
 
-template <int WIN, int K>
-DEV void ring_before(const Params& P, const BatchDev& B, RowSink& S,
+// returns true (RATE: nothing written) when the step spans more buckets
+// than the ring holds
+template <int WIN, int K, int RATE = 0>
+DEV bool ring_before(const Params& P, const BatchDev& B, RowSink& S,
                      int64_t& flushed, int64_t lo, int64_t hi, int64_t base,
-                     const int64_t* t, int carry_key) {
-  if (WIN == 0) return;
+                     const int64_t* t, int carry_key, RateState* R = nullptr) {
+  if (WIN == 0) return false;
   constexpr int64_t pts = 64 * K;
   // last key of the step: from lane 63's last point when the step is full
   // (already in registers; a scalar reload would wait on HBM every step)
@@ -609,8 +714,9 @@ DEV void ring_before(const Params& P, const BatchDev& B, RowSink& S,
     const int64_t k_open = (carry_key >= 0 && carry_key < P.nb)
                                ? carry_key
                                : bucket_of(P, B.ts[base > lo ? base : lo]);
-    sink_flush(S, flushed, k_open);
+    sink_flush<RATE>(S, flushed, k_open, &P, R);
     if (k_hi >= flushed + WIN) {
+      if (RATE) return true;
       // a gap of more than WIN buckets inside this step: mark the span
       // absent, then let the step store straight to HBM behind it
       const int lane = LANE;
@@ -620,12 +726,13 @@ DEV void ring_before(const Params& P, const BatchDev& B, RowSink& S,
       S.direct = 1;
     }
   }
+  return false;
 }
 
-template <int WIN, int FL>
+template <int WIN, int FL, int RATE = 0>
 DEV void ring_after(const Params& P, const BatchDev& B, RowSink& S,
                     int64_t& flushed, int64_t hi, int64_t base, int64_t pts,
-                    int carry_key) {
+                    int carry_key, RateState* R = nullptr) {
   if (WIN == 0) return;
   // buckets below the open one (or the whole step, past the end) are final
   const int64_t limit = (carry_key >= 0 && carry_key < P.nb)
@@ -637,29 +744,75 @@ DEV void ring_after(const Params& P, const BatchDev& B, RowSink& S,
     return;
   }
   const int64_t full = flushed + ((limit - flushed) / FL) * FL;
-  if (full > flushed) sink_flush(S, flushed, full);
+  if (full > flushed) sink_flush<RATE>(S, flushed, full, &P, R);
 }
 
+// The rate row's buckets that depend on the whole series (transform_rate
+// pass 2): fewer than two rates (or none kept) -> absent everywhere; before
+// the first kept rate -> the junk rate, held; past the last kept rate ->
+// absent, or the latest rate held toward a point past the window
+// (AggregationIterator.java:448-459, :744-753).  kl: the last flushed bucket.
+DEV void rate_finish(const Params& P, const SeriesMeta& SM, int64_t s,
+                     RowSink& S, const RateState& R, int64_t kl) {
+  const int lane = LANE;
+  const int64_t nb = P.nb;
+  bool of_kept = false;
+  if (SM.of_has[s]) {
+    const double diff = SM.of_val[s] - R.carry_pv;
+    of_kept = !(P.counter && diff < 0 && P.drop_resets);
+  }
+  const int total = R.kept_count + (of_kept ? 1 : 0);
+  if (total < 2) {
+    for (int64_t b = lane; b < nb; b += 64) S.rows[b] = ST_ABSENT;
+    return;
+  }
+  for (int64_t b = lane; b < R.r0_idx; b += 64) {
+    S.rowv[b] = R.r0_val;
+    S.rows[b] = ST_INTERP;
+  }
+  if (!of_kept) {
+    for (int64_t b = R.last_kept + 1 + lane; b < nb; b += 64)
+      S.rows[b] = ST_ABSENT;
+  } else {
+    for (int64_t b = kl + 1 + lane; b < nb; b += 64) {
+      S.rowv[b] = R.carry_kv;
+      S.rows[b] = ST_INTERP;
+    }
+  }
+}
+
+// RATE: RateSpan fused into the ring flush (rate_flush / rate_finish): the
+// row leaves as rates + states, no k_transform pass; a step spanning more
+// buckets than the ring hands the series back (P.redo).
 template <class M, int K, int PF = 0, int NT = 0, int WAVES = 1, int ABL = 0,
-          int DPP = 0, int WIN = 0, int FL = 64>
+          int DPP = 0, int WIN = 0, int FL = 64, int RATE = 0>
 __global__ __launch_bounds__(256, WAVES) void k_bucketize_k(Params P,
                                                             BatchDev B,
                                                             SeriesMeta SM,
                                                             Rows R) {
   static_assert(K % 2 == 0, "K must be even (16-byte loads)");
   static_assert((WIN & (WIN - 1)) == 0, "WIN: power of two");
+  static_assert(!RATE || WIN > 0, "RATE needs the ring");
   constexpr int WS = WIN > 0 ? WIN : 1;
   __shared__ double ring_v[4][WS];
   const int lane = LANE;
   const int w = threadIdx.x >> 6;
   const int64_t s = (int64_t)blockIdx.x * 4 + w;
   if (s >= B.S) return;
-  if (!SM.keep[s]) return;
-  const int64_t lo = SM.lo[s], hi = SM.hi[s];
-  if (lo >= hi) return;
-  const int sf = B.series_float ? (int)B.series_float[s] : 1;
+  if (P.only_redo && !P.redo[s]) return;
   RowSink S{R.val + s * P.nb, R.state + s * P.nb, ring_v[w], WS - 1,
             WIN == 0, WIN == 0, ABL == 2, NT == 2};
+  const int64_t lo = SM.keep[s] ? SM.lo[s] : 0;
+  const int64_t hi = SM.keep[s] ? SM.hi[s] : 0;
+  if (lo >= hi) {
+    if (RATE) {  // contributes nowhere
+      for (int64_t b = lane; b < P.nb; b += 64) S.rows[b] = ST_ABSENT;
+      if (lane == 0) P.redo[s] = 0;
+    }
+    return;
+  }
+  const int sf = B.series_float ? (int)B.series_float[s] : 1;
+  RateState RS{P.rate_origin_ts, P.rate_origin_val, -1, 0.0, -1, -1, 0.0, 0, 0};
   int64_t flushed = 0;
   if (WIN) {
     for (int i = lane; i < WIN; i += 64) ring_v[w][i] = absent_value();
@@ -720,17 +873,35 @@ __global__ __launch_bounds__(256, WAVES) void k_bucketize_k(Params P,
     // step's loads are issued: vmcnt retires loads and stores in issue
     // order, so stores issued before a load would hold up its data
     if (base != base0)
-      ring_after<WIN, FL>(P, B, S, flushed, hi, base - PTS, PTS, carry_key);
-    ring_before<WIN, K>(P, B, S, flushed, lo, hi, base, t, carry_key);
+      ring_after<WIN, FL, RATE>(P, B, S, flushed, hi, base - PTS, PTS,
+                                carry_key, &RS);
+    if (ring_before<WIN, K, RATE>(P, B, S, flushed, lo, hi, base, t,
+                                  carry_key, &RS)) {
+      RS.bad = 1;  // RATE only: hand the series to the fallback kernels
+      break;
+    }
     reduce_step<M, K, DPP>(P, B, sf, lo, hi, base, i0, t, v, S, err,
                            carry_key, carry);
+  }
+  if (RATE && RS.bad) {
+    if (lane == 0) P.redo[s] = 1;
+    return;
   }
   if (carry_key >= 0 && carry_key < P.nb && lane == 0)
     S.put(carry_key, carry.finish(&err));
   // every bucket from the first point's to the last point's is written; a
   // last step that went direct already stored its buckets behind `flushed`
   // (the ring only holds absent slots there)
-  if (WIN && !S.direct) sink_flush(S, flushed, bucket_of(P, B.ts[hi - 1]) + 1);
+  const int64_t k_last = bucket_of(P, B.ts[hi - 1]);
+  if (WIN && !S.direct) sink_flush<RATE>(S, flushed, k_last + 1, &P, &RS);
+  if (RATE) {
+    if (RS.bad) {
+      if (lane == 0) P.redo[s] = 1;
+      return;
+    }
+    rate_finish(P, SM, s, S, RS, k_last);
+    if (lane == 0) P.redo[s] = 0;
+  }
 }
 
 // ------------------------------------------------------------------------
@@ -858,6 +1029,7 @@ __global__ __launch_bounds__(256) void k_transform(Params P, BatchDev B,
   const int lane = LANE;
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (s >= B.S) return;
+  if (P.only_redo && !P.redo[s]) return;
   const int64_t nb = P.nb;
   double* rowv = R.val + s * nb;
   uint8_t* rows = R.state + s * nb;

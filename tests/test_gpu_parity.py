@@ -407,3 +407,40 @@ def test_device_path_matches_host_path(engine):
     compare(host, ref, False, scale=100.0, where="host")
     for a, h in zip(got, host):
         assert np.array_equal(a.bits, h.bits)
+
+
+@pytest.mark.parametrize("ri", range(len(RATES)))
+def test_rate_long_gaps(engine, ri):
+    """Rate rows whose 512-point steps straddle gaps wider than the fused
+    kernel's 1,024-bucket ring (the series is handed back to k_bucketize +
+    k_transform) next to series that stay fused; 2 days of 1 m buckets."""
+    from opentsdb_amd.batch import HostBatch
+    rng = np.random.default_rng(70 + ri)
+    T0 = datasets.T0
+    offs, tss, vals = [0], [], []
+    for s in range(24):
+        parts = []
+        t = T0 + int(rng.integers(0, 10000))
+        for blk in range(int(rng.integers(1, 5))):
+            n = int(rng.integers(5, 200))
+            parts.append(t + 10000 * np.arange(n, dtype=np.int64))
+            # gaps from minutes to a day: > 1,024 buckets for some
+            t = int(parts[-1][-1]) + int(rng.choice([60000, 3600000, 20 * 3600000,
+                                                     26 * 3600000]))
+        ts = np.concatenate(parts)
+        ts = ts[ts < T0 + 2 * 86400000]
+        v = np.cumsum(rng.integers(0, 1000, len(ts))).astype(np.int64)
+        v[rng.random(len(ts)) < 0.03] = 0  # counter resets
+        tss.append(ts)
+        vals.append(v)
+        offs.append(offs[-1] + len(ts))
+    ts, val = np.concatenate(tss), np.concatenate(vals)
+    hb = HostBatch(np.array(offs, np.int64), ts, val,
+                   np.zeros(len(ts), np.uint8), None,
+                   np.array([0, 8, 16, 24], np.int64),
+                   np.arange(24, dtype=np.int64))
+    for agg, ds in (("sum", "sum"), ("max", "last"), ("dev", "max")):
+        spec = _spec(agg, ds, start=T0, end=T0 + 2 * 86400000 - 1000,
+                     rate=True, ro=RATES[ri])
+        check(engine, spec, hb, agg == "max", scale=1.0,
+              where="rategap%d/%s/%s" % (ri, agg, ds))
