@@ -570,8 +570,8 @@ __global__ void k_series_rows(int64_t R, int64_t S,
   for (int64_t s = prev + 1; s <= cur && s <= S; ++s) series_row[s] = r;
 }
 
-template <class M, int K>
-__global__ __launch_bounds__(256) void k_bucketize_cells(
+template <class M, int K, int WAVES = 1>
+__global__ __launch_bounds__(256, WAVES) void k_bucketize_cells(
     Params P, CellsDev C, const int64_t* __restrict__ series_row, int64_t S,
     SeriesMeta SM, Rows R, int* err_word) {
   static_assert(K % 2 == 0, "K");

@@ -136,6 +136,7 @@ struct Work {
   uint8_t* out_emit;
   int64_t* counts;
   uint64_t* keys = nullptr;
+  uint64_t* key_mm = nullptr;  // per (bucket, 64-member tile) min / max key
   SelState* sel = nullptr;
   uint32_t* hist = nullptr;
   Packed* comb = nullptr;      // two-level combine: first-level slices
@@ -648,6 +649,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     }
     if (sel_large) {
       W.keys = cv.take<uint64_t>((size_t)goff.back() * NB);
+      W.key_mm = cv.take<uint64_t>((size_t)((goff.back() + 63) / 64) * NB * 2);
       W.sel = cv.take<SelState>((size_t)T.LG * NB);
       W.hist = cv.take<uint32_t>((size_t)T.LG * NB * 512);
     }
@@ -687,6 +689,30 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     ok = with_monoid(spec->ds_agg_id, [&](auto tag) {
       using M = decltype(tag);
       StageTimer tm(c, 0);
+#ifdef OTSDB_BUCKETIZE_VARIANTS
+      if constexpr (std::is_same<M, MSum<1>>::value) {
+        const char* e = getenv("OTSDB_CELLS_VARIANT");  // tuning A/B
+        const int v = e ? atoi(e) : 0;
+        if (v == 1) {
+          hipLaunchKernelGGL((k_bucketize_cells<M, 6, 4>), dim3(blocks_for(S, 4)),
+                             dim3(256), 0, st, P, *cells, series_row, S, W.SM,
+                             W.R, c->d_err);
+          return;
+        }
+        if (v == 2) {
+          hipLaunchKernelGGL((k_bucketize_cells<M, 4, 4>), dim3(blocks_for(S, 4)),
+                             dim3(256), 0, st, P, *cells, series_row, S, W.SM,
+                             W.R, c->d_err);
+          return;
+        }
+        if (v == 3) {
+          hipLaunchKernelGGL((k_bucketize_cells<M, 6, 2>), dim3(blocks_for(S, 4)),
+                             dim3(256), 0, st, P, *cells, series_row, S, W.SM,
+                             W.R, c->d_err);
+          return;
+        }
+      }
+#endif
       hipLaunchKernelGGL((k_bucketize_cells<M, 6>), dim3(blocks_for(S, 4)),
                          dim3(256), 0, st, P, *cells, series_row, S, W.SM, W.R,
                          c->d_err);
@@ -921,8 +947,9 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         const int64_t M = goff.back();
         if (M > 0)
           hipLaunchKernelGGL(k_keys_transpose,
-                             dim3(blocks_for(M, 64), blocks_for(NB, 64)),
-                             dim3(256), 0, st, NB, M, d_members, W.R, W.keys);
+                             dim3(blocks_for(M, 64)),
+                             dim3(256), 0, st, NB, M, d_members, W.R, W.keys,
+                             nullptr);
         HIP_TRY(hipGetLastError());
         return OTSDB_OK;
       }
@@ -937,8 +964,9 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         const int64_t M = goff.back();
         const int64_t NSEG = T.LG * NB;
         hipLaunchKernelGGL(k_keys_transpose,
-                           dim3(blocks_for(M, 64), blocks_for(NB, 64)),
-                           dim3(256), 0, st, NB, M, d_members, W.R, W.keys);
+                           dim3(blocks_for(M, 64)),
+                           dim3(256), 0, st, NB, M, d_members, W.R, W.keys,
+                           W.key_mm);
         hipLaunchKernelGGL(k_sel_init, dim3(blocks_for(NSEG, 256)), dim3(256),
                            0, st, NB, T.LG, T.lg_g, (const double*)W.out_val,
                            (const uint8_t*)W.out_emit, W.sel, median, P.pct);
@@ -948,7 +976,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
                            0, st, NB, M, T.LG, T.lg_g, T.lg_off, T.lg_k,
                            (const uint64_t*)W.keys, (const SelState*)W.sel,
                            (const uint8_t*)W.out_emit, W.out_val, c->d_err,
-                           median, P.pct);
+                           median, P.pct, (const uint64_t*)W.key_mm);
       }
     } else {
       ok = with_monoid(spec->agg_id, [&](auto tag) {

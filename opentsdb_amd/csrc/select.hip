@@ -33,34 +33,77 @@ DEV double key_value(uint64_t k) {
   return __longlong_as_double((long long)u);
 }
 
+// One workgroup per 64 members sweeps their rows tile by tile (64 buckets):
+// the members' row offsets are read once, and the next tile's values and
+// states are loaded into registers before the current tile leaves LDS, so
+// each wave keeps a tile's loads in flight while it stores the previous one.
 __global__ __launch_bounds__(256) void k_keys_transpose(
     int64_t nb, int64_t M, const int64_t* __restrict__ members, Rows R,
-    uint64_t* __restrict__ keys) {
+    uint64_t* __restrict__ keys, uint64_t* __restrict__ mm) {
   __shared__ uint64_t tile[64][65];
+  __shared__ int64_t s_row[64];
+  __shared__ uint64_t s_mm[4][64][2];
+  const int64_t ntiles = gridDim.x;
   const int tid = threadIdx.x;
-  const int64_t m0 = (int64_t)blockIdx.x * 64, b0 = (int64_t)blockIdx.y * 64;
-  const int bi = tid & 63;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int mi = r * 4 + (tid >> 6);
-    const int64_t m = m0 + mi, b = b0 + bi;
-    uint64_t k = KEY_NONE;
-    if (m < M && b < nb) {
-      // both loads unconditional: the 16 rows' loads all go out at once
-      const int64_t off = members[m] * nb + b;
-      const uint8_t st = R.state[off];
-      const double v = R.val[off];
-      if (st && !is_nan(v)) k = dkey(v);
-    }
-    tile[mi][bi] = k;
-  }
+  const int64_t m0 = (int64_t)blockIdx.x * 64;
+  const int bi = tid & 63, w = tid >> 6;
+  if (tid < 64) s_row[tid] = m0 + tid < M ? members[m0 + tid] * nb : -1;
   __syncthreads();
-  const int mi = tid & 63;
+  double v[16];
+  uint8_t st[16];
+  auto load = [&](int64_t b0) {
+    const int64_t b = b0 + bi;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int bj = r * 4 + (tid >> 6);
-    const int64_t m = m0 + mi, b = b0 + bj;
-    if (m < M && b < nb) keys[b * M + m] = tile[mi][bj];
+    for (int r = 0; r < 16; ++r) {
+      const int64_t ro = s_row[r * 4 + w];
+      const bool in = ro >= 0 && b < nb;
+      // loads unconditional in shape: the 16 rows' loads all go out at once
+      const int64_t off = in ? ro + b : 0;
+      v[r] = R.val[off];
+      st[r] = in ? R.state[off] : (uint8_t)0;
+    }
+  };
+  load(0);
+  for (int64_t b0 = 0; b0 < nb; b0 += 64) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      tile[r * 4 + w][bi] = (st[r] && !is_nan(v[r])) ? dkey(v[r]) : KEY_NONE;
+    __syncthreads();
+    if (b0 + 64 < nb) load(b0 + 64);
+    const int64_t m = m0 + bi;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int bj = r * 4 + w;
+      const int64_t b = b0 + bj;
+      if (m < M && b < nb) keys[b * M + m] = tile[bi][bj];
+    }
+    if (mm) {
+      // the tile's min / max key per bucket over its non-NONE keys (k_seg_select's
+      // first pass): each thread folds 16 members of bucket column bi
+      uint64_t mn = KEY_NONE, mx = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint64_t x = tile[w * 16 + i][bi];
+        if (x != KEY_NONE) {
+          mn = x < mn ? x : mn;
+          mx = x > mx ? x : mx;
+        }
+      }
+      s_mm[w][bi][0] = mn;
+      s_mm[w][bi][1] = mx;
+      __syncthreads();
+      if (tid < 64 && b0 + tid < nb) {
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+          mn = s_mm[q][tid][0] < mn ? s_mm[q][tid][0] : mn;
+          mx = s_mm[q][tid][1] > mx ? s_mm[q][tid][1] : mx;
+        }
+        uint64_t* o = mm + 2 * ((b0 + tid) * ntiles + blockIdx.x);
+        o[0] = mn;
+        o[1] = mx;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -336,7 +379,7 @@ DEV double sel_value(int median, int64_t n, double pos, double lo, double hi) {
 constexpr int SS_BITS = 11;
 constexpr int SS_BINS = 1 << SS_BITS;
 constexpr int SS_CAP = 1024;
-constexpr int SS_THREADS = 256;
+constexpr int SS_THREADS = 1024;
 
 DEV uint64_t block_min_max_u64(uint64_t v, bool is_max, uint64_t* red) {
   // wave reduce then across the 4 waves of the block
@@ -359,7 +402,7 @@ __global__ __launch_bounds__(SS_THREADS) void k_seg_select(
     const int64_t* __restrict__ lg_off, const int64_t* __restrict__ lg_k,
     const uint64_t* __restrict__ keys, const SelState* __restrict__ sel,
     const uint8_t* __restrict__ emit, double* __restrict__ out_val,
-    int* err_word, int median, double p) {
+    int* err_word, int median, double p, const uint64_t* __restrict__ mm) {
   __shared__ uint32_t h[2][SS_BINS];
   __shared__ uint64_t cand[2][SS_CAP];
   __shared__ uint64_t red[SS_THREADS / 64];
@@ -393,13 +436,29 @@ __global__ __launch_bounds__(SS_THREADS) void k_seg_select(
       }
       for (; i < k; i += SS_THREADS) f(col[i]);
     };
-    // (1) min / max over the non-NONE keys
+    // (1) min / max over the non-NONE keys: from k_keys_transpose's
+    // per-(64-member tile, bucket) partials for the tiles wholly inside the
+    // segment, the keys of the partial tiles at its ends directly
     uint64_t mn = ~0ULL, mx = 0;
-    for_keys([&](uint64_t key) {
+    auto fold = [&](uint64_t key) {
       if (key == KEY_NONE) return;
       mn = key < mn ? key : mn;
       mx = key > mx ? key : mx;
-    });
+    };
+    const int64_t o0 = lg_off[lg], ntiles = (M + 63) / 64;
+    const int64_t t_lo = (o0 + 63) / 64, t_hi = (o0 + k) / 64;
+    if (mm && t_hi > t_lo) {
+      const uint64_t* pm = mm + 2 * (b * ntiles);
+      for (int64_t t = t_lo + tid; t < t_hi; t += SS_THREADS) {
+        mn = pm[2 * t] < mn ? pm[2 * t] : mn;
+        mx = pm[2 * t + 1] > mx ? pm[2 * t + 1] : mx;
+      }
+      const int64_t e0 = t_lo * 64 - o0, e1 = t_hi * 64 - o0;
+      for (int64_t i = tid; i < e0; i += SS_THREADS) fold(col[i]);
+      for (int64_t i = e1 + tid; i < k; i += SS_THREADS) fold(col[i]);
+    } else {
+      for_keys(fold);
+    }
     mn = block_min_max_u64(mn, false, red);
     mx = block_min_max_u64(mx, true, red);
     uint64_t prefix[2], mask[2];

@@ -15,6 +15,9 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--series", type=int, default=100000)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--variants", default="",
+                    help="comma list of OTSDB_CELLS_VARIANT values (variants "
+                         "build), timed interleaved")
     a = ap.parse_args()
     import torch
     from opentsdb_amd import workload
@@ -29,24 +32,43 @@ def main():
     torch.cuda.empty_cache()
     spec = workload.query_spec(a.config)
     res = DeviceResult(torch, db.n_groups, db.n_groups * 2100, "cuda")
-    workload.run_cells_device(eng, spec, cells, db, res)
-    eng.lib.otsdb_prof_enable(eng.ctx, 1)
-    eng.lib.otsdb_prof_read(eng.ctx, None, None, 0, 1)
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(a.reps):
-        workload.run_cells_device(eng, spec, cells, db, res)
-    torch.cuda.synchronize()
-    dq = (time.perf_counter() - t) / a.reps
-    ms = (C.c_double * 8)()
-    nn = (C.c_int64 * 8)()
-    eng.lib.otsdb_prof_read(eng.ctx, ms, nn, 8, 1)
-    kb = ms[0] / max(nn[0], 1) / 1e3
     cb = cells.n_bytes
-    print("cells: %d pts %.3f GB compacted; query %.2f ms (%.1f Gpts/s); "
-          "k_bucketize_cells %.2f ms = %.0f GB/s compacted"
-          % (n, cb / 1e9, dq * 1e3, n / dq / 1e9, kb * 1e3, cb / kb / 1e9))
-
+    vs = [v for v in a.variants.split(",") if v] or [None]
+    ref = None
+    times = {v: [] for v in vs}
+    for rnd in range(3 if len(vs) > 1 else 1):
+        for v in vs:
+            if v is not None:
+                os.environ["OTSDB_CELLS_VARIANT"] = v
+            workload.run_cells_device(eng, spec, cells, db, res)
+            torch.cuda.synchronize()
+            out = res.val[:int(res.offsets[-1])].clone()
+            if ref is None:
+                ref = out
+            same = out.numel() == ref.numel() and bool(
+                ((out.view(torch.float64) - ref.view(torch.float64)).abs()
+                 <= 1e-9 * ref.view(torch.float64).abs().clamp(min=1)).all())
+            eng.lib.otsdb_prof_enable(eng.ctx, 1)
+            eng.lib.otsdb_prof_read(eng.ctx, None, None, 0, 1)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(a.reps):
+                workload.run_cells_device(eng, spec, cells, db, res)
+            torch.cuda.synchronize()
+            dq = (time.perf_counter() - t) / a.reps
+            ms = (C.c_double * 8)()
+            nn = (C.c_int64 * 8)()
+            eng.lib.otsdb_prof_read(eng.ctx, ms, nn, 8, 1)
+            eng.lib.otsdb_prof_enable(eng.ctx, 0)
+            kb = ms[0] / max(nn[0], 1) / 1e3
+            times[v].append(kb)
+            print("variant %s round %d: %d pts %.3f GB compacted; query %.2f ms "
+                  "(%.1f Gpts/s); k_bucketize_cells %.2f ms = %.0f GB/s "
+                  "compacted; same as first: %s"
+                  % (v, rnd, n, cb / 1e9, dq * 1e3, n / dq / 1e9, kb * 1e3,
+                     cb / kb / 1e9, same), flush=True)
+    for v in vs:
+        print("variant %s: k_bucketize_cells min %.2f ms" % (v, min(times[v]) * 1e3))
 
 if __name__ == "__main__":
     main()
