@@ -137,6 +137,8 @@ struct Work {
   int64_t* counts;
   uint64_t* keys = nullptr;
   uint64_t* key_mm = nullptr;  // per (bucket, 64-member tile) min / max key
+  uint32_t* key_cnt = nullptr;  // per (bucket, tile) non-NaN keys (fill mode)
+  uint32_t* lg_kept = nullptr;  // per large group: holds a kept series
   SelState* sel = nullptr;
   uint32_t* hist = nullptr;
   Packed* comb = nullptr;      // two-level combine: first-level slices
@@ -550,6 +552,16 @@ bool bucketize_uses_ring(int code, int ds_agg) {
   return true;
 }
 
+// A/B knob: OTSDB_SEL_FUSED=0 keeps k_transform + k_group for fill-mode
+// percentiles
+static bool sel_fill_fused_on() {
+  static const bool on = [] {
+    const char* e = getenv("OTSDB_SEL_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <class M>
 void launch_combine(otsdb_ctx* c, const Work& W, int64_t NB, int64_t n,
                     const int64_t* g, const int64_t* t0, const int64_t* t1,
@@ -650,6 +662,8 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     if (sel_large) {
       W.keys = cv.take<uint64_t>((size_t)goff.back() * NB);
       W.key_mm = cv.take<uint64_t>((size_t)((goff.back() + 63) / 64) * NB * 2);
+      W.key_cnt = cv.take<uint32_t>((size_t)((goff.back() + 63) / 64) * NB);
+      W.lg_kept = cv.take<uint32_t>((size_t)T.LG + 1);
       W.sel = cv.take<SelState>((size_t)T.LG * NB);
       W.hist = cv.take<uint32_t>((size_t)T.LG * NB * 512);
     }
@@ -903,7 +917,12 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   const bool direct = P.sentinel && !P.rate && !P.fill && !P.run_all &&
                       (P.interp == 1 || P.interp == 2 || P.interp == 3) &&
                       !is_selection(spec->agg_id);
-  if (S > 0 && NB > 0 && !direct) {
+  // percentiles over a FillingDownsampler grid with every group large: the
+  // keys transpose applies the fill and counts, no k_transform / k_group
+  const bool sel_fused = is_selection(spec->agg_id) && mode == 0 &&
+                         P.sentinel && P.fill && !P.rate && !P.run_all &&
+                         T.LG > 0 && T.LG == G && sel_fill_fused_on();
+  if (S > 0 && NB > 0 && !direct && !sel_fused) {
     StageTimer tm(c, 1);
     // rate rows of up to 2,048 buckets stay in registers between the two
     // RateSpan passes (one row read, one write)
@@ -932,6 +951,26 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         return fail(OTSDB_E_UNSUPPORTED,
                     "percentiles across ranks: use the otsdb_sel_* protocol");
       const int median = spec->agg_id == OTSDB_AGG_MEDIAN ? 1 : 0;
+      if (sel_fused) {
+        const int64_t M = goff.back();
+        const int64_t NSEG = T.LG * NB;
+        HIP_TRY(hipMemsetAsync(W.lg_kept, 0, (size_t)T.LG * 4, st));
+        SelFill F{W.SM.keep, W.SM.kf, W.SM.kl, P.fill_value, W.key_cnt,
+                  T.lg_off, T.LG, W.lg_kept};
+        if (M > 0)
+          hipLaunchKernelGGL(k_keys_transpose<true>, dim3(blocks_for(M, 64)),
+                             dim3(256), 0, st, NB, M, d_members, W.R, W.keys,
+                             W.key_mm, F);
+        hipLaunchKernelGGL(k_seg_select, dim3((unsigned)NSEG), dim3(SS_THREADS),
+                           0, st, NB, M, T.LG, T.lg_g, T.lg_off, T.lg_k,
+                           (const uint64_t*)W.keys, (const SelState*)nullptr,
+                           (const uint8_t*)nullptr, W.out_val, c->d_err,
+                           median, P.pct, (const uint64_t*)W.key_mm,
+                           (const uint32_t*)W.key_cnt,
+                           (const uint32_t*)W.lg_kept, W.out_emit);
+        HIP_TRY(hipGetLastError());
+        return OTSDB_OK;
+      }
       // n (non-NaN contributions) and the emit mask of every group
       using MC = MSum<3>;
       if (T.T > 0)
@@ -946,10 +985,10 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         // cross-rank protocol: local counts + keys only (otsdb_sel_*)
         const int64_t M = goff.back();
         if (M > 0)
-          hipLaunchKernelGGL(k_keys_transpose,
+          hipLaunchKernelGGL(k_keys_transpose<false>,
                              dim3(blocks_for(M, 64)),
                              dim3(256), 0, st, NB, M, d_members, W.R, W.keys,
-                             nullptr);
+                             nullptr, SelFill{});
         HIP_TRY(hipGetLastError());
         return OTSDB_OK;
       }
@@ -963,10 +1002,10 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       if (T.LG > 0) {
         const int64_t M = goff.back();
         const int64_t NSEG = T.LG * NB;
-        hipLaunchKernelGGL(k_keys_transpose,
+        hipLaunchKernelGGL(k_keys_transpose<false>,
                            dim3(blocks_for(M, 64)),
                            dim3(256), 0, st, NB, M, d_members, W.R, W.keys,
-                           W.key_mm);
+                           W.key_mm, SelFill{});
         hipLaunchKernelGGL(k_sel_init, dim3(blocks_for(NSEG, 256)), dim3(256),
                            0, st, NB, T.LG, T.lg_g, (const double*)W.out_val,
                            (const uint8_t*)W.out_emit, W.sel, median, P.pct);
@@ -976,7 +1015,9 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
                            0, st, NB, M, T.LG, T.lg_g, T.lg_off, T.lg_k,
                            (const uint64_t*)W.keys, (const SelState*)W.sel,
                            (const uint8_t*)W.out_emit, W.out_val, c->d_err,
-                           median, P.pct, (const uint64_t*)W.key_mm);
+                           median, P.pct, (const uint64_t*)W.key_mm,
+                           (const uint32_t*)nullptr, (const uint32_t*)nullptr,
+                           (uint8_t*)nullptr);
       }
     } else {
       ok = with_monoid(spec->agg_id, [&](auto tag) {

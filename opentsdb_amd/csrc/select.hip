@@ -33,21 +33,73 @@ DEV double key_value(uint64_t k) {
   return __longlong_as_double((long long)u);
 }
 
+// Fill-mode selection without k_transform / k_group (percentiles over a
+// FillingDownsampler grid, every group large): the transpose applies the
+// fill itself (a kept series contributes every bucket, its real value or the
+// fill value; FillingDownsampler.java:258-272), counts the non-NaN keys per
+// (bucket, tile) and flags the groups that hold a kept series (they emit
+// every bucket); k_seg_select derives n and the targets from that.
+struct SelFill {
+  const uint8_t* keep;     // null: the rows are final (k_transform ran)
+  const int32_t* kf;       // sentinel rows: buckets [kf, kl] written
+  const int32_t* kl;
+  double fill_value;
+  uint32_t* cnt;           // [nb][ntiles] non-NONE keys per (bucket, tile)
+  const int64_t* lg_off;   // every group is large: member ranges
+  int64_t n_lg;
+  uint32_t* kept;          // [n_lg] the group has a kept series
+};
+
 // One workgroup per 64 members sweeps their rows tile by tile (64 buckets):
 // the members' row offsets are read once, and the next tile's values and
 // states are loaded into registers before the current tile leaves LDS, so
 // each wave keeps a tile's loads in flight while it stores the previous one.
+// mm (optional): per (bucket, tile) min / max non-NONE key, k_seg_select's
+// first pass.
+template <bool FILL>
 __global__ __launch_bounds__(256) void k_keys_transpose(
     int64_t nb, int64_t M, const int64_t* __restrict__ members, Rows R,
-    uint64_t* __restrict__ keys, uint64_t* __restrict__ mm) {
+    uint64_t* __restrict__ keys, uint64_t* __restrict__ mm, SelFill F) {
   __shared__ uint64_t tile[64][65];
   __shared__ int64_t s_row[64];
+  __shared__ int32_t s_kf[64], s_kl[64];
   __shared__ uint64_t s_mm[4][64][2];
+  __shared__ uint32_t s_cnt[4][64];
   const int64_t ntiles = gridDim.x;
   const int tid = threadIdx.x;
   const int64_t m0 = (int64_t)blockIdx.x * 64;
   const int bi = tid & 63, w = tid >> 6;
-  if (tid < 64) s_row[tid] = m0 + tid < M ? members[m0 + tid] * nb : -1;
+  if (tid < 64) {
+    const int64_t m = m0 + tid;
+    const int64_t sr = m < M ? members[m] : -1;
+    s_row[tid] = sr >= 0 ? sr * nb : -1;
+    if (FILL) {
+      const bool kp = sr >= 0 && F.keep[sr];
+      // not kept: contributes nowhere (kf > kl and no fill)
+      s_kf[tid] = kp ? F.kf[sr] : 1;
+      s_kl[tid] = kp ? F.kl[sr] : 0;
+      if (!kp) s_row[tid] = -1;
+      int64_t g = 0;  // the member's group: the last lg_off <= m
+      if (kp) {
+        int64_t hi = F.n_lg;
+        while (hi - g > 1) {
+          const int64_t mid = (g + hi) >> 1;
+          if (F.lg_off[mid] <= m) g = mid;
+          else hi = mid;
+        }
+      }
+      // one flag write per distinct group of the wave (all of one group,
+      // mostly): a flag every member raised would be 64 atomics per tile on
+      // one word
+      uint64_t todo = __ballot(kp);
+      while (todo) {
+        const int lead = __builtin_ctzll(todo);
+        const int64_t gl = readlane_l(g, lead);
+        if (tid == lead && !F.kept[gl]) atomicOr(&F.kept[gl], 1u);
+        todo &= ~__ballot(kp && g == gl);
+      }
+    }
+  }
   __syncthreads();
   double v[16];
   uint8_t st[16];
@@ -60,14 +112,26 @@ __global__ __launch_bounds__(256) void k_keys_transpose(
       // loads unconditional in shape: the 16 rows' loads all go out at once
       const int64_t off = in ? ro + b : 0;
       v[r] = R.val[off];
-      st[r] = in ? R.state[off] : (uint8_t)0;
+      if (!FILL) st[r] = in ? R.state[off] : (uint8_t)0;
     }
   };
   load(0);
   for (int64_t b0 = 0; b0 < nb; b0 += 64) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-      tile[r * 4 + w][bi] = (st[r] && !is_nan(v[r])) ? dkey(v[r]) : KEY_NONE;
+    for (int r = 0; r < 16; ++r) {
+      const int mi = r * 4 + w;
+      uint64_t k;
+      if (FILL) {
+        const int64_t b = b0 + bi;
+        const bool real = b >= s_kf[mi] && b <= s_kl[mi] &&
+                          __double_as_longlong(v[r]) != kAbsentBits;
+        const double x = real ? v[r] : F.fill_value;
+        k = (s_row[mi] >= 0 && b < nb && !is_nan(x)) ? dkey(x) : KEY_NONE;
+      } else {
+        k = (st[r] && !is_nan(v[r])) ? dkey(v[r]) : KEY_NONE;
+      }
+      tile[mi][bi] = k;
+    }
     __syncthreads();
     if (b0 + 64 < nb) load(b0 + 64);
     const int64_t m = m0 + bi;
@@ -78,29 +142,34 @@ __global__ __launch_bounds__(256) void k_keys_transpose(
       if (m < M && b < nb) keys[b * M + m] = tile[bi][bj];
     }
     if (mm) {
-      // the tile's min / max key per bucket over its non-NONE keys (k_seg_select's
-      // first pass): each thread folds 16 members of bucket column bi
+      // the tile's min / max key (and, FILL, count) per bucket over its
+      // non-NONE keys: each thread folds 16 members of bucket column bi
       uint64_t mn = KEY_NONE, mx = 0;
+      uint32_t nk = 0;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const uint64_t x = tile[w * 16 + i][bi];
         if (x != KEY_NONE) {
           mn = x < mn ? x : mn;
           mx = x > mx ? x : mx;
+          ++nk;
         }
       }
       s_mm[w][bi][0] = mn;
       s_mm[w][bi][1] = mx;
+      s_cnt[w][bi] = nk;
       __syncthreads();
       if (tid < 64 && b0 + tid < nb) {
 #pragma unroll
         for (int q = 1; q < 4; ++q) {
           mn = s_mm[q][tid][0] < mn ? s_mm[q][tid][0] : mn;
           mx = s_mm[q][tid][1] > mx ? s_mm[q][tid][1] : mx;
+          nk += s_cnt[q][tid];
         }
-        uint64_t* o = mm + 2 * ((b0 + tid) * ntiles + blockIdx.x);
-        o[0] = mn;
-        o[1] = mx;
+        const int64_t oi = (b0 + tid) * ntiles + blockIdx.x;
+        mm[2 * oi] = mn;
+        mm[2 * oi + 1] = mx;
+        if (FILL) F.cnt[oi] = nk;
       }
     }
     __syncthreads();
@@ -115,20 +184,14 @@ struct SelState {
   int32_t _pad;
 };
 
-// segments: seg = lg * nb + b for large group lg (group id lg_g[lg])
-__global__ void k_sel_init(int64_t nb, int64_t n_lg,
-                           const int64_t* __restrict__ lg_g,
-                           const double* __restrict__ count_val,
-                           const uint8_t* __restrict__ count_emit,
-                           SelState* __restrict__ sel, int median, double p) {
-  const int64_t seg = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (seg >= n_lg * nb) return;
-  const int64_t lg = seg / nb, b = seg - lg * nb;
-  const int64_t o = lg_g[lg] * nb + b;
+// the one or two order statistics Median / PercentileAgg.runDouble read
+// over n non-NaN values (Aggregators.java:412-431, :687-706)
+DEV SelState sel_state_of(int64_t n, int median, double p) {
   SelState s;
   s.prefix[0] = s.prefix[1] = 0;
-  s.n = count_emit[o] ? (int64_t)count_val[o] : 0;
+  s.n = n;
   s.ntarget = 0;
+  s._pad = 0;
   s.rank[0] = s.rank[1] = 0;
   if (s.n > 0) {
     if (median) {
@@ -149,7 +212,20 @@ __global__ void k_sel_init(int64_t nb, int64_t n_lg,
     }
     s.ntarget = (s.rank[0] == s.rank[1]) ? 1 : 2;
   }
-  sel[seg] = s;
+  return s;
+}
+
+// segments: seg = lg * nb + b for large group lg (group id lg_g[lg])
+__global__ void k_sel_init(int64_t nb, int64_t n_lg,
+                           const int64_t* __restrict__ lg_g,
+                           const double* __restrict__ count_val,
+                           const uint8_t* __restrict__ count_emit,
+                           SelState* __restrict__ sel, int median, double p) {
+  const int64_t seg = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (seg >= n_lg * nb) return;
+  const int64_t lg = seg / nb, b = seg - lg * nb;
+  const int64_t o = lg_g[lg] * nb + b;
+  sel[seg] = sel_state_of(count_emit[o] ? (int64_t)count_val[o] : 0, median, p);
 }
 
 __global__ __launch_bounds__(256) void k_radix_hist(
@@ -397,12 +473,25 @@ DEV uint64_t block_min_max_u64(uint64_t v, bool is_max, uint64_t* red) {
   return r;
 }
 
+DEV uint64_t block_sum_u64(uint64_t v, uint64_t* red) {
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if (LANE == 0) red[w] = v;
+  __syncthreads();
+  uint64_t r = 0;
+  for (int j = 0; j < SS_THREADS / 64; ++j) r += red[j];
+  return r;
+}
+
 __global__ __launch_bounds__(SS_THREADS) void k_seg_select(
     int64_t nb, int64_t M, int64_t n_lg, const int64_t* __restrict__ lg_g,
     const int64_t* __restrict__ lg_off, const int64_t* __restrict__ lg_k,
     const uint64_t* __restrict__ keys, const SelState* __restrict__ sel,
     const uint8_t* __restrict__ emit, double* __restrict__ out_val,
-    int* err_word, int median, double p, const uint64_t* __restrict__ mm) {
+    int* err_word, int median, double p, const uint64_t* __restrict__ mm,
+    const uint32_t* __restrict__ cnt_p, const uint32_t* __restrict__ kept,
+    uint8_t* __restrict__ out_emit) {
   __shared__ uint32_t h[2][SS_BINS];
   __shared__ uint64_t cand[2][SS_CAP];
   __shared__ uint64_t red[SS_THREADS / 64];
@@ -415,35 +504,46 @@ __global__ __launch_bounds__(SS_THREADS) void k_seg_select(
   if (seg >= n_lg * nb) return;
   const int64_t lg = seg / nb, b = seg - lg * nb;
   const int64_t o = lg_g[lg] * nb + b;
-  if (!emit[o]) return;
-  const SelState s0 = sel[seg];
-  const int nt = s0.ntarget;
+  const bool fused = cnt_p != nullptr;
+  if (fused) {  // FillingDownsampler grid: every bucket of a group holding a
+                // kept series is emitted
+    const bool e = kept[lg] != 0;
+    if (tid == 0) out_emit[o] = e;
+    if (!e) return;
+  } else if (!emit[o]) {
+    return;
+  }
+  SelState s0;
+  if (!fused) s0 = sel[seg];
   double r = qnan();
-  if (nt > 0) {
-    const uint64_t* col = keys + b * M + lg_off[lg];
-    const int64_t k = lg_k[lg];
-    // every key of the segment, 4 independent loads in flight per thread
-    auto for_keys = [&](auto&& f) {
-      int64_t i = tid;
-      for (; i + 3 * SS_THREADS < k; i += 4 * SS_THREADS) {
-        const uint64_t a0 = col[i], a1 = col[i + SS_THREADS],
-                       a2 = col[i + 2 * SS_THREADS],
-                       a3 = col[i + 3 * SS_THREADS];
-        f(a0);
-        f(a1);
-        f(a2);
-        f(a3);
-      }
-      for (; i < k; i += SS_THREADS) f(col[i]);
-    };
-    // (1) min / max over the non-NONE keys: from k_keys_transpose's
-    // per-(64-member tile, bucket) partials for the tiles wholly inside the
-    // segment, the keys of the partial tiles at its ends directly
-    uint64_t mn = ~0ULL, mx = 0;
+  const uint64_t* col = keys + b * M + lg_off[lg];
+  const int64_t k = lg_k[lg];
+  // every key of the segment, 4 independent loads in flight per thread
+  auto for_keys = [&](auto&& f) {
+    int64_t i = tid;
+    for (; i + 3 * SS_THREADS < k; i += 4 * SS_THREADS) {
+      const uint64_t a0 = col[i], a1 = col[i + SS_THREADS],
+                     a2 = col[i + 2 * SS_THREADS],
+                     a3 = col[i + 3 * SS_THREADS];
+      f(a0);
+      f(a1);
+      f(a2);
+      f(a3);
+    }
+    for (; i < k; i += SS_THREADS) f(col[i]);
+  };
+  // (1) min / max (fused: and count) over the non-NONE keys: from
+  // k_keys_transpose's per-(64-member tile, bucket) partials for the tiles
+  // wholly inside the segment, the keys of the partial tiles at its ends
+  // directly
+  uint64_t mn = ~0ULL, mx = 0;
+  if (fused || s0.ntarget > 0) {
+    uint64_t nn = 0;
     auto fold = [&](uint64_t key) {
       if (key == KEY_NONE) return;
       mn = key < mn ? key : mn;
       mx = key > mx ? key : mx;
+      ++nn;
     };
     const int64_t o0 = lg_off[lg], ntiles = (M + 63) / 64;
     const int64_t t_lo = (o0 + 63) / 64, t_hi = (o0 + k) / 64;
@@ -452,6 +552,7 @@ __global__ __launch_bounds__(SS_THREADS) void k_seg_select(
       for (int64_t t = t_lo + tid; t < t_hi; t += SS_THREADS) {
         mn = pm[2 * t] < mn ? pm[2 * t] : mn;
         mx = pm[2 * t + 1] > mx ? pm[2 * t + 1] : mx;
+        if (fused) nn += cnt_p[b * ntiles + t];
       }
       const int64_t e0 = t_lo * 64 - o0, e1 = t_hi * 64 - o0;
       for (int64_t i = tid; i < e0; i += SS_THREADS) fold(col[i]);
@@ -461,6 +562,10 @@ __global__ __launch_bounds__(SS_THREADS) void k_seg_select(
     }
     mn = block_min_max_u64(mn, false, red);
     mx = block_min_max_u64(mx, true, red);
+    if (fused) s0 = sel_state_of((int64_t)block_sum_u64(nn, red), median, p);
+  }
+  const int nt = s0.ntarget;
+  if (nt > 0) {
     uint64_t prefix[2], mask[2];
     int64_t rank[2], cnt[2];
     int shift = 0;

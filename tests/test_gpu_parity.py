@@ -256,6 +256,29 @@ def test_percentiles_large_groups(engine, n_series, kind):
                 n_series, agg, fill))
 
 
+def test_percentiles_fill_several_large_groups(engine):
+    """Fill-mode percentiles with every group large: the keys transpose
+    applies the FillingDownsampler fill and counts the non-NaN keys per
+    (bucket, 64-member tile), with group boundaries inside tiles and a group
+    whose series are all empty (not kept: it emits nothing)."""
+    import numpy as np
+    from opentsdb_amd.batch import HostBatch
+    b = datasets.random_batch(79, n_series=300, n_groups=3,
+                              span_ms=3600 * 1000, cadence_ms=30000,
+                              nan_frac=0.05, empty_frac=0.1)
+    n_empty = 40
+    offs = np.concatenate([b.offsets, np.full(n_empty, b.offsets[-1])])
+    g_off = np.concatenate([b.group_offsets, [b.group_offsets[-1] + n_empty]])
+    members = np.concatenate([b.group_members,
+                              300 + np.arange(n_empty, dtype=np.int64)])
+    b2 = HostBatch(offs.astype(np.int64), b.ts, b.val, b.is_float, None,
+                   g_off.astype(np.int64), members.astype(np.int64))
+    for agg in ("median", "p50", "p99", "p999", "ep95r3"):
+        for fill in ("nan", "null", "zero"):
+            spec = _spec(agg, "avg", fill, end=datasets.T0 + 3600 * 1000)
+            check(engine, spec, b2, True, where="selfill/%s/%s" % (agg, fill))
+
+
 def test_got_infinity(engine):
     """AggregationIterator.doubleValue throws on +-Infinity
     (AggregationIterator.java:640-643)."""
