@@ -570,7 +570,7 @@ __global__ void k_series_rows(int64_t R, int64_t S,
   for (int64_t s = prev + 1; s <= cur && s <= S; ++s) series_row[s] = r;
 }
 
-template <class M, int K, int WAVES = 1>
+template <class M, int K, int WAVES = 1, int ABL = 0>
 __global__ __launch_bounds__(256, WAVES) void k_bucketize_cells(
     Params P, CellsDev C, const int64_t* __restrict__ series_row, int64_t S,
     SeriesMeta SM, Rows R, int* err_word) {
@@ -820,7 +820,12 @@ __global__ __launch_bounds__(256, WAVES) void k_bucketize_cells(
         }
       }
       const int64_t lo = st0 + sum_seek, hi = st0 + sum_stop;
-      if (hi > lo)
+      if (ABL == 1) {  // tuning ablation: decode only, no reduction
+        int64_t x = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) x ^= t[j] + v[j];
+        if (x == 42) Sk.rowv[0] = 1.0;
+      } else if (hi > lo)
         reduce_step<M, K, 1>(P, Bd, 1, lo, hi, st0, st0 + (int64_t)K * lane,
                              t, v, Sk, err, carry_key, carry);
       if (hi < st0 + n_st) {  // reached stop_ts inside this row

@@ -719,6 +719,12 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
                              W.R, c->d_err);
           return;
         }
+        if (v == 4) {
+          hipLaunchKernelGGL((k_bucketize_cells<M, 6, 1, 1>), dim3(blocks_for(S, 4)),
+                             dim3(256), 0, st, P, *cells, series_row, S, W.SM,
+                             W.R, c->d_err);
+          return;
+        }
         if (v == 3) {
           hipLaunchKernelGGL((k_bucketize_cells<M, 6, 2>), dim3(blocks_for(S, 4)),
                              dim3(256), 0, st, P, *cells, series_row, S, W.SM,
