@@ -309,7 +309,13 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_bucketize",
+                # the downsample stage's kernel: k_bucketize_group when the
+                # group-by folds into it (zimsum over one-chunk groups, C2),
+                # k_bucketize_k otherwise
+                "kernel": ("k_bucketize_group" if (
+                    args.config == "C2" and world == 1 and
+                    os.environ.get("OTSDB_GRP_FUSED", "1") != "0")
+                    else "k_bucketize_k"),
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

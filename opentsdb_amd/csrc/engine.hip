@@ -552,6 +552,29 @@ bool bucketize_uses_ring(int code, int ds_agg) {
   return true;
 }
 
+// k_bucketize_group's downsamplers (instantiated for these monoids only)
+template <class M>
+constexpr bool grp_fused_monoid() {
+  return std::is_same<M, MSum<0>>::value || std::is_same<M, MSum<1>>::value ||
+         std::is_same<M, MMinMax<false>>::value ||
+         std::is_same<M, MMinMax<true>>::value;
+}
+static bool grp_fused_ds(int ds_agg) {
+  bool r = false;
+  with_monoid(ds_agg, [&](auto tag) {
+    r = grp_fused_monoid<decltype(tag)>();
+  });
+  return r;
+}
+// A/B knob: OTSDB_GRP_FUSED=0 keeps series rows + k_group_direct for zimsum
+static bool grp_fused_on() {
+  static const bool on = [] {
+    const char* e = getenv("OTSDB_GRP_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // A/B knob: OTSDB_SEL_FUSED=0 keeps k_transform + k_group for fill-mode
 // percentiles
 static bool sel_fill_fused_on() {
@@ -696,6 +719,13 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   }();
   const bool rate_fused = rate_fuse_on && P.sentinel && P.rate && !P.fill &&
                           !P.run_all && c->bucketize_k == 0;
+  // zimsum over groups of one chunk each: k_bucketize_group builds the group
+  // rows in LDS (ZIM's 0.0 changes no sum), no series rows, no k_group
+  const bool grp_fused = grp_fused_on() && mode == 0 && !cells && P.sentinel &&
+                         !P.rate && !P.fill && !P.run_all && P.interp == 1 &&
+                         spec->agg_id == OTSDB_AGG_ZIMSUM && T.T > 0 &&
+                         T.MG == 0 && NB <= GRP_NB_MAX &&
+                         c->bucketize_k == 0 && grp_fused_ds(spec->ds_agg_id);
 
   bool ok = true;
   if (cells && S > 0 && NB > 0) {
@@ -910,6 +940,14 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
             PF.only_redo = 1;
             hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 256>), grid,
                                blk, 0, st, PF, B, W.SM, W.R);
+          } else if (grp_fused) {
+            // zimsum over single-chunk groups: the group row is built in
+            // LDS, no series rows and no k_group pass
+            if constexpr (grp_fused_monoid<M>())
+              hipLaunchKernelGGL((k_bucketize_group<M, 8>), dim3((unsigned)T.T),
+                                 dim3(256), 0, st, P, B, W.SM, T.tg, T.tm0,
+                                 T.tm1, d_members, W.out_val, W.out_emit,
+                                 c->d_err);
           } else {
             hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 256>), grid,
                                blk, 0, st, P, B, W.SM, W.R);
@@ -1028,7 +1066,9 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     } else {
       ok = with_monoid(spec->agg_id, [&](auto tag) {
         using M = decltype(tag);
-        if (T.T > 0 && direct)
+        if (grp_fused) {
+          // k_bucketize_group wrote the group rows
+        } else if (T.T > 0 && direct)
           hipLaunchKernelGGL(k_group_direct<M>, dim3(blocks_for(T.T * NB, 256)),
                              dim3(256), 0, st, P, NB, T.T, T.tg, T.tm0, T.tm1,
                              T.single, d_members, W.SM, W.R, W.partial,
@@ -1112,6 +1152,8 @@ otsdb_status finish(otsdb_ctx* c, int64_t G, otsdb_result* out) {
   if (err & ERR_CAL_RANGE)
     return fail(OTSDB_E_UNSUPPORTED,
                 "a point past the window lies outside the calendar table");
+  if (err & ERR_INTERNAL)
+    return fail(OTSDB_E_DEVICE, "internal: bucket outside the group row");
   if (total > out->capacity)
     return fail(OTSDB_E_CAPACITY, "result capacity %lld < %lld points",
                 (long long)out->capacity, (long long)total);

@@ -41,6 +41,7 @@ enum : int {
                         // in AggregationIterator.java:706-708, :776-778)
   ERR_RAW_DUP = 32,     // timestamps not increasing inside a raw span
   ERR_CAL_RANGE = 64,   // a point past the window outside the calendar table
+  ERR_INTERNAL = 128,   // engine invariant broken          -> E_DEVICE
 };
 
 struct Params {

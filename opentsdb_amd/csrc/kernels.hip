@@ -308,7 +308,29 @@ struct RowSink {
   int states;      // direct writes also store the state byte (no ring)
   int nostore;     // tuning ablation (ABL == 2): the flush stores nothing
   int nt;          // flush with non-temporal stores
+  // group mode (k_bucketize_group): closed buckets fold straight into the
+  // workgroup's LDS group row instead of the series row
+  double* gsum;    // sum of the non-NaN bucket values
+  uint32_t* gcnt;  // packed: real (bits 0-9), non-NaN (10-19), real strictly
+                   // inside (gkf, gkl) (20-29)
+  int32_t gkf, gkl;
+  int32_t gnb;     // buckets in the group row
+  int* gbad;       // set on a bucket index outside the row
   DEV void put(int k, double v) {
+    if (gsum) {
+      if ((uint32_t)k >= (uint32_t)gnb) {  // never expected: report, no write
+        *gbad = 1;
+        return;
+      }
+      const bool nn = !is_nan(v);
+      if (nn) __hip_atomic_fetch_add(&gsum[k], v, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(&gcnt[k],
+                             1u | (nn ? (1u << 10) : 0u) |
+                                 ((k > gkf && k < gkl) ? (1u << 20) : 0u),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return;
+    }
     if (states) {
       rowv[k] = v;
       rows[k] = ST_REAL;
@@ -784,24 +806,17 @@ DEV void rate_finish(const Params& P, const SeriesMeta& SM, int64_t s,
 // RATE: RateSpan fused into the ring flush (rate_flush / rate_finish): the
 // row leaves as rates + states, no k_transform pass; a step spanning more
 // buckets than the ring hands the series back (P.redo).
-template <class M, int K, int PF = 0, int NT = 0, int WAVES = 1, int ABL = 0,
-          int DPP = 0, int WIN = 0, int FL = 64, int RATE = 0>
-__global__ __launch_bounds__(256, WAVES) void k_bucketize_k(Params P,
-                                                            BatchDev B,
-                                                            SeriesMeta SM,
-                                                            Rows R) {
+// One series (wavefront) of k_bucketize_k: S says where its closed buckets
+// go (row, LDS ring, or k_bucketize_group's group row).
+template <class M, int K, int PF, int NT, int ABL, int DPP, int WIN, int FL,
+          int RATE>
+DEV void bucketize_series(const Params& P, const BatchDev& B,
+                          const SeriesMeta& SM, RowSink& S, double* ring,
+                          int64_t s) {
   static_assert(K % 2 == 0, "K must be even (16-byte loads)");
   static_assert((WIN & (WIN - 1)) == 0, "WIN: power of two");
   static_assert(!RATE || WIN > 0, "RATE needs the ring");
-  constexpr int WS = WIN > 0 ? WIN : 1;
-  __shared__ double ring_v[4][WS];
   const int lane = LANE;
-  const int w = threadIdx.x >> 6;
-  const int64_t s = (int64_t)blockIdx.x * 4 + w;
-  if (s >= B.S) return;
-  if (P.only_redo && !P.redo[s]) return;
-  RowSink S{R.val + s * P.nb, R.state + s * P.nb, ring_v[w], WS - 1,
-            WIN == 0, WIN == 0, ABL == 2, NT == 2};
   const int64_t lo = SM.keep[s] ? SM.lo[s] : 0;
   const int64_t hi = SM.keep[s] ? SM.hi[s] : 0;
   if (lo >= hi) {
@@ -815,7 +830,7 @@ __global__ __launch_bounds__(256, WAVES) void k_bucketize_k(Params P,
   RateState RS{P.rate_origin_ts, P.rate_origin_val, -1, 0.0, -1, -1, 0.0, 0, 0};
   int64_t flushed = 0;
   if (WIN) {
-    for (int i = lane; i < WIN; i += 64) ring_v[w][i] = absent_value();
+    for (int i = lane; i < WIN; i += 64) ring[i] = absent_value();
     flushed = bucket_of(P, B.ts[lo]);
   }
   int err = 0;
@@ -902,6 +917,125 @@ __global__ __launch_bounds__(256, WAVES) void k_bucketize_k(Params P,
     rate_finish(P, SM, s, S, RS, k_last);
     if (lane == 0) P.redo[s] = 0;
   }
+}
+
+template <class M, int K, int PF = 0, int NT = 0, int WAVES = 1, int ABL = 0,
+          int DPP = 0, int WIN = 0, int FL = 64, int RATE = 0>
+__global__ __launch_bounds__(256, WAVES) void k_bucketize_k(Params P,
+                                                            BatchDev B,
+                                                            SeriesMeta SM,
+                                                            Rows R) {
+  constexpr int WS = WIN > 0 ? WIN : 1;
+  __shared__ double ring_v[4][WS];
+  const int w = threadIdx.x >> 6;
+  const int64_t s = (int64_t)blockIdx.x * 4 + w;
+  if (s >= B.S) return;
+  if (P.only_redo && !P.redo[s]) return;
+  RowSink S{R.val + s * P.nb, R.state + s * P.nb, ring_v[w], WS - 1,
+            WIN == 0, WIN == 0, ABL == 2, NT == 2};
+  bucketize_series<M, K, PF, NT, ABL, DPP, WIN, FL, RATE>(P, B, SM, S,
+                                                          ring_v[w], s);
+}
+
+// ------------------------------------------------------------------------
+// k_bucketize_group: zimsum over groups of at most one 256-series chunk with
+// NONE fill and no rate (C2's zimsum:5m-avg{host=*}).  One workgroup per
+// group; its wavefronts take the group's series in turn and fold every
+// closed bucket straight into the group's LDS row (f64 sum of the non-NaN
+// values, packed counts) — no series rows, no k_group pass.  ZIM's 0.0 for a
+// series inside a gap (or past its last bucket toward a point past the
+// window) changes no sum (0.0 + x is exact); it only decides "0.0, not NaN"
+// when no real value is a number, so the block counts those contributors
+// with a difference array over [kf + 1, kl) (+ (kl, nb) with a point past
+// the window) minus the real points strictly inside.  The group's series add
+// into a bucket in whatever order their wavefronts reach it (LDS atomics):
+// within 1e-12 relative of the reference's SpanCmp-order sum, not bit for
+// bit (OTSDB_GRP_FUSED=0 keeps the ordered k_group_direct).
+// ------------------------------------------------------------------------
+constexpr int GRP_NB_MAX = 2048;
+
+template <class M, int K>
+__global__ __launch_bounds__(256) void k_bucketize_group(
+    Params P, BatchDev B, SeriesMeta SM, const int64_t* __restrict__ tile_g,
+    const int64_t* __restrict__ tile_m0, const int64_t* __restrict__ tile_m1,
+    const int64_t* __restrict__ members, double* __restrict__ out_val,
+    uint8_t* __restrict__ out_emit, int* err_word) {
+  __shared__ double gsum[GRP_NB_MAX];
+  __shared__ uint32_t gcnt[GRP_NB_MAX];
+  __shared__ int32_t span[GRP_NB_MAX + 1];
+  __shared__ int32_t s_scan[256];
+  __shared__ int s_next, s_bad;
+  const int tid = threadIdx.x, lane = LANE;
+  const int64_t nb = P.nb;
+  const int64_t t = blockIdx.x;
+  for (int b = tid; b <= nb; b += 256) {
+    if (b < nb) {
+      gsum[b] = 0.0;
+      gcnt[b] = 0;
+    }
+    span[b] = 0;
+  }
+  if (tid == 0) s_next = s_bad = 0;
+  __syncthreads();
+  const int64_t m0 = tile_m0[t], m1 = tile_m1[t];
+  for (;;) {
+    int i = 0;
+    if (lane == 0) i = atomicAdd(&s_next, 1);
+    i = __shfl(i, 0);
+    if (m0 + i >= m1) break;
+    const int64_t s = members[m0 + i];
+    const int32_t kf = SM.kf[s], kl = SM.kl[s];
+    if (lane == 0 && SM.keep[s] && kf <= kl) {
+      if (kl > kf + 1) {
+        atomicAdd(&span[kf + 1], 1);
+        atomicAdd(&span[kl], -1);
+      }
+      if (SM.of_has[s] && kl + 1 < nb) atomicAdd(&span[kl + 1], 1);
+    }
+    RowSink S{nullptr, nullptr, nullptr, 0, 1, 1, 0, 0,
+              gsum, gcnt, kf, kl, (int32_t)nb, &s_bad};
+    bucketize_series<M, K, 0, 0, 0, 1, 0, 64, 0>(P, B, SM, S, nullptr, s);
+  }
+  __syncthreads();
+  // span -> number of series contributing ZIM's 0.0 at each bucket (before
+  // subtracting those with a real point there): block prefix sum, 8 buckets
+  // per thread
+  constexpr int PER = GRP_NB_MAX / 256;
+  int32_t loc[PER], acc = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int b = tid * PER + j;
+    acc += b < nb ? span[b] : 0;
+    loc[j] = acc;
+  }
+  s_scan[tid] = acc;
+  __syncthreads();
+  for (int d = 1; d < 256; d <<= 1) {
+    const int32_t y = tid >= d ? s_scan[tid - d] : 0;
+    __syncthreads();
+    s_scan[tid] += y;
+    __syncthreads();
+  }
+  const int32_t excl = tid > 0 ? s_scan[tid - 1] : 0;
+  const int64_t g = tile_g[t];
+  int e = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int b = tid * PER + j;
+    if (b >= nb) break;
+    const uint32_t c = gcnt[b];
+    const int real = (int)(c & 1023), nn = (int)((c >> 10) & 1023);
+    const int cst = excl + loc[j] - (int)(c >> 20);
+    double r = 0.0;
+    if (real) {
+      r = nn ? gsum[b] : (cst > 0 ? 0.0 : qnan());
+      if (is_inf(r)) e |= ERR_INFINITY;
+    }
+    out_val[g * nb + b] = r;
+    out_emit[g * nb + b] = (uint8_t)(real > 0);
+  }
+  if (tid == 0 && s_bad) e |= ERR_INTERNAL;
+  if (e) atomicOr(err_word, e);
 }
 
 // ------------------------------------------------------------------------

@@ -122,7 +122,10 @@ def test_cross_series_aggregators(engine, agg):
     b = datasets.random_batch(11, n_series=60, n_groups=6)
     for ds in ("avg", "max"):
         spec = _spec(agg, ds)
-        check(engine, spec, b, ds == "max", scale=100.0, where="%s:%s" % (agg, ds))
+        # zimsum over one-chunk groups folds in LDS as the series' wavefronts
+        # reach each bucket (k_bucketize_group): 1e-12, not bit for bit
+        exact = ds == "max" and agg != "zimsum"
+        check(engine, spec, b, exact, scale=100.0, where="%s:%s" % (agg, ds))
 
 
 @pytest.mark.parametrize("ds", DS)
