@@ -313,7 +313,7 @@ def main():
                 # group-by folds into it (zimsum over one-chunk groups, C2),
                 # k_bucketize_k otherwise
                 "kernel": ("k_bucketize_group" if (
-                    args.config == "C2" and world == 1 and
+                    args.config == "C2" and
                     os.environ.get("OTSDB_GRP_FUSED", "1") != "0")
                     else "k_bucketize_k"),
                 "achieved": achieved,
