@@ -934,9 +934,21 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
             // then the plain kernel for the series handed back
             Params PF = P;
             PF.redo = W.redo;
-            hipLaunchKernelGGL(
-                (k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 1024, 512, 1>), grid, blk,
-                0, st, PF, B, W.SM, W.R);
+            // launch-bounded to 128 VGPRs (4 waves / SIMD instead of the
+            // 3 its 140 VGPRs allow; 8 cold spills): C4 bucketize 14.1 ->
+            // 13.3 ms.  OTSDB_RATE_WAVES=1 keeps the unbounded build (A/B)
+            static const int rate_waves = [] {
+              const char* e = getenv("OTSDB_RATE_WAVES");
+              return e ? atoi(e) : 4;
+            }();
+            if (rate_waves == 4)
+              hipLaunchKernelGGL(
+                  (k_bucketize_k<M, 8, 0, 0, 4, 0, 1, 1024, 512, 1>), grid,
+                  blk, 0, st, PF, B, W.SM, W.R);
+            else
+              hipLaunchKernelGGL(
+                  (k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 1024, 512, 1>), grid,
+                  blk, 0, st, PF, B, W.SM, W.R);
             PF.only_redo = 1;
             hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 256>), grid,
                                blk, 0, st, PF, B, W.SM, W.R);
