@@ -65,6 +65,16 @@ DEV int64_t lower_bound(const int64_t* ts, int64_t a, int64_t b, int64_t t) {
   return a;
 }
 
+// lower_bound that first tests the ends of [a, b): when the whole series
+// lies on one side of t (every series of a whole-range query) no search runs
+// — the dependent-load chain of the binary search was most of k_prep
+DEV int64_t lower_bound_ends(const int64_t* ts, int64_t a, int64_t b,
+                             int64_t t) {
+  if (a >= b || ts[a] >= t) return a;
+  if (ts[b - 1] < t) return b;
+  return lower_bound(ts, a + 1, b - 1, t);
+}
+
 DEV int64_t wave_incl_max(int64_t x) {
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -108,8 +118,8 @@ __global__ void k_prep(Params P, BatchDev B, SeriesMeta SM, int* err_word) {
   int64_t of_ts = 0;
   double of_val = 0.0;
   if (keep) {
-    lo = lower_bound(B.ts, p0, p1, P.seek_ts);
-    hi = lower_bound(B.ts, lo, p1, P.stop_ts);
+    lo = lower_bound_ends(B.ts, p0, p1, P.seek_ts);
+    hi = lower_bound_ends(B.ts, lo, p1, P.stop_ts);
     if (!P.run_all && P.fill == 0 && hi < p1) {
       const int sf = B.series_float ? (int)B.series_float[s] : 1;
       const int64_t t = B.ts[hi];
