@@ -2,26 +2,32 @@
 
 hipcc cross-compiles without a GPU, so this runs in the CPU container; the
 resulting .so travels to the GPU box with the repository snapshot.
+
+The device code is split over translation units compiled in parallel: the
+engine (host code, the non-template kernels and the aggregator-templated
+ones) and one unit per downsampling monoid (csrc/ds_tu.hip with
+-DOTSDB_DS_MONOID=n: the downsample / ordered-fold kernels of that monoid).
 """
+import glob
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "engine.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in
-        ("engine.hip", "kernels.hip", "kernels.h", "monoids.h", "select.hip",
-         "decode.hip", "raw.hip")] + [
+CSRC = os.path.join(HERE, "csrc")
+DEPS = sorted(glob.glob(os.path.join(CSRC, "*.hip")) +
+              glob.glob(os.path.join(CSRC, "*.h"))) + [
     os.path.join(ROOT, "include", "otsdb_agg.h")]
 OUT_DIR = os.path.join(HERE, "_build")
 OUT = os.path.join(OUT_DIR, "libotsdb_agg.so")
-# tuning build: every k_bucketize variant compiled in (scripts/ab_bucketize.py)
-OUT_VARIANTS = os.path.join(OUT_DIR, "libotsdb_agg_variants.so")
 ARCH = os.environ.get("OTSDB_OFFLOAD_ARCH", "gfx950")
+N_DS_MONOIDS = 12  # dispatch.h with_monoid: distinct reduction state types
+HIPCC = "/opt/rocm/bin/hipcc"
 
 FLAGS = [
-    "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
+    "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC",
     # Java rounds every multiply and add separately: no FMA contraction
     "-ffp-contract=off",
     "-Wall", "-Wno-unused-variable", "-Wno-unused-lambda-capture",
@@ -36,22 +42,56 @@ def up_to_date(out=OUT):
     return all(os.path.getmtime(d) <= t for d in DEPS)
 
 
-def build(force=False, verbose=False, variants=False):
-    out = OUT_VARIANTS if variants else OUT
-    if not force and up_to_date(out):
-        return out
-    flags = list(FLAGS)
-    if variants:
-        flags.append("-DOTSDB_BUCKETIZE_VARIANTS=1")
-    os.makedirs(OUT_DIR, exist_ok=True)
-    cmd = ["/opt/rocm/bin/hipcc"] + flags + ["-o", out + ".tmp", SRC]
+def _units(out_dir, defines):
+    d = ["-D" + x for x in defines]
+    units = [(os.path.join(CSRC, "engine.hip"), d,
+              os.path.join(out_dir, "engine.o"))]
+    for m in range(N_DS_MONOIDS):
+        units.append((os.path.join(CSRC, "ds_tu.hip"),
+                      d + ["-DOTSDB_DS_MONOID=%d" % m],
+                      os.path.join(out_dir, "ds_%d.o" % m)))
+    return units
+
+
+def build(force=False, verbose=False, jobs=None, defines=(), out=None):
+    """defines / out: a debug or tuning variant (extra -D flags) built into
+    its own directory next to the production library."""
+    out_dir = OUT_DIR
+    if out:
+        out_dir = os.path.dirname(out)
+    OUT_ = out or OUT
+    if not force and up_to_date(OUT_):
+        return OUT_
+    os.makedirs(out_dir, exist_ok=True)
+    jobs = jobs or min(8, os.cpu_count() or 1)
+
+    def compile_unit(u):
+        src, extra, obj = u
+        cmd = [HIPCC] + FLAGS + extra + ["-c", "-o", obj + ".tmp", src]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                           text=True)
+        if r.returncode != 0:
+            raise RuntimeError("compile failed: %s\n%s" % (" ".join(cmd),
+                                                           r.stdout))
+        if r.stdout.strip() and verbose:
+            print(r.stdout, flush=True)
+        os.replace(obj + ".tmp", obj)
+        return obj
+
+    units = _units(out_dir, defines)
+    # the engine unit is the longest: start it first
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_unit, units))
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o",
+           OUT_ + ".tmp"] + objs
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(out + ".tmp", out)
-    return out
+    os.replace(OUT_ + ".tmp", OUT_)
+    return OUT_
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True,
-                variants="--variants" in sys.argv))
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -16,18 +16,10 @@
 #include <stdint.h>
 
 #include "kernels.h"
+#include "launch.h"
 
 namespace otsdb {
 
-struct CellsDev {
-  int64_t R;
-  const int64_t* row_series;
-  const int64_t* row_base_s;
-  const int64_t* qual_off;
-  const uint8_t* qual;
-  const int64_t* val_off;
-  const uint8_t* val;
-};
 
 enum : int { ERR_CORRUPT_CELL = 16 };
 
@@ -139,6 +131,7 @@ DEV bool decode_uniform(const CellsDev& C, int64_t r, int mode,
 }
 
 // one wavefront per row; mode 0 counts (and validates), mode 1 writes
+#ifndef OTSDB_DS_TU
 __global__ __launch_bounds__(256) void k_decode(
     CellsDev C, int mode, int64_t* __restrict__ row_count,
     const int64_t* __restrict__ row_out, uint8_t* __restrict__ fast,
@@ -259,6 +252,7 @@ __global__ __launch_bounds__(256) void k_decode(
   }
   if (__ballot(bad) && lane == 0) atomicOr(err_word, ERR_CORRUPT_CELL);
 }
+#endif  // OTSDB_DS_TU
 
 // ------------------------------------------------------------------------
 // k_encode: the inverse — columnar series -> compacted RowSeq columns, the
@@ -274,6 +268,7 @@ __global__ __launch_bounds__(256) void k_decode(
 // masks for the in-chunk parts, carries across chunks).  mode 0 counts
 // rows / qualifier bytes / value bytes per series, mode 1 writes them at
 // the per-series bases the caller scanned.
+#ifndef OTSDB_DS_TU
 // ------------------------------------------------------------------------
 DEV int enc_long_len(int64_t v) {
   if (v >= -128 && v <= 127) return 1;
@@ -403,6 +398,7 @@ __global__ __launch_bounds__(256) void k_encode(
     s_vb[s] = vo - vo0;
   }
 }
+#endif  // OTSDB_DS_TU
 
 // ------------------------------------------------------------------------
 // k_bucketize_cells: decode fused into the downsample.
@@ -560,6 +556,7 @@ DEV void lds_values(const uint8_t* lds, int o, int64_t* v) {
   }
 }
 
+#ifndef OTSDB_DS_TU
 __global__ void k_series_rows(int64_t R, int64_t S,
                               const int64_t* __restrict__ row_series,
                               int64_t* __restrict__ series_row) {
@@ -569,6 +566,7 @@ __global__ void k_series_rows(int64_t R, int64_t S,
   const int64_t cur = r == R ? S : row_series[r];
   for (int64_t s = prev + 1; s <= cur && s <= S; ++s) series_row[s] = r;
 }
+#endif  // OTSDB_DS_TU
 
 template <class M, int K, int WAVES = 1, int ABL = 0>
 __global__ __launch_bounds__(256, WAVES) void k_bucketize_cells(
@@ -911,6 +909,7 @@ __global__ __launch_bounds__(256, WAVES) void k_bucketize_cells(
 }
 
 // series point offsets from per-row output offsets (rows sorted by series)
+#ifndef OTSDB_DS_TU
 __global__ void k_series_offsets(int64_t R, int64_t S,
                                  const int64_t* __restrict__ row_series,
                                  const int64_t* __restrict__ row_out,
@@ -922,5 +921,6 @@ __global__ void k_series_offsets(int64_t R, int64_t S,
   const int64_t cur = r == R ? S : row_series[r];
   for (int64_t s = prev + 1; s <= cur && s <= S; ++s) offsets[s] = row_out[r];
 }
+#endif  // OTSDB_DS_TU
 
 }  // namespace otsdb

@@ -1,0 +1,94 @@
+// ds_tu.hip — the kernels templated on one downsampling monoid, compiled once
+// per monoid with -DOTSDB_DS_MONOID=<n> (opentsdb_amd/build.py runs the
+// thirteen compilations in parallel; the engine links them).  Non-template
+// kernels are compiled only in engine.hip (OTSDB_DS_TU hides them here).
+#define OTSDB_DS_TU 1
+#include "kernels.hip"
+#include "decode.hip"
+#include "fold.hip"
+
+namespace otsdb {
+
+namespace {
+inline unsigned ds_blocks(int64_t n, int per) {
+  return (unsigned)((n + per - 1) / per);
+}
+}  // namespace
+
+template <class M>
+bool launch_ds(DsKernel k, const DsLaunch& a) {
+  const int64_t S = a.B.S;
+  switch (k) {
+    case DS_PREP:
+      hipLaunchKernelGGL(k_prep<M>, dim3(ds_blocks(S, 256)), dim3(256), 0,
+                         a.st, a.P, a.B, a.SM, a.err);
+      OTSDB_DBG(a.st, "k_prep");
+      return true;
+    case DS_RING:  // production: LDS ring sink, sentinel rows, DPP scan
+      hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 256>),
+                         dim3(ds_blocks(S, 4)), dim3(256), 0, a.st, a.P, a.B,
+                         a.SM, a.R);
+      return true;
+    case DS_RATE:
+      // launch-bounded to 128 VGPRs (4 waves / SIMD instead of the 3 its 140
+      // VGPRs allow; 8 cold spills): C4 bucketize 14.1 -> 13.3 ms
+      hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 4, 0, 1, 1024, 512, 1>),
+                         dim3(ds_blocks(S, 4)), dim3(256), 0, a.st, a.P, a.B,
+                         a.SM, a.R);
+      return true;
+    case DS_CELLS:
+      hipLaunchKernelGGL((k_bucketize_cells<M, 6>), dim3(ds_blocks(S, 4)),
+                         dim3(256), 0, a.st, a.P, a.cells, a.series_row, S,
+                         a.SM, a.R, a.err);
+      return true;
+    case DS_FOLD_PREP:
+      if (a.NW > 1 && S > 0)
+        hipLaunchKernelGGL(k_fold_prep<M>,
+                           dim3(ds_blocks(S * (a.NW - 1), 256)), dim3(256), 0,
+                           a.st, a.P, a.B, a.SM, a.NW, a.WB, a.wc);
+      return true;
+    case DS_FOLD:
+      return with_monoid(a.agg_id, [&](auto tag) {
+        using A = decltype(tag);
+        hipLaunchKernelGGL((k_fold<M, A, 8>),
+                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(256), 0,
+                           a.st, a.P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
+                           a.tm1, a.single, a.members, a.wc, a.NW, a.partial,
+                           a.tile_emit, a.out_val, a.out_emit, a.err,
+                           a.always_partial);
+        OTSDB_DBG(a.st, "k_fold");
+      });
+  }
+  return false;
+}
+
+#ifndef OTSDB_DS_MONOID
+#error "compile with -DOTSDB_DS_MONOID=<0..12>"
+#endif
+#if OTSDB_DS_MONOID == 0
+template bool launch_ds<MSum<0>>(DsKernel, const DsLaunch&);
+#elif OTSDB_DS_MONOID == 1
+template bool launch_ds<MSum<1>>(DsKernel, const DsLaunch&);
+#elif OTSDB_DS_MONOID == 2
+template bool launch_ds<MSum<2>>(DsKernel, const DsLaunch&);
+#elif OTSDB_DS_MONOID == 3
+template bool launch_ds<MSum<3>>(DsKernel, const DsLaunch&);
+#elif OTSDB_DS_MONOID == 4
+template bool launch_ds<MMinMax<false>>(DsKernel, const DsLaunch&);
+#elif OTSDB_DS_MONOID == 5
+template bool launch_ds<MMinMax<true>>(DsKernel, const DsLaunch&);
+#elif OTSDB_DS_MONOID == 6
+template bool launch_ds<MDev>(DsKernel, const DsLaunch&);
+#elif OTSDB_DS_MONOID == 7
+template bool launch_ds<MFirstLast<false>>(DsKernel, const DsLaunch&);
+#elif OTSDB_DS_MONOID == 8
+template bool launch_ds<MFirstLast<true>>(DsKernel, const DsLaunch&);
+#elif OTSDB_DS_MONOID == 9
+template bool launch_ds<MMult>(DsKernel, const DsLaunch&);
+#elif OTSDB_DS_MONOID == 10
+template bool launch_ds<MDiff>(DsKernel, const DsLaunch&);
+#elif OTSDB_DS_MONOID == 11
+template bool launch_ds<MNone>(DsKernel, const DsLaunch&);
+#endif
+
+}  // namespace otsdb

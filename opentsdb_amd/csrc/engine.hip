@@ -25,6 +25,7 @@
 #include "select.hip"
 #include "decode.hip"
 #include "raw.hip"
+#include "launch.h"
 
 using namespace otsdb;
 
@@ -83,30 +84,6 @@ bool is_selection(int agg) {
 double pct_of(int agg) {  // PercentileAgg(percentile).evaluate(): p / 100d
   static const double P[6] = {99.9, 99.0, 95.0, 90.0, 75.0, 50.0};
   return P[(agg - OTSDB_AGG_P999) % 6] / 100.0;
-}
-
-// Calls f(M{}) with the reduction state type of aggregator `agg`.
-template <class F>
-bool with_monoid(int agg, F&& f) {
-  switch (agg) {
-    case OTSDB_AGG_SUM:
-    case OTSDB_AGG_PFSUM:
-    case OTSDB_AGG_ZIMSUM: f(MSum<0>{}); return true;
-    case OTSDB_AGG_AVG: f(MSum<1>{}); return true;
-    case OTSDB_AGG_SQUARESUM: f(MSum<2>{}); return true;
-    case OTSDB_AGG_COUNT: f(MSum<3>{}); return true;
-    case OTSDB_AGG_MIN:
-    case OTSDB_AGG_MIMMIN: f(MMinMax<false>{}); return true;
-    case OTSDB_AGG_MAX:
-    case OTSDB_AGG_MIMMAX: f(MMinMax<true>{}); return true;
-    case OTSDB_AGG_DEV: f(MDev{}); return true;
-    case OTSDB_AGG_FIRST: f(MFirstLast<false>{}); return true;
-    case OTSDB_AGG_LAST: f(MFirstLast<true>{}); return true;
-    case OTSDB_AGG_MULT: f(MMult{}); return true;
-    case OTSDB_AGG_DIFF: f(MDiff{}); return true;
-    case OTSDB_AGG_NONE: f(MNone{}); return true;
-    default: return false;
-  }
 }
 
 inline int64_t jmod(int64_t a, int64_t b) { return a % b; }
@@ -179,7 +156,6 @@ struct otsdb_ctx {
   size_t cells_col_cap = 0;
   void* cal = nullptr;  // calendar bucket edges of the current query
   size_t cal_cap = 0;
-  int bucketize_k = 0;  // k_bucketize variant (OTSDB_BUCKETIZE_K; 0 = production)
   void* dec_ws = nullptr;  // decode workspace
   size_t dec_ws_cap = 0;
   void* ws2 = nullptr;     // raw group-by: candidates, sort, selection slab
@@ -209,6 +185,17 @@ otsdb_status ensure(void** p, size_t* cap, size_t need) {
   *cap = n;
   return OTSDB_OK;
 }
+
+// Binds a caller's stream to the context for one call and restores the
+// context's own stream on every exit path (early HIP_TRY returns included).
+struct StreamBinding {
+  otsdb_ctx* c;
+  hipStream_t saved;
+  StreamBinding(otsdb_ctx* c_, void* hip_stream) : c(c_), saved(c_->stream) {
+    if (hip_stream) c->stream = (hipStream_t)hip_stream;
+  }
+  ~StreamBinding() { c->stream = saved; }
+};
 
 // --------------------------------------------------------------- planning
 struct Plan {
@@ -537,54 +524,6 @@ inline unsigned blocks_for(int64_t n, int per) {
 
 
 
-// Whether the k_bucketize variant `code` (OTSDB_BUCKETIZE_K) launched for
-// downsampler `ds_agg` writes sentinel rows through the LDS ring sink.
-bool bucketize_uses_ring(int code, int ds_agg) {
-  if (code == 2 || code == 4 || code == 8) return false;
-#ifdef OTSDB_BUCKETIZE_VARIANTS
-  static const int kDirect[] = {16, 41, 81, 86, 88, 46, 48, 99, 80, 40, 97,
-                                85, 89, 49, 82, 42, 96, 201, 202, 203, 204,
-                                205, 206};
-  if (ds_agg == OTSDB_AGG_AVG)
-    for (int d : kDirect)
-      if (code == d) return false;
-#endif
-  return true;
-}
-
-// k_bucketize_group's downsamplers (instantiated for these monoids only)
-template <class M>
-constexpr bool grp_fused_monoid() {
-  return std::is_same<M, MSum<0>>::value || std::is_same<M, MSum<1>>::value ||
-         std::is_same<M, MMinMax<false>>::value ||
-         std::is_same<M, MMinMax<true>>::value;
-}
-static bool grp_fused_ds(int ds_agg) {
-  bool r = false;
-  with_monoid(ds_agg, [&](auto tag) {
-    r = grp_fused_monoid<decltype(tag)>();
-  });
-  return r;
-}
-// A/B knob: OTSDB_GRP_FUSED=0 keeps series rows + k_group_direct for zimsum
-static bool grp_fused_on() {
-  static const bool on = [] {
-    const char* e = getenv("OTSDB_GRP_FUSED");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-// A/B knob: OTSDB_SEL_FUSED=0 keeps k_transform + k_group for fill-mode
-// percentiles
-static bool sel_fill_fused_on() {
-  static const bool on = [] {
-    const char* e = getenv("OTSDB_SEL_FUSED");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 template <class M>
 void launch_combine(otsdb_ctx* c, const Work& W, int64_t NB, int64_t n,
                     const int64_t* g, const int64_t* t0, const int64_t* t1,
@@ -609,8 +548,31 @@ void launch_combine(otsdb_ctx* c, const Work& W, int64_t NB, int64_t n,
                      out_partial, c->d_err, kCombineSlices);
 }
 
+// The per-downsampler kernels live in one translation unit per downsampling
+// monoid (ds_tu.hip, built in parallel); this fills their launch record.
+DsLaunch ds_args(otsdb_ctx* c, const Params& P, const BatchDev& B,
+                 const Work& W) {
+  DsLaunch a{};
+  a.st = c->stream;
+  a.P = P;
+  a.B = B;
+  a.SM = W.SM;
+  a.R = W.R;
+  a.err = c->d_err;
+  return a;
+}
+
+// Whether the ordered group fold (fold.hip) runs this query: every
+// downsampled, non-rate query with a monoid aggregator, fill or not.
+bool fold_path(const otsdb_query_spec* spec, const Params& P, bool cells,
+               int mode) {
+  return !cells && !P.ds_sel && !P.rate && !P.run_all &&
+         !is_selection(spec->agg_id) && mode != 2;
+}
+
 // Everything up to dense (group, bucket) results / partials.
-// mode 0: final dense results; mode 1: per-group partials into `gpart/gemit`
+// mode 0: final dense results; mode 1: per-group partials into `gpart/gemit`;
+// mode 2: the cross-rank selection protocol's local part.
 // cells != null: the series come as compacted columns (k_bucketize_cells
 // decodes them inside the downsample; B carries only S)
 otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
@@ -626,6 +588,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   if (rc) return rc;
   const Tiles T = tiles_of(c, G);
   const int64_t nb = P.nb;
+  const bool fold = fold_path(spec, P, cells != nullptr, mode);
 
   // grid trimming for very wide windows (NONE fill only): the rows span only
   // the buckets that hold data
@@ -646,20 +609,33 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       P.gbase += b_lo * P.interval;
       P.nb = b_hi - b_lo + 1;
     }
-    if ((double)S * (double)P.nb > 2.0e10)
-      return fail(OTSDB_E_UNSUPPORTED, "bucket grid too large (%lld x %lld)",
-                  (long long)S, (long long)P.nb);
-  } else if ((double)S * (double)nb > 2.0e10) {
-    return fail(OTSDB_E_UNSUPPORTED, "bucket grid too large (%lld x %lld)",
-                (long long)S, (long long)nb);
   }
   const int64_t NB = P.nb;
+  // bucket indices are 32-bit inside the kernels (SeriesMeta.kf/kl, the
+  // wave-scan keys): a wider grid would wrap silently
+  if (NB > (int64_t)INT32_MAX - 2)
+    return fail(OTSDB_E_UNSUPPORTED, "bucket grid of %lld buckets per series",
+                (long long)NB);
+  // the bucket matrix (series rows) exists only off the fold path
+  if (!fold && (double)S * (double)NB > 2.0e10)
+    return fail(OTSDB_E_UNSUPPORTED, "bucket grid too large (%lld x %lld)",
+                (long long)S, (long long)NB);
+  int64_t WB = 0, NW = 0;
+  if (fold) {
+    if (!with_monoid(spec->agg_id, [&](auto tag) {
+          WB = fold_wb<decltype(tag)>();
+        }))
+      return fail(OTSDB_E_NO_SUCH_ELEMENT, "aggregator %d", spec->agg_id);
+    NW = (NB + WB - 1) / WB;
+  }
 
   // workspace
   const bool sel_large = is_selection(spec->agg_id) && (T.LG > 0 || mode == 2);
   const int64_t n_comb = (mode == 1) ? G : T.MG;
   const bool two_level = T.max_chunks > kCombineL1 &&
                          (double)n_comb * kCombineSlices * NB * 33.0 < 2.0e9;
+  const size_t rows = fold ? 0 : (size_t)S * NB;
+  WinCtx* wc = nullptr;
   auto carve = [&](char* base) {
     Carve cv{base};
     W.SM.lo = cv.take<int64_t>(S);
@@ -671,13 +647,14 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     W.SM.keep = cv.take<uint8_t>(S);
     W.SM.of_has = cv.take<uint8_t>(S);
     W.redo = cv.take<uint8_t>(S);
-    W.R.val = cv.take<double>((size_t)S * NB);
-    W.R.state = cv.take<uint8_t>((size_t)S * NB);
+    W.R.val = cv.take<double>(rows);
+    W.R.state = cv.take<uint8_t>(rows);
     W.partial = cv.take<Packed>((size_t)T.T * NB);
     W.tile_emit = cv.take<uint8_t>((size_t)T.T * NB);
     W.out_val = cv.take<double>((size_t)G * NB);
     W.out_emit = cv.take<uint8_t>((size_t)G * NB);
     W.counts = cv.take<int64_t>(G + 1);
+    if (NW > 1) wc = cv.take<WinCtx>((size_t)S * (NW - 1));
     if (two_level) {
       W.comb = cv.take<Packed>((size_t)n_comb * kCombineSlices * NB);
       W.comb_emit = cv.take<uint8_t>((size_t)n_comb * kCombineSlices * NB);
@@ -700,80 +677,72 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), st));
   if (G * NB > 0 && mode != 1)
     HIP_TRY(hipMemsetAsync(W.out_emit, 0, (size_t)G * NB, st));
-  // the production k_bucketize (ring sink) leaves sentinel rows whose states
-  // k_transform writes; the other kernels store states into a zeroed row
-#ifdef OTSDB_BUCKETIZE_VARIANTS
-  // tuning build: the variant may change between queries of one context, so
-  // an A/B compares kernels over the same workspace placement
-  if (const char* k = getenv("OTSDB_BUCKETIZE_K")) c->bucketize_k = atoi(k);
-#endif
-  P.sentinel = !cells && !P.ds_sel &&
-               bucketize_uses_ring(c->bucketize_k, spec->ds_agg_id);
-  if (S > 0 && NB > 0 && !P.sentinel)
+  // the ring-sink k_bucketize leaves sentinel rows whose states k_transform
+  // writes; the cells and selection downsamplers store states into a
+  // zeroed row
+  P.sentinel = !fold && !cells && !P.ds_sel;
+  if (!fold && S > 0 && NB > 0 && !P.sentinel)
     HIP_TRY(hipMemsetAsync(W.R.state, 0, (size_t)S * NB, st));
   // RateSpan inside k_bucketize (NONE fill; the FillingDownsampler's rate
   // origin and fill points stay with k_transform)
-  static const bool rate_fuse_on = [] {
-    const char* e = getenv("OTSDB_RATE_FUSED");  // A/B knob
-    return !(e && e[0] == '0');
-  }();
-  const bool rate_fused = rate_fuse_on && P.sentinel && P.rate && !P.fill &&
-                          !P.run_all && c->bucketize_k == 0;
-  // zimsum over groups of one chunk each: k_bucketize_group builds the group
-  // rows in LDS (ZIM's 0.0 changes no sum), no series rows, no k_group
-  const bool grp_fused = grp_fused_on() && mode == 0 && !cells && P.sentinel &&
-                         !P.rate && !P.fill && !P.run_all && P.interp == 1 &&
-                         spec->agg_id == OTSDB_AGG_ZIMSUM && T.T > 0 &&
-                         T.MG == 0 && NB <= GRP_NB_MAX &&
-                         c->bucketize_k == 0 && grp_fused_ds(spec->ds_agg_id);
+  const bool rate_fused = P.sentinel && P.rate && !P.fill && !P.run_all;
 
   bool ok = true;
-  if (cells && S > 0 && NB > 0) {
+  DsLaunch a = ds_args(c, P, B, W);
+#ifdef OTSDB_DEBUG_SYNC
+  fprintf(stderr, "[otsdb] pipeline S=%lld NB=%lld fold=%d NW=%lld T=%lld G=%lld\n",
+          (long long)S, (long long)NB, (int)fold, (long long)NW, (long long)T.T,
+          (long long)G);
+#endif
+  OTSDB_DBG(st, "setup");
+  if (fold && S > 0 && NB > 0) {
+    // downsample + contribution + aggregator in one ordered pass
+    ok = with_monoid(spec->ds_agg_id, [&](auto tag) {
+      using M = decltype(tag);
+      {
+        StageTimer tm(c, 3);
+        launch_ds<M>(DS_PREP, a);
+        if (NW > 1) {
+          a.wc = wc;
+          a.NW = NW;
+          a.WB = WB;
+          launch_ds<M>(DS_FOLD_PREP, a);
+        }
+      }
+      StageTimer tm(c, 0);
+      a.n_tiles = T.T;
+      a.tg = T.tg;
+      a.tm0 = T.tm0;
+      a.tm1 = T.tm1;
+      a.single = T.single;
+      a.members = d_members;
+      a.wc = wc;
+      a.NW = NW;
+      a.WB = WB;
+      a.partial = W.partial;
+      a.tile_emit = W.tile_emit;
+      a.out_val = W.out_val;
+      a.out_emit = W.out_emit;
+      a.always_partial = mode == 1;
+      a.agg_id = spec->agg_id;
+      if (T.T > 0) launch_ds<M>(DS_FOLD, a);
+    });
+    if (!ok) return fail(OTSDB_E_UNSUPPORTED, "downsampler %d", spec->ds_agg_id);
+  } else if (cells && S > 0 && NB > 0) {
     // decode fused into the downsample (decode.hip)
     ok = with_monoid(spec->ds_agg_id, [&](auto tag) {
       using M = decltype(tag);
       StageTimer tm(c, 0);
-#ifdef OTSDB_BUCKETIZE_VARIANTS
-      if constexpr (std::is_same<M, MSum<1>>::value) {
-        const char* e = getenv("OTSDB_CELLS_VARIANT");  // tuning A/B
-        const int v = e ? atoi(e) : 0;
-        if (v == 1) {
-          hipLaunchKernelGGL((k_bucketize_cells<M, 6, 4>), dim3(blocks_for(S, 4)),
-                             dim3(256), 0, st, P, *cells, series_row, S, W.SM,
-                             W.R, c->d_err);
-          return;
-        }
-        if (v == 2) {
-          hipLaunchKernelGGL((k_bucketize_cells<M, 4, 4>), dim3(blocks_for(S, 4)),
-                             dim3(256), 0, st, P, *cells, series_row, S, W.SM,
-                             W.R, c->d_err);
-          return;
-        }
-        if (v == 4) {
-          hipLaunchKernelGGL((k_bucketize_cells<M, 6, 1, 1>), dim3(blocks_for(S, 4)),
-                             dim3(256), 0, st, P, *cells, series_row, S, W.SM,
-                             W.R, c->d_err);
-          return;
-        }
-        if (v == 3) {
-          hipLaunchKernelGGL((k_bucketize_cells<M, 6, 2>), dim3(blocks_for(S, 4)),
-                             dim3(256), 0, st, P, *cells, series_row, S, W.SM,
-                             W.R, c->d_err);
-          return;
-        }
-      }
-#endif
-      hipLaunchKernelGGL((k_bucketize_cells<M, 6>), dim3(blocks_for(S, 4)),
-                         dim3(256), 0, st, P, *cells, series_row, S, W.SM, W.R,
-                         c->d_err);
+      a.cells = *cells;
+      a.series_row = series_row;
+      launch_ds<M>(DS_CELLS, a);
     });
     if (!ok) return fail(OTSDB_E_UNSUPPORTED, "downsampler %d", spec->ds_agg_id);
   } else if (S > 0 && NB > 0 && P.ds_sel) {
     // median / percentile downsampling: per-bucket selection
     {
       StageTimer tm(c, 3);
-      hipLaunchKernelGGL(k_prep<MSum<3>>, dim3(blocks_for(S, 256)), dim3(256),
-                         0, st, P, B, W.SM, c->d_err);
+      launch_ds<MSum<3>>(DS_PREP, a);
     }
     StageTimer tm(c, 0);
     hipLaunchKernelGGL(k_ds_select, dim3((unsigned)S), dim3(64), 0, st, P, B,
@@ -783,222 +752,37 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       using M = decltype(tag);
       {
         StageTimer tm(c, 3);
-        hipLaunchKernelGGL(k_prep<M>, dim3(blocks_for(S, 256)), dim3(256), 0,
-                           st, P, B, W.SM, c->d_err);
+        launch_ds<M>(DS_PREP, a);
       }
       StageTimer tm(c, 0);
-      const dim3 grid(blocks_for(S, 4)), blk(256);
-      switch (c->bucketize_k) {
-        case 2:
-          hipLaunchKernelGGL(k_bucketize<M>, grid, blk, 0, st, P, B, W.SM,
-                             W.R);
-          break;
-        case 4:
-          hipLaunchKernelGGL((k_bucketize_k<M, 4>), grid, blk, 0, st, P, B,
-                             W.SM, W.R);
-          break;
-#ifdef OTSDB_BUCKETIZE_VARIANTS
-        // tuning variants (K, prefetch, non-temporal), avg downsampler only
-        case 16: case 41: case 81: case 86: case 88: case 46: case 48: case 99:
-        case 80: case 40: case 97: case 85: case 89: case 49: case 82: case 42: case 96:
-        case 201: case 202: case 203: case 204: case 205: case 206:
-        case 401: case 402: case 403: case 404: case 405: case 406:
-        case 407: case 408: case 409: case 410: case 411: case 412:
-        case 413: case 414: case 415:
-          if constexpr (std::is_same<M, MSum<1>>::value) {
-            const int v = c->bucketize_k;
-            Params P0 = P;  // 80/40: the generic (branchy) fold only
-            P0.narrow = 0;
-            if (v >= 401 && v <= 404) {  // LDS ring sink variants
-              if (v == 401)
-                hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 0, 256>),
-                                   grid, blk, 0, st, P, B, W.SM, W.R);
-              else if (v == 402)
-                hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 0, 512>),
-                                   grid, blk, 0, st, P, B, W.SM, W.R);
-              else if (v == 403)
-                hipLaunchKernelGGL((k_bucketize_k<M, 4, 0, 0, 1, 0, 0, 256>),
-                                   grid, blk, 0, st, P, B, W.SM, W.R);
-              else
-                hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 256>),
-                                   grid, blk, 0, st, P, B, W.SM, W.R);
-            } else if (v == 405) {  // ablation: ring, no row stores
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 2, 1, 256>),
-                                 grid, blk, 0, st, P, B, W.SM, W.R);
-            } else if (v == 406) {  // non-temporal row stores
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 2, 1, 0, 1, 256>),
-                                 grid, blk, 0, st, P, B, W.SM, W.R);
-            } else if (v == 407) {  // 4 KiB flushes
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 1024, 512>),
-                                 grid, blk, 0, st, P, B, W.SM, W.R);
-            } else if (v == 408) {
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 2, 1, 0, 1, 1024, 512>),
-                                 grid, blk, 0, st, P, B, W.SM, W.R);
-            } else if (v == 409) {
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 512, 256>),
-                                 grid, blk, 0, st, P, B, W.SM, W.R);
-            } else if (v == 410) {  // production + next-step prefetch
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 1, 0, 1, 0, 1, 256, 64>),
-                                 grid, blk, 0, st, P, B, W.SM, W.R);
-            } else if (v == 411) {  // prefetch + 4 KiB flushes
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 1, 0, 1, 0, 1, 1024, 512>),
-                                 grid, blk, 0, st, P, B, W.SM, W.R);
-            } else if (v == 413) {  // production, >= 5 waves / SIMD
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 5, 0, 1, 256, 64>),
-                                 grid, blk, 0, st, P, B, W.SM, W.R);
-            } else if (v == 414) {  // production, >= 6 waves / SIMD
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 6, 0, 1, 256, 64>),
-                                 grid, blk, 0, st, P, B, W.SM, W.R);
-            } else if (v == 415) {  // prefetch, >= 4 waves / SIMD
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 1, 0, 4, 0, 1, 256, 64>),
-                                 grid, blk, 0, st, P, B, W.SM, W.R);
-            } else if (v == 412) {  // K=4 + prefetch
-              hipLaunchKernelGGL((k_bucketize_k<M, 4, 1, 0, 1, 0, 1, 256, 64>),
-                                 grid, blk, 0, st, P, B, W.SM, W.R);
-            } else if (v >= 201 && v <= 206) {  // LDS-DMA staged variants
-              auto L = [&](auto kern, int wpb) {
-                hipLaunchKernelGGL(kern, dim3(blocks_for(S, wpb)),
-                                   dim3(64 * wpb), 0, st, P, B, W.SM, W.R);
-              };
-              if (v == 201) L(k_bucketize_lds<M, 4, 4, 4>, 4);
-              else if (v == 202) L(k_bucketize_lds<M, 4, 3, 4>, 4);
-              else if (v == 203) L(k_bucketize_lds<M, 8, 3, 2>, 2);
-              else if (v == 204) L(k_bucketize_lds<M, 4, 4, 2>, 2);
-              else if (v == 205) L(k_bucketize_lds<M, 8, 4, 1>, 1);
-              else L(k_bucketize_lds<M, 2, 8, 4>, 4);
-            } else if (v == 80)
-              hipLaunchKernelGGL((k_bucketize_k<M, 8>), grid, blk, 0, st, P0,
-                                 B, W.SM, W.R);
-            else if (v == 40)
-              hipLaunchKernelGGL((k_bucketize_k<M, 4>), grid, blk, 0, st, P0,
-                                 B, W.SM, W.R);
-            else if (v == 97)  // loads-only at 4 waves/SIMD (LDS-limited)
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 1>), grid, blk,
-                                 36 * 1024, st, P, B, W.SM, W.R);
-            else if (v == 89)
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1>), grid, blk,
-                                 0, st, P, B, W.SM, W.R);
-            else if (v == 49)
-              hipLaunchKernelGGL((k_bucketize_k<M, 4, 0, 0, 1, 0, 1>), grid, blk,
-                                 0, st, P, B, W.SM, W.R);
-            else if (v == 96) {  // timing only: every series writes one row
-              Params P1 = P;
-              P1.nb = 0;
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1>), grid, blk,
-                                 0, st, P1, B, W.SM, W.R);
-            } else if (v == 82)
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 1, 0, 1, 0, 1>), grid, blk,
-                                 0, st, P, B, W.SM, W.R);
-            else if (v == 42)
-              hipLaunchKernelGGL((k_bucketize_k<M, 4, 1, 0, 1, 0, 1>), grid, blk,
-                                 0, st, P, B, W.SM, W.R);
-            else if (v == 85)
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 5>), grid, blk, 0,
-                                 st, P, B, W.SM, W.R);
-            else if (v == 16)
-              hipLaunchKernelGGL((k_bucketize_k<M, 16>), grid, blk, 0, st, P,
-                                 B, W.SM, W.R);
-            else if (v == 41)
-              hipLaunchKernelGGL((k_bucketize_k<M, 4, 1, 0>), grid, blk, 0, st,
-                                 P, B, W.SM, W.R);
-            else if (v == 81)
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 1, 0>), grid, blk, 0, st,
-                                 P, B, W.SM, W.R);
-            else if (v == 99)
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 1>), grid, blk, 0,
-                                 st, P, B, W.SM, W.R);
-            else if (v == 86)
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 6>), grid, blk, 0,
-                                 st, P, B, W.SM, W.R);
-            else if (v == 88)
-              hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 8>), grid, blk, 0,
-                                 st, P, B, W.SM, W.R);
-            else if (v == 46)
-              hipLaunchKernelGGL((k_bucketize_k<M, 4, 0, 0, 6>), grid, blk, 0,
-                                 st, P, B, W.SM, W.R);
-            else
-              hipLaunchKernelGGL((k_bucketize_k<M, 4, 0, 0, 8>), grid, blk, 0,
-                                 st, P, B, W.SM, W.R);
-            break;
-          }
-          [[fallthrough]];
-#endif
-        case 8:  // direct (scattered) row stores
-          hipLaunchKernelGGL((k_bucketize_k<M, 8>), grid, blk, 0, st, P, B,
-                             W.SM, W.R);
-          break;
-        default:  // production: LDS ring sink, sentinel rows, DPP scan
-          if (rate_fused) {
-            // RateSpan fused into the ring flush (1,024-bucket ring: a step
-            // hands its series back only across a gap of ~1,000 buckets);
-            // then the plain kernel for the series handed back
-            Params PF = P;
-            PF.redo = W.redo;
-            // launch-bounded to 128 VGPRs (4 waves / SIMD instead of the
-            // 3 its 140 VGPRs allow; 8 cold spills): C4 bucketize 14.1 ->
-            // 13.3 ms.  OTSDB_RATE_WAVES=1 keeps the unbounded build (A/B)
-            static const int rate_waves = [] {
-              const char* e = getenv("OTSDB_RATE_WAVES");
-              return e ? atoi(e) : 4;
-            }();
-            if (rate_waves == 4)
-              hipLaunchKernelGGL(
-                  (k_bucketize_k<M, 8, 0, 0, 4, 0, 1, 1024, 512, 1>), grid,
-                  blk, 0, st, PF, B, W.SM, W.R);
-            else
-              hipLaunchKernelGGL(
-                  (k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 1024, 512, 1>), grid,
-                  blk, 0, st, PF, B, W.SM, W.R);
-            PF.only_redo = 1;
-            hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 256>), grid,
-                               blk, 0, st, PF, B, W.SM, W.R);
-          } else if (grp_fused) {
-            // zimsum over single-chunk groups: the group row is built in
-            // LDS, no series rows and no k_group pass
-            if constexpr (grp_fused_monoid<M>())
-              hipLaunchKernelGGL((k_bucketize_group<M, 8>), dim3((unsigned)T.T),
-                                 dim3(256), 0, st, P, B, W.SM, T.tg, T.tm0,
-                                 T.tm1, d_members, W.out_val, W.out_emit,
-                                 c->d_err);
-          } else {
-            hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 256>), grid,
-                               blk, 0, st, P, B, W.SM, W.R);
-          }
+      if (rate_fused) {
+        // RateSpan fused into the ring flush (1,024-bucket ring: a step
+        // hands its series back only across a gap of ~1,000 buckets); then
+        // the plain ring kernel for the series handed back
+        a.P.redo = W.redo;
+        launch_ds<M>(DS_RATE, a);
+        a.P.only_redo = 1;
+        launch_ds<M>(DS_RING, a);
+      } else {
+        launch_ds<M>(DS_RING, a);
       }
     });
     if (!ok) return fail(OTSDB_E_UNSUPPORTED, "downsampler %d", spec->ds_agg_id);
   }
-  // constant interpolation, NONE fill, no rate, sentinel rows: k_group
-  // derives each contribution itself and k_transform is not needed
-  const bool direct = P.sentinel && !P.rate && !P.fill && !P.run_all &&
-                      (P.interp == 1 || P.interp == 2 || P.interp == 3) &&
-                      !is_selection(spec->agg_id);
   // percentiles over a FillingDownsampler grid with every group large: the
   // keys transpose applies the fill and counts, no k_transform / k_group
   const bool sel_fused = is_selection(spec->agg_id) && mode == 0 &&
                          P.sentinel && P.fill && !P.rate && !P.run_all &&
-                         T.LG > 0 && T.LG == G && sel_fill_fused_on();
-  if (S > 0 && NB > 0 && !direct && !sel_fused) {
+                         T.LG > 0 && T.LG == G;
+  if (!fold && S > 0 && NB > 0 && !sel_fused) {
     StageTimer tm(c, 1);
-    // rate rows of up to 2,048 buckets stay in registers between the two
-    // RateSpan passes (one row read, one write)
-    auto L = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3(blocks_for(S, 4)), dim3(256), 0, st, P, B,
-                         W.SM, W.R, c->d_err);
-    };
-    static const int64_t reg_max = [] {
-      const char* e = getenv("OTSDB_TRANSFORM_REG_MAX");  // tuning knob
-      return e ? (int64_t)atoll(e) : (int64_t)0;
-    }();
     if (rate_fused) {  // only the series the fused kernel handed back
       P.redo = W.redo;
       P.only_redo = 1;
-      L(k_transform<0>);
-      P.only_redo = 0;
-    } else if (!P.rate || NB > reg_max) L(k_transform<0>);
-    else if (NB <= 512) L(k_transform<8>);
-    else if (NB <= 1024) L(k_transform<16>);
-    else L(k_transform<32>);
+    }
+    hipLaunchKernelGGL(k_transform<0>, dim3(blocks_for(S, 4)), dim3(256), 0,
+                       st, P, B, W.SM, W.R, c->d_err);
+    P.only_redo = 0;
   }
   if (G > 0 && NB > 0) {
     StageTimer tm(c, 2);
@@ -1078,15 +862,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     } else {
       ok = with_monoid(spec->agg_id, [&](auto tag) {
         using M = decltype(tag);
-        if (grp_fused) {
-          // k_bucketize_group wrote the group rows
-        } else if (T.T > 0 && direct)
-          hipLaunchKernelGGL(k_group_direct<M>, dim3(blocks_for(T.T * NB, 256)),
-                             dim3(256), 0, st, P, NB, T.T, T.tg, T.tm0, T.tm1,
-                             T.single, d_members, W.SM, W.R, W.partial,
-                             W.tile_emit, W.out_val, W.out_emit, c->d_err,
-                             mode);
-        else if (T.T > 0)
+        if (!fold && T.T > 0)
           hipLaunchKernelGGL(k_group<M>, dim3(blocks_for(T.T * NB, 256)),
                              dim3(256), 0, st, NB, T.T, T.tg, T.tm0, T.tm1,
                              T.single, d_members, W.R, W.partial, W.tile_emit,
@@ -1522,7 +1298,6 @@ otsdb_status otsdb_ctx_create(int device, otsdb_ctx** out) {
   HIP_TRY(hipSetDevice(device));
   otsdb_ctx* c = new otsdb_ctx();
   c->device = device;
-  if (const char* k = getenv("OTSDB_BUCKETIZE_K")) c->bucketize_k = atoi(k);
   // a blocking stream: ordered with the legacy default stream torch uses,
   // so tensors torch writes are complete before this context reads them
   HIP_TRY(hipStreamCreate(&c->stream));
@@ -1601,12 +1376,10 @@ otsdb_status otsdb_agg_run_device(otsdb_ctx* c, const otsdb_query_spec* spec,
   if (!c || !spec || !b || !out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
-  hipStream_t saved = c->stream;
-  if (hip_stream) c->stream = (hipStream_t)hip_stream;
+  StreamBinding bind(c, hip_stream);
   std::vector<int64_t> goff;
   otsdb_status rc = read_goff(c, b, true, goff);
   if (!rc) rc = run_device_impl(c, spec, b, out, goff);
-  c->stream = saved;
   return rc;
 }
 
@@ -1619,12 +1392,10 @@ otsdb_status otsdb_agg_run_cells_device(otsdb_ctx* c,
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
-  hipStream_t saved = c->stream;
-  if (hip_stream) c->stream = (hipStream_t)hip_stream;
+  StreamBinding bind(c, hip_stream);
   std::vector<int64_t> goff;
   otsdb_status rc = read_goff(c, b, true, goff);
   if (!rc) rc = run_cells_impl(c, spec, cells, b, out, goff);
-  c->stream = saved;
   return rc;
 }
 
@@ -1715,8 +1486,7 @@ otsdb_status otsdb_agg_partials_device(otsdb_ctx* c,
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
-  hipStream_t saved = c->stream;
-  if (hip_stream) c->stream = (hipStream_t)hip_stream;
+  StreamBinding bind(c, hip_stream);
   std::vector<int64_t> goff;
   otsdb_status rc = read_goff(c, b, true, goff);
   Params P;
@@ -1749,7 +1519,6 @@ otsdb_status otsdb_agg_partials_device(otsdb_ctx* c,
                   "Next timestamp is supposed to be strictly greater");
     }
   }
-  c->stream = saved;
   return rc;
 }
 
@@ -1763,8 +1532,7 @@ otsdb_status otsdb_agg_finalize_device(otsdb_ctx* c,
   if (!c || !spec || !out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
-  hipStream_t saved = c->stream;
-  if (hip_stream) c->stream = (hipStream_t)hip_stream;
+  StreamBinding bind(c, hip_stream);
   otsdb_status rc = check_spec(spec);
   Params P;
   if (!rc) rc = make_params(spec, &P, c);
@@ -1801,7 +1569,6 @@ otsdb_status otsdb_agg_finalize_device(otsdb_ctx* c,
       if (!rc) rc = finish(c, G, out);
     }
   }
-  c->stream = saved;
   return rc;
 }
 
@@ -1814,8 +1581,7 @@ otsdb_status otsdb_sel_prepare_device(otsdb_ctx* c, const otsdb_query_spec* spec
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
   c->sel.active = false;
-  hipStream_t saved = c->stream;
-  if (hip_stream) c->stream = (hipStream_t)hip_stream;
+  StreamBinding bind(c, hip_stream);
   std::vector<int64_t> goff;
   otsdb_status rc = read_goff(c, b, true, goff);
   Params P;
@@ -1859,7 +1625,6 @@ otsdb_status otsdb_sel_prepare_device(otsdb_ctx* c, const otsdb_query_spec* spec
       c->sel.median = spec->agg_id == OTSDB_AGG_MEDIAN ? 1 : 0;
     }
   }
-  c->stream = saved;
   return rc;
 }
 
@@ -1911,8 +1676,7 @@ otsdb_status otsdb_sel_finish_device(otsdb_ctx* c, uint32_t* hist_last,
   std::lock_guard<std::mutex> lk(c->mu);
   if (!c->sel.active) return fail(OTSDB_E_ILLEGAL_STATE, "no selection session");
   HIP_TRY(hipSetDevice(c->device));
-  hipStream_t saved = c->stream;
-  if (hip_stream) c->stream = (hipStream_t)hip_stream;
+  StreamBinding bind(c, hip_stream);
   auto& S = c->sel;
   const int64_t G = S.G, NB = S.NB, GB = G * NB;
   const Tiles T = tiles_of(c, G);
@@ -1928,7 +1692,6 @@ otsdb_status otsdb_sel_finish_device(otsdb_ctx* c, uint32_t* hist_last,
   otsdb_status rc = compact(c, S.P, G, S.W.out_val, S.W.out_emit, S.W.counts, out);
   if (!rc) rc = finish(c, G, out);
   S.active = false;
-  c->stream = saved;
   return rc;
 }
 

@@ -149,110 +149,6 @@ __global__ void k_prep(Params P, BatchDev B, SeriesMeta SM, int* err_word) {
 }
 
 // ------------------------------------------------------------------------
-// k_bucketize: Downsampler.next / ValuesInInterval (Downsampler.java:162-228,
-// :461-479) for every series at once.  One wavefront per series; each lane
-// takes 2 consecutive points per step (16-byte loads of ts and value, fully
-// coalesced 1 KiB per wave instruction), computes their epoch-aligned bucket
-// and the wave reduces equal-bucket runs with a segmented inclusive scan.
-// Buckets that close inside the step are written to the series' row; the
-// open one is carried to the next step.
-// ------------------------------------------------------------------------
-template <class M>
-__global__ __launch_bounds__(256) void k_bucketize(Params P, BatchDev B,
-                                                   SeriesMeta SM, Rows R) {
-  const int lane = LANE;
-  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (s >= B.S) return;
-  if (!SM.keep[s]) return;
-  const int64_t lo = SM.lo[s], hi = SM.hi[s];
-  if (lo >= hi) return;
-  const int sf = B.series_float ? (int)B.series_float[s] : 1;
-  double* rowv = R.val + s * P.nb;
-  uint8_t* rows = R.state + s * P.nb;
-
-  int carry_key = INT32_MIN;
-  M carry = M::init();
-
-  const int64_t base0 = lo & ~(int64_t)1;
-  // software pipeline: loads of step k+1 are issued before step k reduces
-  int64_t i0 = base0 + 2 * lane;
-  int64_t ta = 0, tb = 0, va = 0, vb = 0;
-  auto load = [&](int64_t i, int64_t& t0, int64_t& t1, int64_t& v0,
-                  int64_t& v1) {
-    if (i + 1 < hi) {
-      const longlong2 tt = *reinterpret_cast<const longlong2*>(B.ts + i);
-      const longlong2 vv = *reinterpret_cast<const longlong2*>(B.val + i);
-      t0 = tt.x; t1 = tt.y; v0 = vv.x; v1 = vv.y;
-    } else if (i < hi) {
-      t0 = B.ts[i]; v0 = B.val[i];
-    }
-  };
-  load(i0, ta, tb, va, vb);
-  for (int64_t base = base0; base < hi; base += 128) {
-    const int64_t ia = base + 2 * lane, ib = ia + 1;
-    const int64_t cta = ta, ctb = tb, cva = va, cvb = vb;
-    if (base + 128 < hi) load(ia + 128, ta, tb, va, vb);
-
-    const bool inA = ia >= lo && ia < hi;
-    const bool inB = ib >= lo && ib < hi;
-    const int kA = inA ? (int)bucket_of(P, cta) : (ia < lo ? -1 : INT32_MAX);
-    const int kB = inB ? (int)bucket_of(P, ctb) : (ib < lo ? -1 : INT32_MAX);
-    M sA = inA ? M::from(point_value(B, ia, cva, sf)) : M::init();
-    const M sB = inB ? M::from(point_value(B, ib, cvb, sf)) : M::init();
-    if (lane == 0) {
-      if (carry_key == kA) {
-        sA = M::combine(carry, sA);
-      } else if (carry_key >= 0 && carry_key < P.nb) {
-        // the bucket carried from the previous step closed on its boundary
-        int err = 0;
-        rowv[carry_key] = carry.finish(&err);
-        rows[carry_key] = ST_REAL;
-      }
-    }
-    // inclusive segmented scan keyed by each lane's last bucket
-    int key = kB;
-    M st = (kA == kB) ? M::combine(sA, sB) : sB;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int k2 = __shfl_up(key, d);
-      M o = st;
-      o.shfl_up(d);
-      if (lane >= d && k2 == key) st = M::combine(o, st);
-    }
-    // bucket of element A closes inside this lane
-    const int pkey = __shfl_up(key, 1);
-    M pst = st;
-    pst.shfl_up(1);
-    const int next_kA = __shfl_down(kA, 1);
-    int err = 0;
-    if (inA && kA != kB) {
-      const M full = (lane > 0 && pkey == kA) ? M::combine(pst, sA) : sA;
-      rowv[kA] = full.finish(&err);
-      rows[kA] = ST_REAL;
-    }
-    if (inB && lane < 63 && next_kA != kB) {
-      rowv[kB] = st.finish(&err);
-      rows[kB] = ST_REAL;
-    }
-    // carry the bucket still open at lane 63 (broadcast lane 63's state)
-    carry_key = __shfl(key, 63);
-    {
-      Packed p = st.pack();
-      p.x = __shfl(p.x, 63);
-      p.y = __shfl(p.y, 63);
-      p.z = __shfl(p.z, 63);
-      p.w = __shfl(p.w, 63);
-      carry = M::unpack(p);
-    }
-  }
-  if (lane == 0 && carry_key >= 0 && carry_key < P.nb) {
-    int err = 0;
-    rowv[carry_key] = carry.finish(&err);
-    rows[carry_key] = ST_REAL;
-  }
-}
-
-// ------------------------------------------------------------------------
 // k_bucketize_k: the same reduction with K consecutive points per lane
 // (K/2 16-byte loads per column per lane; a step covers 64*K points).  Each
 // lane folds its points sequentially (Java order inside the lane), closes
@@ -318,29 +214,7 @@ struct RowSink {
   int states;      // direct writes also store the state byte (no ring)
   int nostore;     // tuning ablation (ABL == 2): the flush stores nothing
   int nt;          // flush with non-temporal stores
-  // group mode (k_bucketize_group): closed buckets fold straight into the
-  // workgroup's LDS group row instead of the series row
-  double* gsum;    // sum of the non-NaN bucket values
-  uint32_t* gcnt;  // packed: real (bits 0-9), non-NaN (10-19), real strictly
-                   // inside (gkf, gkl) (20-29)
-  int32_t gkf, gkl;
-  int32_t gnb;     // buckets in the group row
-  int* gbad;       // set on a bucket index outside the row
   DEV void put(int k, double v) {
-    if (gsum) {
-      if ((uint32_t)k >= (uint32_t)gnb) {  // never expected: report, no write
-        *gbad = 1;
-        return;
-      }
-      const bool nn = !is_nan(v);
-      if (nn) __hip_atomic_fetch_add(&gsum[k], v, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_fetch_add(&gcnt[k],
-                             1u | (nn ? (1u << 10) : 0u) |
-                                 ((k > gkf && k < gkl) ? (1u << 20) : 0u),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      return;
-    }
     if (states) {
       rowv[k] = v;
       rows[k] = ST_REAL;
@@ -948,190 +822,6 @@ __global__ __launch_bounds__(256, WAVES) void k_bucketize_k(Params P,
 }
 
 // ------------------------------------------------------------------------
-// k_bucketize_group: zimsum over groups of at most one 256-series chunk with
-// NONE fill and no rate (C2's zimsum:5m-avg{host=*}).  One workgroup per
-// group; its wavefronts take the group's series in turn and fold every
-// closed bucket straight into the group's LDS row (f64 sum of the non-NaN
-// values, packed counts) — no series rows, no k_group pass.  ZIM's 0.0 for a
-// series inside a gap (or past its last bucket toward a point past the
-// window) changes no sum (0.0 + x is exact); it only decides "0.0, not NaN"
-// when no real value is a number, so the block counts those contributors
-// with a difference array over [kf + 1, kl) (+ (kl, nb) with a point past
-// the window) minus the real points strictly inside.  The group's series add
-// into a bucket in whatever order their wavefronts reach it (LDS atomics):
-// within 1e-12 relative of the reference's SpanCmp-order sum, not bit for
-// bit (OTSDB_GRP_FUSED=0 keeps the ordered k_group_direct).
-// ------------------------------------------------------------------------
-constexpr int GRP_NB_MAX = 2048;
-
-template <class M, int K>
-__global__ __launch_bounds__(256) void k_bucketize_group(
-    Params P, BatchDev B, SeriesMeta SM, const int64_t* __restrict__ tile_g,
-    const int64_t* __restrict__ tile_m0, const int64_t* __restrict__ tile_m1,
-    const int64_t* __restrict__ members, double* __restrict__ out_val,
-    uint8_t* __restrict__ out_emit, int* err_word) {
-  __shared__ double gsum[GRP_NB_MAX];
-  __shared__ uint32_t gcnt[GRP_NB_MAX];
-  __shared__ int32_t span[GRP_NB_MAX + 1];
-  __shared__ int32_t s_scan[256];
-  __shared__ int s_next, s_bad;
-  const int tid = threadIdx.x, lane = LANE;
-  const int64_t nb = P.nb;
-  const int64_t t = blockIdx.x;
-  for (int b = tid; b <= nb; b += 256) {
-    if (b < nb) {
-      gsum[b] = 0.0;
-      gcnt[b] = 0;
-    }
-    span[b] = 0;
-  }
-  if (tid == 0) s_next = s_bad = 0;
-  __syncthreads();
-  const int64_t m0 = tile_m0[t], m1 = tile_m1[t];
-  for (;;) {
-    int i = 0;
-    if (lane == 0) i = atomicAdd(&s_next, 1);
-    i = __shfl(i, 0);
-    if (m0 + i >= m1) break;
-    const int64_t s = members[m0 + i];
-    const int32_t kf = SM.kf[s], kl = SM.kl[s];
-    if (lane == 0 && SM.keep[s] && kf <= kl) {
-      if (kl > kf + 1) {
-        atomicAdd(&span[kf + 1], 1);
-        atomicAdd(&span[kl], -1);
-      }
-      if (SM.of_has[s] && kl + 1 < nb) atomicAdd(&span[kl + 1], 1);
-    }
-    RowSink S{nullptr, nullptr, nullptr, 0, 1, 1, 0, 0,
-              gsum, gcnt, kf, kl, (int32_t)nb, &s_bad};
-    bucketize_series<M, K, 0, 0, 0, 1, 0, 64, 0>(P, B, SM, S, nullptr, s);
-  }
-  __syncthreads();
-  // span -> number of series contributing ZIM's 0.0 at each bucket (before
-  // subtracting those with a real point there): block prefix sum, 8 buckets
-  // per thread
-  constexpr int PER = GRP_NB_MAX / 256;
-  int32_t loc[PER], acc = 0;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int b = tid * PER + j;
-    acc += b < nb ? span[b] : 0;
-    loc[j] = acc;
-  }
-  s_scan[tid] = acc;
-  __syncthreads();
-  for (int d = 1; d < 256; d <<= 1) {
-    const int32_t y = tid >= d ? s_scan[tid - d] : 0;
-    __syncthreads();
-    s_scan[tid] += y;
-    __syncthreads();
-  }
-  const int32_t excl = tid > 0 ? s_scan[tid - 1] : 0;
-  const int64_t g = tile_g[t];
-  int e = 0;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int b = tid * PER + j;
-    if (b >= nb) break;
-    const uint32_t c = gcnt[b];
-    const int real = (int)(c & 1023), nn = (int)((c >> 10) & 1023);
-    const int cst = excl + loc[j] - (int)(c >> 20);
-    double r = 0.0;
-    if (real) {
-      r = nn ? gsum[b] : (cst > 0 ? 0.0 : qnan());
-      if (is_inf(r)) e |= ERR_INFINITY;
-    }
-    out_val[g * nb + b] = r;
-    out_emit[g * nb + b] = (uint8_t)(real > 0);
-  }
-  if (tid == 0 && s_bad) e |= ERR_INTERNAL;
-  if (e) atomicOr(err_word, e);
-}
-
-// ------------------------------------------------------------------------
-// k_bucketize_lds: k_bucketize_k with the point stream staged by LDS-DMA
-// (global_load_lds_dwordx4: HBM -> LDS with no VGPR destination).  Each
-// wavefront keeps NBUF stages of its series in an LDS ring and issues stage
-// s + NBUF - 1 before it reduces stage s, so NBUF - 1 stages (K*(NBUF-1)
-// wave-instructions of 1 KiB) stay in flight while it computes — latency
-// hiding that no longer costs registers (the register-staged kernel holds
-// its in-flight points in 32 VGPRs at K = 8 and runs at 4 waves/SIMD).
-// A stage is 64*K points of ts and of val, lane-linear: lane l of load j
-// brings points 128j + 2l, 128j + 2l + 1.  vmcnt counts LDS-DMA in issue
-// order with every other vector memory op, so the counted wait below (the
-// glds issued after stage s) covers stage s; younger row stores only make it
-// wait longer.  Steps that reach past the series' end (the last one) read
-// HBM directly, range checked.
-// ------------------------------------------------------------------------
-
-template <class M, int K, int NBUF, int WPB>
-__global__ __launch_bounds__(64 * WPB) void k_bucketize_lds(Params P,
-                                                           BatchDev B,
-                                                           SeriesMeta SM,
-                                                           Rows R) {
-  static_assert(K % 2 == 0 && K * (NBUF - 1) <= 32, "K, NBUF");
-  constexpr int PTS = 64 * K;
-  __shared__ __attribute__((aligned(16))) int64_t ring[WPB][NBUF][2][PTS];
-  const int lane = LANE;
-  const int w = threadIdx.x >> 6;
-  const int64_t s = (int64_t)blockIdx.x * WPB + w;
-  if (s >= B.S) return;
-  if (!SM.keep[s]) return;
-  const int64_t lo = SM.lo[s], hi = SM.hi[s];
-  if (lo >= hi) return;
-  const int sf = B.series_float ? (int)B.series_float[s] : 1;
-  RowSink S{R.val + s * P.nb, R.state + s * P.nb, nullptr, 0, 1, 1, 0, 0};
-  int err = 0;
-  int carry_key = INT32_MIN;
-  M carry = M::init();
-  const int64_t base0 = lo & ~(int64_t)1;
-  // steps whose PTS points all lie before hi come through the LDS ring
-  const int64_t nfull = (hi - base0) / PTS;
-  auto issue = [&](int64_t st) {
-    const int64_t b = base0 + st * PTS;
-    int64_t* slot = &ring[w][st % NBUF][0][0];
-#pragma unroll
-    for (int j = 0; j < K / 2; ++j) {
-      __builtin_amdgcn_global_load_lds(B.ts + b + 128 * j + 2 * lane,
-                                       slot + 128 * j, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(B.val + b + 128 * j + 2 * lane,
-                                       slot + PTS + 128 * j, 16, 0, 0);
-    }
-  };
-  for (int64_t st = 0; st < NBUF - 1 && st < nfull; ++st) issue(st);
-  int64_t st = 0;
-  for (int64_t base = base0; base < hi; base += PTS, ++st) {
-    const int64_t i0 = base + (int64_t)K * lane;
-    int64_t t[K], v[K];
-    if (st < nfull) {
-      if (st + NBUF - 1 < nfull) issue(st + NBUF - 1);
-      const int64_t after = (nfull - 1 - st) < (NBUF - 1) ? (nfull - 1 - st)
-                                                          : (NBUF - 1);
-      wait_vmcnt((int)after * K);
-      const int64_t* slot = &ring[w][st % NBUF][0][0];
-#pragma unroll
-      for (int j = 0; j < K; j += 2) {
-        const ll2_t tt = *reinterpret_cast<const ll2_t*>(slot + K * lane + j);
-        const ll2_t vv = *reinterpret_cast<const ll2_t*>(slot + PTS + K * lane + j);
-        t[j] = tt.x; t[j + 1] = tt.y;
-        v[j] = vv.x; v[j + 1] = vv.y;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        t[j] = (i0 + j < hi) ? B.ts[i0 + j] : 0;
-        v[j] = (i0 + j < hi) ? B.val[i0 + j] : 0;
-      }
-    }
-    reduce_step<M, K, 0>(P, B, sf, lo, hi, base, i0, t, v, S, err,
-                         carry_key, carry);
-  }
-  if (lane == 0 && carry_key >= 0 && carry_key < P.nb) {
-    S.put(carry_key, carry.finish(&err));
-  }
-}
-
-// ------------------------------------------------------------------------
 // interpolation of a series between two of its points, exactly as
 // AggregationIterator.nextDoubleValue (AggregationIterator.java:772-793)
 // ------------------------------------------------------------------------
@@ -1527,78 +1217,6 @@ __global__ __launch_bounds__(256) void k_group(
   }
 }
 
-// k_group over sentinel rows without k_transform, for queries whose
-// interpolation is a constant (ZIM -> 0, MAX / MIN -> +-Double.MAX_VALUE,
-// AggregationIterator.java:782-789), NONE fill and no rate: what the
-// transform would derive per (series, bucket) is local — a real point iff
-// the bucket lies in the series' [kf, kl] and does not hold the absent
-// sentinel; otherwise the constant iff it lies strictly inside (kf, kl) or
-// past kl with a point past the window; else nothing.  Saves the row sweep
-// and the state bytes.
-template <class M>
-__global__ __launch_bounds__(256) void k_group_direct(
-    Params P, int64_t nb, int64_t n_tiles, const int64_t* __restrict__ tile_g,
-    const int64_t* __restrict__ tile_m0, const int64_t* __restrict__ tile_m1,
-    const uint8_t* __restrict__ tile_single, const int64_t* __restrict__ members,
-    SeriesMeta SM, Rows R, Packed* __restrict__ partial,
-    uint8_t* __restrict__ tile_emit, double* __restrict__ out_val,
-    uint8_t* __restrict__ out_emit, int* err_word, int always_partial) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t t = idx / nb;
-  if (t >= n_tiles) return;
-  const int64_t b = idx - t * nb;
-  const int64_t m0 = tile_m0[t], m1 = tile_m1[t];
-  const double cst = P.interp == 1 ? 0.0 : (P.interp == 2 ? kDoubleMax : -kDoubleMax);
-  M st = M::init();
-  int emit = 0;
-  auto one = [&](int64_t sidx, double v, int32_t kf, int32_t kl, uint8_t of) {
-    const bool in = b >= kf && b <= kl;
-    if (in && __double_as_longlong(v) != kAbsentBits) {
-      st.push(v);
-      emit = 1;
-    } else if ((b > kf && b < kl) || (of && kf <= kl && b > kl)) {
-      st.push(cst);
-    }
-  };
-  int64_t m = m0;
-  for (; m + 4 <= m1; m += 4) {
-    int64_t sx[4];
-    double v[4];
-    int32_t kf[4], kl[4];
-    uint8_t of[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) sx[u] = members[m + u];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      kf[u] = SM.kf[sx[u]];
-      kl[u] = SM.kl[sx[u]];
-      of[u] = SM.of_has[sx[u]];
-      v[u] = R.val[sx[u] * nb + b];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) one(sx[u], v[u], kf[u], kl[u], of[u]);
-  }
-  for (; m < m1; ++m) {
-    const int64_t sx = members[m];
-    one(sx, R.val[sx * nb + b], SM.kf[sx], SM.kl[sx], SM.of_has[sx]);
-  }
-  if (tile_single[t] && !always_partial) {
-    const int64_t o = tile_g[t] * nb + b;
-    double r = 0.0;
-    if (emit) {
-      int e = 0;
-      r = st.finish(&e);
-      if (is_inf(r)) e |= ERR_INFINITY;
-      if (e) atomicOr(err_word, e);
-    }
-    out_val[o] = r;
-    out_emit[o] = (uint8_t)emit;
-  } else {
-    partial[t * nb + b] = st.pack();
-    tile_emit[t * nb + b] = (uint8_t)emit;
-  }
-}
-
 // ordered fold of the chunk partials [t0, t1) of bucket b; loads issued in
 // batches of 8 ahead of the dependent combines (the chain is latency-bound)
 template <class M>
@@ -1712,6 +1330,7 @@ __global__ __launch_bounds__(256) void k_finalize_ranks(
   out_emit[o] = (uint8_t)emit;
 }
 
+#ifndef OTSDB_DS_TU
 // ------------------------------------------------------------------------
 // Percentile / median across series (PercentileAgg.runDouble,
 // Aggregators.java:687-706 — LEGACY estimation whatever the name says; and
@@ -1985,5 +1604,7 @@ __global__ __launch_bounds__(256) void k_gen_fill(GenP g, int64_t series0,
     pos += __popcll(m);
   }
 }
+
+#endif  // OTSDB_DS_TU
 
 }  // namespace otsdb

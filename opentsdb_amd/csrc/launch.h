@@ -1,0 +1,99 @@
+// launch.h — the host-side record through which the engine launches the
+// kernels templated on the DOWNSAMPLING monoid.  Those kernels (k_prep, the
+// ring k_bucketize_k, the rate-fused one, k_bucketize_cells, k_fold_prep and
+// the ordered group fold k_fold x every aggregator) are compiled in one
+// translation unit per downsampling monoid (ds_tu.hip), in parallel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dispatch.h"
+#include "kernels.h"
+
+namespace otsdb {
+
+// compacted columns of a query (otsdb_cells, device pointers)
+struct CellsDev {
+  int64_t R;
+  const int64_t* row_series;
+  const int64_t* row_base_s;
+  const int64_t* qual_off;
+  const uint8_t* qual;
+  const int64_t* val_off;
+  const uint8_t* val;
+};
+
+// per (series, inner window boundary j = 1 .. NW-1) of the ordered fold,
+// window start W = j*WB (fold.hip)
+struct WinCtx {
+  int64_t bnd;      // first point with ts >= bucket_ts(W)
+  int64_t prev_ts;  // last real bucket before W: its timestamp (INT64_MIN:
+  double prev_val;  //   none) and downsampled value
+  int64_t next_ts;  // first real bucket at or after W (INT64_MIN: none)
+  double next_val;
+};
+
+// buckets per fold window: the aggregator states of a window live in LDS
+template <class A>
+constexpr int fold_wb() {
+  return sizeof(A) <= 16 ? 2048 : 1024;
+}
+
+enum DsKernel {
+  DS_PREP,       // k_prep: bounds, seek, point past the window
+  DS_RING,       // k_bucketize_k, LDS ring sink -> sentinel series rows
+  DS_RATE,       // k_bucketize_k with RateSpan fused into the ring flush
+  DS_CELLS,      // k_bucketize_cells: decode fused into the downsample
+  DS_FOLD_PREP,  // k_fold_prep: window boundaries of the ordered fold
+  DS_FOLD        // k_fold: downsample + contribution + ordered aggregator
+};
+
+struct DsLaunch {
+  hipStream_t st;
+  Params P;
+  BatchDev B;
+  SeriesMeta SM;
+  Rows R;
+  int* err;
+  // DS_CELLS
+  CellsDev cells;
+  const int64_t* series_row;
+  // DS_FOLD_PREP / DS_FOLD
+  WinCtx* wc;
+  int64_t NW, WB;
+  int64_t n_tiles;
+  const int64_t *tg, *tm0, *tm1;
+  const uint8_t* single;
+  const int64_t* members;
+  Packed* partial;
+  uint8_t* tile_emit;
+  double* out_val;
+  uint8_t* out_emit;
+  int always_partial;
+  int agg_id;
+};
+
+// Debug builds (-DOTSDB_DEBUG_SYNC): every launch reports itself and waits
+// for the device, so a kernel that does not finish names itself.
+#ifdef OTSDB_DEBUG_SYNC
+#include <cstdio>
+#define OTSDB_DBG(st, what)                                              \
+  do {                                                                   \
+    fprintf(stderr, "[otsdb] %s ...\n", what);                          \
+    fflush(stderr);                                                      \
+    hipError_t e_ = hipStreamSynchronize(st);                            \
+    fprintf(stderr, "[otsdb] %s done (%s)\n", what, hipGetErrorString(e_)); \
+    fflush(stderr);                                                      \
+  } while (0)
+#else
+#define OTSDB_DBG(st, what) \
+  do {                      \
+  } while (0)
+#endif
+
+// Defined (explicitly instantiated) in ds_tu.hip for every downsampling
+// monoid; false when the kernel does not exist for (M, agg).
+template <class M>
+bool launch_ds(DsKernel k, const DsLaunch& a);
+
+}  // namespace otsdb

@@ -62,7 +62,7 @@ def test_calendar_group_by(engine, ds, tz, t0, days, cad, agg):  # noqa: F811
     fn = ds.split("-")[1]
     exact = fn in ("min", "max", "count", "last") and agg in (
         "max", "count", "p90")
-    check(engine, spec, b, exact, scale=1e3, where="%s/%s/%s" % (ds, tz, agg))
+    check(engine, spec, b, exact, where="%s/%s/%s" % (ds, tz, agg))
 
 
 @pytest.mark.parametrize("ds,tz", [("1hc-sum", "Asia/Kabul"),
@@ -73,4 +73,4 @@ def test_calendar_rate(engine, ds, tz):  # noqa: F811
     ro = core.RateOptions(True, core.LONG_MAX, 1000000)
     spec = _cal_spec("sum", ds, tz, T_SPRING, T_SPRING + 4 * DAY, True, ro,
                      batch=b)
-    check(engine, spec, b, False, scale=1e3, where=ds)
+    check(engine, spec, b, False, where=ds)

@@ -109,7 +109,7 @@ def test_partials_across_ranks(engines, agg, world):
         ref = pyoracle.group_by(spec, hb)
         got = _partials_emulated(engines, spec, hb, world)
         # downsample avg/sum reduce buckets in a wave tree (1e-12)
-        compare(got, ref, agg in ORDER_FREE and ds == "max", scale=100.0,
+        compare(got, ref, agg in ORDER_FREE and ds == "max",
                 where="w%d/%s/%s/%s" % (world, agg, ds, fill))
 
 
@@ -125,7 +125,7 @@ def test_percentiles_across_ranks(engines, agg, world):
         spec = _spec(agg, ds, fill, end=datasets.T0 + 3600 * 1000)
         ref = pyoracle.group_by(spec, hb)
         got = _select_emulated(engines, spec, hb, world)
-        compare(got, ref, ds == "max", scale=100.0,
+        compare(got, ref, ds == "max",
                 where="w%d/%s/%s" % (world, agg, fill))
 
 
@@ -183,5 +183,5 @@ def test_two_processes_gloo():
     for (agg, ds, fill), groups in zip(QUERIES, out):
         ref = pyoracle.group_by(_spec(agg, ds, fill), hb)
         got = [DataPoints(t, b, i) for t, b, i in groups]
-        compare(got, ref, ds == "max" and agg not in ("sum", "dev"), scale=100.0,
+        compare(got, ref, ds == "max" and agg not in ("sum", "dev"),
                 where="gloo/%s" % agg)
