@@ -60,8 +60,14 @@ namespace otsdb {
   }
 #endif
 
+#ifndef OTSDB_FOLD_FL
+#define OTSDB_FOLD_FL 32
+#endif
+#ifndef OTSDB_FOLD_WAVES
+#define OTSDB_FOLD_WAVES 1
+#endif
 constexpr int FOLD_WIN = 128;  // per-wave ring of closed bucket values
-constexpr int FOLD_FL = 32;    // flush once this many buckets are final
+constexpr int FOLD_FL = OTSDB_FOLD_FL;  // flush once this many buckets are final
 constexpr int32_t kProgDone = INT32_MAX;
 
 // k_fold_prep: one thread per (series, inner boundary).  The boundary
@@ -110,6 +116,7 @@ __global__ __launch_bounds__(256) void k_fold_prep(Params P, BatchDev B,
 }
 
 // One wavefront's view of the fold (wave-uniform except the pointers).
+// Bucket indices are 32-bit (run_pipeline rejects wider grids).
 template <class A>
 struct FoldSink {
   A* st;              // LDS aggregator states of the window
@@ -119,9 +126,9 @@ struct FoldSink {
   int* err;           // device error word (watchdog)
   int32_t mi;         // this member's index in the chunk
   int32_t eff;        // cached effective mark of the predecessors
-  int64_t W0, W1;     // window buckets [W0, W1)
-  int64_t flushed;    // buckets below are pushed or pending
-  int64_t pend;       // start of the pending gap, -1: none
+  int32_t W0, W1;     // window buckets [W0, W1)
+  int32_t flushed;    // buckets below are pushed or pending
+  int32_t pend;       // start of the pending gap, -1: none
   int64_t x0;         // the latest real bucket before `pend`
   double y0;
 };
@@ -129,11 +136,11 @@ struct FoldSink {
 // Waits until every member before this one has pushed all its contributions
 // to buckets < need.
 template <class A>
-DEV void fold_wait(FoldSink<A>& F, int64_t need) {
+DEV void fold_wait(FoldSink<A>& F, int32_t need) {
 #ifdef OTSDB_FOLD_NOWAIT  // debug build: no ordering
   return;
 #endif
-  if ((int64_t)F.eff >= need) return;
+  if (F.eff >= need) return;
   const int lane = LANE;
   for (uint32_t spin = 0;; ++spin) {
     int32_t e = INT32_MAX;  // no unfinished predecessor
@@ -150,7 +157,7 @@ DEV void fold_wait(FoldSink<A>& F, int64_t need) {
       }
     }
     F.eff = e;
-    if ((int64_t)e >= need) break;
+    if (e >= need) break;
     if (spin > (1u << 24)) {
       // watchdog: an invariant is broken (never expected); report it and
       // let the grid drain instead of spinning forever
@@ -164,21 +171,21 @@ DEV void fold_wait(FoldSink<A>& F, int64_t need) {
 }
 
 template <class A>
-DEV void fold_publish(FoldSink<A>& F, int64_t p) {
+DEV void fold_publish(FoldSink<A>& F, int32_t p) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if (LANE == 0)
-    __hip_atomic_store(&F.prog[F.mi], (int32_t)p, __ATOMIC_RELAXED,
+    __hip_atomic_store(&F.prog[F.mi], p, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // pushes the member's interpolated contribution to every bucket of [a, e)
 // (between its real buckets x0 -> x1, or toward the point past the window)
 template <class A>
-DEV void fold_fill_gap(const Params& P, FoldSink<A>& F, int64_t a, int64_t e,
+DEV void fold_fill_gap(const Params& P, FoldSink<A>& F, int32_t a, int32_t e,
                        int64_t x1, double y1) {
   const int lane = LANE;
-  for (int64_t j0 = a; j0 < e; j0 += 64) {
-    const int64_t b = j0 + lane;
+  for (int32_t j0 = a; j0 < e; j0 += 64) {
+    const int32_t b = j0 + lane;
     if (b < e)
       F.st[b - F.W0].push(
           interp_value(P.interp, bucket_ts(P, b), F.x0, F.y0, x1, y1));
@@ -187,19 +194,23 @@ DEV void fold_fill_gap(const Params& P, FoldSink<A>& F, int64_t a, int64_t e,
 
 // Turns the ring's buckets [flushed, limit) (all final) into contributions.
 template <class A>
-DEV void fold_flush(const Params& P, FoldSink<A>& F, int64_t limit) {
+DEV void fold_flush(const Params& P, FoldSink<A>& F, int32_t limit) {
   if (limit <= F.flushed) return;
+#ifdef OTSDB_FOLD_ABL_NOFLUSH  // timing ablation: no contributions
+  F.flushed = limit;
+  return;
+#endif
   fold_wait(F, limit);
   const int lane = LANE;
   const bool fill = P.fill != 0;
   int dbg_n = 0;
-  for (int64_t f = F.flushed; f < limit; f += 64) {
-    FOLD_GUARD(dbg_n, 1 << 26, F.err, "flush loop mi=%d f=%ld limit=%ld\n", F.mi, (long)f, (long)limit)
-    const int64_t b = f + lane;
+  for (int32_t f = F.flushed; f < limit; f += 64) {
+    FOLD_GUARD(dbg_n, 1 << 26, F.err, "flush loop mi=%d f=%d limit=%d\n", F.mi, f, limit)
+    const int32_t b = f + lane;
     const bool inb = b < limit;
     double v = absent_value();
     if (inb) {
-      const int i = (int)(b & (FOLD_WIN - 1));
+      const int i = b & (FOLD_WIN - 1);
       v = F.ring[i];
       F.ring[i] = absent_value();
     }
@@ -252,16 +263,14 @@ DEV int wave_sum(int x) {
   return x;
 }
 
-// t[] element holding point `idx` of the step at `base` (idx wave-uniform)
-template <int K>
-DEV int64_t step_ts(const int64_t* t, int64_t base, int64_t idx) {
-  const int64_t r = idx - base;
-  const int j = (int)(r % K);
-  int64_t x = t[0];
-#pragma unroll
-  for (int q = 1; q < K; ++q)
-    if (q == j) x = t[q];
-  return readlane_l(x, (int)(r / K));
+// timestamp of point `idx` (wave-uniform): a scalar load.  Only steps that
+// are not full (a member's first / last step, a cut) need it; picking the
+// element out of t[] by a computed index would put t[] in scratch memory.
+DEV int64_t point_ts(const BatchDev& B, int64_t idx) { return uni(B.ts[idx]); }
+
+// bucket of a wave-uniform timestamp
+DEV int32_t fold_bucket(const Params& P, int64_t ts) {
+  return P.narrow ? bucket_narrow(P, ts) : (int32_t)bucket_of(P, ts);
 }
 
 // One member's points [pa, pb) of the window (the member's wave).
@@ -269,27 +278,37 @@ DEV int64_t step_ts(const int64_t* t, int64_t base, int64_t idx) {
 // where its contribution goes past its last real bucket of the window
 // (has_next: toward (nx, ny) — the next real bucket, or the point past the
 // grid, AggregationIterator.java:760-775).
+// A member's window context, kept in LDS while its points stream (only the
+// member prologue and the tail read it: not held in SGPRs across the loop).
+struct FoldMember {
+  int64_t pa, pb;    // its points of the window
+  int64_t px, nx;    // previous / next real bucket timestamps
+  double py, ny;
+  int32_t kept, sf, has_prev, has_next;
+};
+
 template <class M, class A, int K>
 DEV void fold_member(const Params& P, const BatchDev& B, FoldSink<A>& F,
-                     int sf, bool kept, int64_t pa, int64_t pb, bool has_prev,
-                     int64_t px, double py, bool has_next, int64_t nx,
-                     double ny) {
+                     const FoldMember* mc) {
   constexpr int PTS = 64 * K;
   const int lane = LANE;
+  const bool kept = uni(mc->kept) != 0;
+  const int sf = uni(mc->sf);
+  const int64_t pa = uni(mc->pa), pb = uni(mc->pb);
   F.flushed = F.W0;
-  F.pend = has_prev ? F.W0 : -1;
-  F.x0 = px;
-  F.y0 = py;
+  F.pend = uni(mc->has_prev) ? F.W0 : -1;
+  F.x0 = uni(mc->px);
+  F.y0 = uni(mc->py);
   if (!kept) return;  // contributes nowhere (SpanGroup.add dropped it)
   RowSink S{nullptr, nullptr, F.ring, FOLD_WIN - 1, 0, 0, 0, 0};
   int err = 0;
   int carry_key = INT32_MIN;
   M carry = M::init();
   int64_t lo_eff = pa;
-  int64_t k_last = -1;
+  int32_t prev_hi = -1;  // bucket of the previous step's last point
   int dbg_n = 0;
   for (int64_t base = pa & ~(int64_t)1; base < pb;) {
-    FOLD_GUARD(dbg_n, 1 << 30, F.err, "stream loop mi=%d base=%ld pa=%ld pb=%ld lo_eff=%ld\n", F.mi, (long)base, (long)pa, (long)pb, (long)lo_eff)
+    FOLD_GUARD(dbg_n, 1 << 30, F.err, "stream loop mi=%d base=%ld pa=%ld pb=%ld\n", F.mi, (long)base, (long)pa, (long)pb)
     const int64_t i0 = base + (int64_t)K * lane;
     int64_t t[K], v[K];
     if (i0 + K <= pb) {
@@ -307,66 +326,112 @@ DEV void fold_member(const Params& P, const BatchDev& B, FoldSink<A>& F,
         v[j] = (i0 + j < pb) ? B.val[i0 + j] : 0;
       }
     }
-    const int64_t first_i = base > lo_eff ? base : lo_eff;
-    const int64_t last_i = (base + PTS < pb ? base + PTS : pb) - 1;
-    const int64_t k_first = bucket_of(P, step_ts<K>(t, base, first_i));
-    const int64_t k_hi = bucket_of(P, step_ts<K>(t, base, last_i));
-    k_last = k_hi;
-    const bool carry_ok = carry_key >= 0 && carry_key < P.nb;
-    if (carry_ok && carry_key < k_first) {
-      // the open bucket ends before this step: close it now
-      if (lane == 0) S.put(carry_key, carry.finish(&err));
-      carry_key = INT32_MIN;
+#ifdef OTSDB_FOLD_ABL_STREAM  // timing ablation: the loads alone
+    {
+      int64_t x = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) x ^= t[j] + v[j];
+      if (x == 42) F.emit[0] = 1;
+      base += PTS;
+      continue;
     }
-    const int64_t k_open = (carry_key >= 0 && carry_key < P.nb) ? carry_key : k_first;
-    if (k_open - F.flushed >= FOLD_FL || k_hi >= F.flushed + FOLD_WIN)
-      fold_flush(P, F, k_open);
+#endif
+    // buckets below the open one are final (every bucket of the previous
+    // step when it ended on a bucket boundary): drain them while this
+    // step's loads are in flight (nothing below reads t[] / v[])
+    const bool carry_ok = carry_key >= 0 && carry_key < P.nb;
+    int32_t limit = carry_ok ? carry_key : prev_hi + 1;
+    if (limit - F.flushed >= FOLD_FL) fold_flush(P, F, limit);
+    const bool full = base >= lo_eff && base + PTS <= pb;
+    const int64_t last_i = (base + PTS < pb ? base + PTS : pb) - 1;
+    // the step's last bucket: lane 63's last point when the step is full
+    const int32_t k_hi = fold_bucket(
+        P, full ? readlane_l(t[K - 1], 63) : point_ts(B, last_i));
     int64_t hi_step = pb;
     if (k_hi >= F.flushed + FOLD_WIN) {
-      // the step spans more buckets than the ring: cut it where the ring
-      // ends (a bucket boundary) and resume from there
-      const int64_t T = bucket_ts(P, F.flushed + FOLD_WIN);
-      int cnt = 0;
+      // ring pressure (a gap or sparse buckets inside the step): close the
+      // open bucket if the step starts past it, drain, and cut the step
+      // where the ring ends (a bucket boundary) if it still does not fit
+      const int64_t first_i = base > lo_eff ? base : lo_eff;
+      const int32_t k_first = fold_bucket(P, point_ts(B, first_i));
+      if (carry_ok && carry_key < k_first) {
+        if (lane == 0) S.put(carry_key, carry.finish(&err));
+        carry_key = INT32_MIN;
+        limit = k_first;
+      } else if (!carry_ok) {
+        limit = k_first;
+      }
+      fold_flush(P, F, limit);
+      if (k_hi >= F.flushed + FOLD_WIN) {
+        const int64_t T = bucket_ts(P, F.flushed + FOLD_WIN);
+        int cnt = 0;
 #pragma unroll
-      for (int j = 0; j < K; ++j)
-        cnt += (i0 + j >= first_i && i0 + j <= last_i && t[j] < T) ? 1 : 0;
-      hi_step = first_i + uni((int32_t)wave_sum(cnt));
+        for (int j = 0; j < K; ++j)
+          cnt += (i0 + j >= first_i && i0 + j <= last_i && t[j] < T) ? 1 : 0;
+        hi_step = first_i + uni((int32_t)wave_sum(cnt));
+      }
     }
+#ifdef OTSDB_FOLD_ABL_NOREDUCE  // timing ablation: stream + ring bookkeeping
+    {
+      int64_t x = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) x ^= t[j] + v[j];
+      if (x == 42) F.emit[0] = 1;
+    }
+#else
     reduce_step<M, K, 1>(P, B, sf, lo_eff, hi_step, base, i0, t, v, S, err,
                          carry_key, carry);
+#endif
     if (hi_step < pb) {
+      prev_hi = fold_bucket(P, point_ts(B, hi_step - 1));
       lo_eff = hi_step;
       base = hi_step & ~(int64_t)1;
     } else {
+      prev_hi = k_hi;
       base += PTS;
     }
   }
   if (carry_key >= 0 && carry_key < P.nb && lane == 0)
     S.put(carry_key, carry.finish(&err));
-  if (k_last >= 0) fold_flush(P, F, k_last + 1);
+  if (prev_hi >= 0) fold_flush(P, F, prev_hi + 1);
   // the window's remaining buckets
   if (P.fill) {
     if (F.flushed < F.W1) {
       fold_wait(F, F.W1);
-      for (int64_t j0 = F.flushed; j0 < F.W1; j0 += 64) {
-        const int64_t b = j0 + lane;
+      for (int32_t j0 = F.flushed; j0 < F.W1; j0 += 64) {
+        const int32_t b = j0 + lane;
         if (b < F.W1) {
           F.st[b - F.W0].push(P.fill_value);
           F.emit[b - F.W0] = 1;
         }
       }
     }
-  } else if (F.pend >= 0 && has_next && F.pend < F.W1) {
+  } else if (F.pend >= 0 && F.pend < F.W1 && uni(mc->has_next)) {
     fold_wait(F, F.W1);
-    fold_fill_gap(P, F, F.pend, F.W1, nx, ny);
+    fold_fill_gap(P, F, F.pend, F.W1, uni(mc->nx), uni(mc->ny));
   }
 }
+
+// the kernel's own arguments the member loop and the finalisation read,
+// stashed in LDS so they do not occupy SGPRs across the point stream
+struct FoldKernel {
+  SeriesMeta SM;
+  const int64_t* members;
+  const WinCtx* wc;
+  const uint8_t* series_float;
+  int64_t nbd, win, m0, m1, g, t;
+  Packed* partial;
+  uint8_t* tile_emit;
+  double* out_val;
+  uint8_t* out_emit;
+  int32_t fin;
+};
 
 // k_fold: see the file header.  Single-chunk groups finish here (out_val /
 // out_emit); chunks of larger groups (and every chunk with always_partial,
 // the multi-GPU partials) leave their window of partials for k_combine.
 template <class M, class A, int K>
-__global__ __launch_bounds__(256) void k_fold(
+__global__ __launch_bounds__(256, OTSDB_FOLD_WAVES) void k_fold(
     Params P, BatchDev B, SeriesMeta SM, int64_t n_tiles,
     const int64_t* __restrict__ tile_g, const int64_t* __restrict__ tile_m0,
     const int64_t* __restrict__ tile_m1,
@@ -381,72 +446,98 @@ __global__ __launch_bounds__(256) void k_fold(
   __shared__ double ring[4][FOLD_WIN];
   __shared__ int32_t prog[256];
   __shared__ int s_next;
+  __shared__ FoldKernel kc;
+  __shared__ FoldMember mc[4];
   const int tid = threadIdx.x, lane = LANE, w = tid >> 6;
-  const int64_t t = (int64_t)blockIdx.x % n_tiles;
-  const int64_t win = (int64_t)blockIdx.x / n_tiles;
   const int64_t nb = P.nb;
-  const int64_t W0 = win * WB, W1 = (W0 + WB < nb) ? W0 + WB : nb;
-  const int nw = (int)(W1 - W0);
+  int32_t W0, W1;
+  {
+    const int64_t t = (int64_t)blockIdx.x % n_tiles;
+    const int64_t win = (int64_t)blockIdx.x / n_tiles;
+    W0 = (int32_t)(win * WB);
+    W1 = (int32_t)((W0 + WB < nb) ? W0 + WB : nb);
+    if (tid == 0) {
+      kc.SM = SM;
+      kc.members = members;
+      kc.wc = wc;
+      kc.series_float = B.series_float;
+      kc.nbd = NW - 1;
+      kc.win = win;
+      kc.m0 = tile_m0[t];
+      kc.m1 = tile_m1[t];
+      kc.g = tile_g[t];
+      kc.t = t;
+      kc.partial = partial;
+      kc.tile_emit = tile_emit;
+      kc.out_val = out_val;
+      kc.out_emit = out_emit;
+      kc.fin = tile_single[t] && !always_partial;
+      s_next = 0;
+    }
+  }
+  const int nw = W1 - W0;
   for (int b = tid; b < nw; b += 256) {
     st[b] = A::init();
     emit[b] = 0;
   }
   prog[tid] = 0;
   for (int i = lane; i < FOLD_WIN; i += 64) ring[w][i] = absent_value();
-  if (tid == 0) s_next = 0;
   __syncthreads();
-  const int64_t m0 = tile_m0[t], m1 = tile_m1[t];
-  const int64_t nbd = NW - 1;
   int dbg_n = 0;
   FoldSink<A> F{st, emit, ring[w], prog, err_word, 0, 0, W0, W1, W0, -1, 0, 0.0};
   for (;;) {
     int i = 0;
     if (lane == 0) i = atomicAdd(&s_next, 1);
     i = __builtin_amdgcn_readlane(i, 0);
-    if (m0 + i >= m1) break;
-    FOLD_GUARD(dbg_n, 1 << 20, err_word, "claim loop i=%d m0=%ld m1=%ld\n", i, (long)m0, (long)m1)
-    const int64_t s = uni(members[m0 + i]);
+    const int64_t m0 = uni(kc.m0);
+    if (m0 + i >= uni(kc.m1)) break;
+    FOLD_GUARD(dbg_n, 1 << 20, err_word, "claim loop i=%d\n", i)
     F.mi = i;
     F.eff = 0;
-    const bool kept = uni((int32_t)SM.keep[s]) != 0;
-    const int64_t lo = kept ? uni(SM.lo[s]) : 0, hi = kept ? uni(SM.hi[s]) : 0;
-    int64_t pa = lo, pb = hi;
-    bool has_prev = false, has_next = false;
-    int64_t px = 0, nx = 0;
-    double py = 0.0, ny = 0.0;
-    if (win > 0) {
-      const WinCtx* c = wc + s * nbd + win - 1;
-      pa = uni(c->bnd);
-      const int64_t pt = uni(c->prev_ts);
-      if (pt != INT64_MIN) {
-        has_prev = true;
-        px = pt;
-        py = uni(c->prev_val);
+    // the member's window context, lane 0 -> LDS
+    if (lane == 0) {
+      const SeriesMeta& sm = kc.SM;
+      const int64_t s = kc.members[m0 + i];
+      const int64_t nbd = kc.nbd, win = kc.win;
+      FoldMember m;
+      m.kept = sm.keep[s] != 0;
+      m.pa = m.kept ? sm.lo[s] : 0;
+      m.pb = m.kept ? sm.hi[s] : 0;
+      m.has_prev = m.has_next = 0;
+      m.px = m.nx = 0;
+      m.py = m.ny = 0.0;
+      if (win > 0) {
+        const WinCtx& c = kc.wc[s * nbd + win - 1];
+        m.pa = c.bnd;
+        if (c.prev_ts != INT64_MIN) {
+          m.has_prev = 1;
+          m.px = c.prev_ts;
+          m.py = c.prev_val;
+        }
       }
-    }
-    if (win < nbd) {
-      const WinCtx* c = wc + s * nbd + win;
-      pb = uni(c->bnd);
-      const int64_t nt = uni(c->next_ts);
-      if (nt != INT64_MIN) {
-        has_next = true;
-        nx = nt;
-        ny = uni(c->next_val);
+      if (win < nbd) {
+        const WinCtx& c = kc.wc[s * nbd + win];
+        m.pb = c.bnd;
+        if (c.next_ts != INT64_MIN) {
+          m.has_next = 1;
+          m.nx = c.next_ts;
+          m.ny = c.next_val;
+        }
       }
+      if (!m.has_next && sm.of_has[s]) {  // toward the point past the grid
+        m.has_next = 1;
+        m.nx = sm.of_ts[s];
+        m.ny = sm.of_val[s];
+      }
+      m.sf = kc.series_float ? (int)kc.series_float[s] : 1;
+      mc[w] = m;
     }
-    if (!has_next && uni((int32_t)SM.of_has[s])) {  // toward the point past the grid
-      has_next = true;
-      nx = uni(SM.of_ts[s]);
-      ny = uni(SM.of_val[s]);
-    }
-    const int sf = B.series_float ? uni((int32_t)B.series_float[s]) : 1;
-    fold_member<M, A, K>(P, B, F, sf, kept, pa, pb, has_prev, px, py,
-                         has_next, nx, ny);
+    fold_member<M, A, K>(P, B, F, &mc[w]);
     fold_publish(F, kProgDone);
   }
   __syncthreads();
-  const bool fin = tile_single[t] && !always_partial;
-  const int64_t g = tile_g[t];
+  const bool fin = kc.fin;
+  const int64_t g = kc.g, t = kc.t;
   int e = 0;
   for (int b = tid; b < nw; b += 256) {
     const int64_t gb = W0 + b;
@@ -456,11 +547,11 @@ __global__ __launch_bounds__(256) void k_fold(
         r = st[b].finish(&e);
         if (is_inf(r)) e |= ERR_INFINITY;
       }
-      out_val[g * nb + gb] = r;
-      out_emit[g * nb + gb] = emit[b];
+      kc.out_val[g * nb + gb] = r;
+      kc.out_emit[g * nb + gb] = emit[b];
     } else {
-      partial[t * nb + gb] = st[b].pack();
-      tile_emit[t * nb + gb] = emit[b];
+      kc.partial[t * nb + gb] = st[b].pack();
+      kc.tile_emit[t * nb + gb] = emit[b];
     }
   }
   if (e) atomicOr(err_word, e);

@@ -12,7 +12,8 @@ import sys
 
 def short(name):
     name = name.split("(")[0]
-    for key in ("k_bucketize_k", "k_bucketize", "k_transform", "k_group",
+    for key in ("k_fold_prep", "k_fold", "k_bucketize_k", "k_bucketize",
+                "k_transform", "k_group",
                 "k_combine", "k_compact", "k_prep", "k_gen"):
         if key in name:
             i = name.find("<")
@@ -30,7 +31,7 @@ def main(root):
                 acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     out = {}
     for k, cs in acc.items():
-        if "bucketize" not in k:
+        if "bucketize" not in k and "k_fold" not in k:
             continue
         d = {c: sum(v) / len(v) for c, v in cs.items()}
         d["dispatches"] = max(len(v) for v in cs.values())
