@@ -4,17 +4,23 @@ group-by query (BASELINE.json metric), on N GPUs of one node.
 One process per GPU.  Each rank owns a contiguous shard of series of the
 synthetic dataset (weak scaling: `--series` per GPU, default the BASELINE
 config's series count), generated straight into HBM.  A step is one
-execution of the query (otsdb_agg_run_device: downsample, interpolate,
-group-by, compact) over the rank's resident batch; for the host-grouped
-workload every group is rank-local, so there is no data-path collective.
+execution of the query over the rank's resident batch: otsdb_agg_run_device
+(downsample, interpolate, group-by, compact) for groups that live on one
+rank; groups spanning ranks add the partial all-gather over RCCL
+(opentsdb_amd/dist.py).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
 
-Prints ONE JSON line (rank 0).
+With --gpus N > 1 outside a torch.distributed launch, this process starts
+the N ranks itself (torch.distributed.run on 127.0.0.1, one rank per GPU)
+without touching the GPU, and relays rank 0's line.  Prints ONE JSON line
+(rank 0).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -23,12 +29,15 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, MI355X_MICROARCH.md
 BYTES_PER_POINT = 16   # int64 ts + 64-bit value, one read
+METRIC = ("data points aggregated/sec (node) for 1m-avg downsample + sum "
+          "group-by, 1/2/4/8 GPU")
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    # BASELINE.md protocol: 3 warm-ups, then 10 timed executions
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--series", type=int, default=0,
@@ -36,8 +45,130 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-decode", action="store_true",
-                    help="skip the secondary compacted-cell decode figure")
+                    help="skip the secondary compacted-cell figures")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the named-query and PCIe-inclusive figures")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / collective rehearsal without the HIP "
+                         "engine (CPU tests): times a gloo all-reduce")
     return ap.parse_args()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(args):
+    """--gpus N > 1 without WORLD_SIZE: run this script as N ranks under
+    torch.distributed.run (one process per GPU) and relay rank 0's JSON
+    line.  The parent never initialises the GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % args.gpus, "--master-addr=127.0.0.1",
+           "--master-port=%d" % _free_port(), os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    for ln in p.stdout.splitlines():
+        if not ln.startswith("{"):
+            print(ln, file=sys.stderr)
+    if lines:
+        print(lines[-1], flush=True)
+    return p.returncode if lines or p.returncode else 1
+
+
+def timed_reps(fn, warm, reps):
+    """median / mean seconds of `reps` synchronous calls after `warm`."""
+    import statistics
+    import torch
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t)
+    return statistics.median(ts), sum(ts) / len(ts)
+
+
+def stage_reader(eng):
+    import ctypes as C
+
+    def read(reset=True):
+        ms = (C.c_double * 8)()
+        n = (C.c_int64 * 8)()
+        eng.lib.otsdb_prof_read(eng.ctx, ms, n, 8, 1 if reset else 0)
+        return [ms[i] / max(n[i], 1) for i in range(5)]
+    return read
+
+
+def named_query_figure(eng, db, config, warm=3, reps=10):
+    """Secondary figure: the metric's own query shape, sum:1m-avg{host=*}
+    (LERP interpolation), over the same resident C2 series — the ordered
+    group fold with 10,080 one-minute buckets in 5 LDS windows."""
+    from opentsdb_amd import core, workload
+    from opentsdb_amd.engine import DeviceResult, run_device
+    import torch
+    c = workload.CONFIGS[config]
+    ds = core.DownsamplingSpecification("1m-avg")
+    q0 = workload.T0_S
+    q1 = q0 + c["days"] * 86400 - 1
+    spec = core.make_spec(core.get_scan_start_time_seconds(q0, ds),
+                          core.get_scan_end_time_seconds(q1, ds),
+                          core.Aggregators.get("sum"), ds, q0 * 1000,
+                          q1 * 1000, normalize=True)
+    sz = eng.plan(spec, db)
+    res = DeviceResult(torch, db.n_groups, int(sz.max_out_points), "cuda")
+    read = stage_reader(eng)
+    eng.lib.otsdb_prof_enable(eng.ctx, 1)
+    read()
+    med, mean = timed_reps(lambda: run_device(eng, spec, db, res), warm, reps)
+    st = read()
+    eng.lib.otsdb_prof_enable(eng.ctx, 0)
+    n = db.n_points_total
+    kf = st[0] / 1e3
+    out = {"query": "sum:1m-avg:sys.cpu.user{host=*} (LERP) over the same "
+                    "%d series x %d d" % (db.n_series, c["days"]),
+           "buckets": int(sz.n_buckets), "value": n / med,
+           "unit": "data points/s", "ms_median": med * 1e3,
+           "ms_mean": mean * 1e3,
+           "stage_ms": {"fold": st[0], "prep": st[3], "compact": st[4]},
+           "kernel": "k_fold (+ k_fold_prep)",
+           "achieved_GBs": BYTES_PER_POINT * n / kf / 1e9 if kf else None}
+    out["frac"] = out["achieved_GBs"] / HBM_PEAK_GBS if kf else None
+    del res
+    return out
+
+
+def pcie_figure(eng, config):
+    """PCIe-inclusive rate (not the headline): otsdb_agg_run from host
+    buffers — H2D of the columns, the query, D2H of the result — at C1 and
+    on a 2,000-series subset of the config."""
+    from opentsdb_amd import workload
+    from oracle import pyoracle  # the data generator only (bench input)
+    out = {}
+    for name, cfg, n in (("C1", "C1", 1000), (config + "_subset", config, 2000)):
+        g = workload.gen_spec(cfg)
+        spec = workload.query_spec(cfg)
+        hb = pyoracle.gen_batch(g, 0, n,
+                                lambda s, c=cfg: workload.group_of(c, s))
+        pts = len(hb.ts)
+        eng.run(spec, hb)  # warm-up (staging allocation)
+        t = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            eng.run(spec, hb)
+        dt = (time.perf_counter() - t) / reps
+        out[name] = {"series": n, "points": pts, "ms": dt * 1e3,
+                     "value": pts / dt, "unit": "data points/s",
+                     "bytes_h2d": 16 * pts}
+        del hb
+    return out
 
 
 def decode_figure(eng, config, n_series, reps=5):
@@ -60,13 +191,8 @@ def decode_figure(eng, config, n_series, reps=5):
            torch.empty(n, dtype=torch.int64, device="cuda"),
            torch.empty(n, dtype=torch.int64, device="cuda"),
            torch.empty(n, dtype=torch.uint8, device="cuda"))
-    workload.decode_cells_device(eng, cells, out=out)  # warm-up
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(reps):
-        workload.decode_cells_device(eng, cells, out=out)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t) / reps
+    dt, _ = timed_reps(lambda: workload.decode_cells_device(eng, cells, out=out),
+                       1, reps)
     cb = cells.n_bytes
     del out
     torch.cuda.empty_cache()
@@ -75,21 +201,13 @@ def decode_figure(eng, config, n_series, reps=5):
     from opentsdb_amd.engine import DeviceResult
     spec = workload.query_spec(config)
     res = DeviceResult(torch, db.n_groups, db.n_groups * 2100, "cuda")
-    workload.run_cells_device(eng, spec, cells, db, res)  # warm-up
+    read = stage_reader(eng)
     eng.lib.otsdb_prof_enable(eng.ctx, 1)
-    eng.lib.otsdb_prof_read(eng.ctx, None, None, 0, 1)
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(reps):
-        workload.run_cells_device(eng, spec, cells, db, res)
-    torch.cuda.synchronize()
-    dq = (time.perf_counter() - t) / reps
-    import ctypes as C
-    ms = (C.c_double * 8)()
-    nn = (C.c_int64 * 8)()
-    eng.lib.otsdb_prof_read(eng.ctx, ms, nn, 8, 1)
+    read()
+    dq, _ = timed_reps(
+        lambda: workload.run_cells_device(eng, spec, cells, db, res), 1, reps)
+    kb = read()[0] / 1e3
     eng.lib.otsdb_prof_enable(eng.ctx, 0)
-    kb = ms[0] / max(nn[0], 1) / 1e3
     del cells, res, db
     torch.cuda.empty_cache()
     return {"kernel": "k_decode (count + scan + write)",
@@ -156,19 +274,59 @@ def cpu_baseline(config, target_s):
     return out
 
 
-_last = None
+def dry_run(args, world, rank):
+    """Launcher rehearsal for CPU tests: the same process-group setup,
+    barrier-bracketed timing and max-over-ranks reduction, with a gloo
+    all-reduce of a small tensor as the step."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    x = torch.ones(1024, dtype=torch.float64)
+    step = (lambda: dist.all_reduce(x)) if world > 1 else (lambda: x.sum())
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    seen = dist.get_world_size() if world > 1 else 1
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit":
+                          "data points/s", "n_gpus": world,
+                          "ranks_seen": seen, "steps": args.steps,
+                          "warmup": args.warmup,
+                          "ms_per_step": el / max(args.steps, 1) * 1e3,
+                          "dry_run": True}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
-    import numpy as np
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (
+            args.gpus, world))
+    if args.dry_run:
+        return dry_run(args, world, rank)
+
     import torch
     from opentsdb_amd import workload
     from opentsdb_amd.engine import DeviceResult, Engine, run_device
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal knobs (a multi-rank run on a one-GPU box): every rank on
     # device 0 and gloo instead of RCCL; the driver's runs use neither
     if os.environ.get("OTSDB_BENCH_SAME_DEVICE"):
@@ -176,6 +334,7 @@ def main():
     backend = os.environ.get("OTSDB_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dist = None
+    ranks_seen = 1
     if world > 1:
         import torch.distributed as dist
         if backend == "nccl":
@@ -183,12 +342,15 @@ def main():
                                     device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        ranks_seen = dist.get_world_size()
+        assert ranks_seen == world == args.gpus
 
     cfg = workload.CONFIGS[args.config]
     n_series = args.series or workload.default_series_per_gpu(args.config)
     # groups that span ranks ({dc=*}, no group-by) take the cross-rank
-    # exchange: partial all-gather, or the histogram protocol for
-    # percentiles (opentsdb_amd/dist.py); host groups stay rank-local
+    # exchange: partial all-gather of the shared groups, or the histogram
+    # protocol for percentiles (opentsdb_amd/dist.py); host groups stay
+    # rank-local
     sharded = world > 1 and workload.spans_ranks(args.config)
     G_glob = (workload.n_groups_global(args.config, n_series * world)
               if sharded else None)
@@ -203,12 +365,12 @@ def main():
     spec = workload.query_spec(args.config)
     sz = eng.plan(spec, db)
     res = DeviceResult(torch, db.n_groups, int(sz.max_out_points), "cuda")
+    last = [None]
     if sharded:
         from opentsdb_amd import dist as odist
 
         def step():
-            global _last
-            _last = odist.run_sharded_any(eng, spec, db, G_glob)
+            last[0] = odist.run_sharded_any(eng, spec, db, G_glob)
     else:
         def step():
             run_device(eng, spec, db, res)
@@ -216,72 +378,83 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    import ctypes as C
+    read = stage_reader(eng)
     eng.lib.otsdb_prof_enable(eng.ctx, 1)
-    eng.lib.otsdb_prof_read(eng.ctx, None, None, 0, 1)  # reset
+    read()  # reset
 
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    per_step = []
     for _ in range(args.steps):
-        step()
+        ts = time.perf_counter()
+        step()  # synchronous: the engine reads the device error word
+        per_step.append(time.perf_counter() - ts)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-
-    ms = (C.c_double * 8)()
-    n = (C.c_int64 * 8)()
-    eng.lib.otsdb_prof_read(eng.ctx, ms, n, 8, 1)
+    stage_ms = read()
     eng.lib.otsdb_prof_enable(eng.ctx, 0)
-    stage_ms = [ms[i] / max(n[i], 1) for i in range(5)]
 
     total_points = n_points * world
-    out_points = int((_last if sharded else res).offsets[-1].item())
+    out_points = (last[0].n_points() if sharded
+                  else int(res.offsets[-1].item()))
+    per_step.sort()
+    med = per_step[len(per_step) // 2] if per_step else 0.0
     if dist:
         dev = "cuda" if backend == "nccl" else "cpu"
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, med], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, med = float(t[0].item()), float(t[1].item())
         tp = torch.tensor([n_points], dtype=torch.int64, device=dev)
         dist.all_reduce(tp)
         total_points = int(tp.item())
     step_s = elapsed / args.steps
     value = total_points / step_s
 
-    # dominant kernel: k_bucketize streams every point once (16 B/point)
+    # dominant kernel: the downsample stage streams every point once
+    # (16 B/point) — k_fold, or k_bucketize_k on the rate path
     kb_s = stage_ms[0] / 1e3
     achieved = BYTES_PER_POINT * n_points / kb_s / 1e9 if kb_s > 0 else None
+    kernel = "k_bucketize_k (rate-fused)" if cfg["rate"] else (
+        "k_bucketize_k + k_keys_transpose/k_seg_select"
+        if cfg["agg"] in ("p99", "p999", "median") else "k_fold")
     # PMC traffic of this exact workload (scripts/gpu_pmc.sh, default size,
-    # one GPU), per k_bucketize launch
+    # one GPU, the shipped kernels), per launch of the dominant kernel
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
     if os.path.exists(pmc) and not args.series and world == 1:
         with open(pmc) as f:
             traffic = json.load(f).get("k_bucketize_hbm_bytes_per_launch")
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.config, args.cpu_seconds)
+    extra = {}
+    if rank == 0 and world == 1:
+        if not args.no_cpu_baseline:
+            extra["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
+        if not args.no_extra and args.config == "C2":
+            extra["named_query"] = named_query_figure(eng, db, args.config)
+        if not args.no_extra:
+            extra["pcie_inclusive"] = pcie_figure(eng, args.config)
 
     n_groups, n_buckets = db.n_groups, int(sz.n_buckets)
-    decode = None
     if world == 1 and not args.no_decode and args.config == "C2":
         del db, res
         torch.cuda.empty_cache()
-        decode = decode_figure(eng, args.config, n_series)
+        extra["decode"] = decode_figure(eng, args.config, n_series)
 
     if rank == 0:
         line = {
-            "metric": "data points aggregated/sec (node) for 1m-avg "
-                      "downsample + sum group-by, 1/2/4/8 GPU",
+            "metric": METRIC,
             "value": value,
             "unit": "data points/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": step_s * 1e3,
+            "ms_per_step_median": med * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -300,8 +473,10 @@ def main():
                 "buckets": n_buckets,
                 "output_points_per_gpu": out_points,
                 "parallelism": "series-sharded dp%d%s" % (
-                    world, " + RCCL exchange" if sharded else ""),
-                "stage_ms": {"bucketize": stage_ms[0],
+                    world, (" + %s exchange of shared groups" % (
+                        "RCCL" if backend == "nccl" else backend))
+                    if sharded else ""),
+                "stage_ms": {"downsample": stage_ms[0],
                              "transform": stage_ms[1],
                              "group": stage_ms[2], "prep": stage_ms[3],
                              "compact": stage_ms[4]},
@@ -309,13 +484,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                # the downsample stage's kernel: k_bucketize_group when the
-                # group-by folds into it (zimsum over one-chunk groups, C2),
-                # k_bucketize_k otherwise
-                "kernel": ("k_bucketize_group" if (
-                    args.config == "C2" and
-                    os.environ.get("OTSDB_GRP_FUSED", "1") != "0")
-                    else "k_bucketize_k"),
+                "kernel": kernel,
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -323,9 +492,11 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": BYTES_PER_POINT * n_points,
             },
-            "cpu_baseline": cpu,
-            "decode": decode,
+            "cpu_baseline": extra.get("cpu_baseline"),
         }
+        for k in ("named_query", "pcie_inclusive", "decode"):
+            if k in extra:
+                line[k] = extra[k]
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -15,22 +15,37 @@ import numpy as np
 PARTIAL_WORDS = 4  # otsdb_partial = 3 doubles + int64
 
 
-def shard_range(n_series, world, rank):
-    """Contiguous, balanced series range of `rank`."""
+def shard_range(n_series, world, rank, offsets=None):
+    """Contiguous series range [a, b) of `rank`.  With the batch's point
+    offsets (CSR, S+1) the ranges are balanced by POINT count:
+    rank r starts at the first series whose first point is at or past
+    r/world of the points; otherwise by series count."""
+    if offsets is not None and n_series > 0:
+        off = np.asarray(offsets, np.int64)
+        total = int(off[-1])
+
+        def cut(r):
+            if r <= 0:
+                return 0
+            if r >= world:
+                return n_series
+            return int(np.searchsorted(off[:-1], (total * r + world - 1) // world,
+                                       side="left"))
+        return cut(rank), max(cut(rank), cut(rank + 1))
     per = n_series // world
     rem = n_series % world
     a = rank * per + min(rank, rem)
     return a, a + per + (1 if rank < rem else 0)
 
 
-def shared_groups(group_of_series, world):
+def shared_groups(group_of_series, world, offsets=None):
     """Global group ids whose members span more than one rank (group ids in
-    ByteMap order, one per series)."""
+    ByteMap order, one per series; shards as shard_range cuts them)."""
     gid = np.asarray(group_of_series, np.int64)
     n = len(gid)
     owner = np.empty(n, np.int64)
     for r in range(world):
-        a, b = shard_range(n, world, r)
+        a, b = shard_range(n, world, r, offsets)
         owner[a:b] = r
     G = int(gid.max()) + 1 if n else 0
     lo = np.full(G, world, np.int64)
@@ -77,39 +92,128 @@ def all_gather_partials(partials, emit, group=None):
     return torch.stack(gp).to(dev), torch.stack(ge).to(dev)
 
 
-def run_sharded(engine, spec, dbatch, n_groups_global, torch_mod=None,
-                group=None):
-    """Runs one query over a rank's DeviceBatch whose group_offsets span all
-    `n_groups_global` groups (empty for groups with no local members).
-    Returns (offsets, ts, val, is_int) device tensors of the final result on
-    every rank."""
-    import ctypes as C
+def classify_groups(group_offsets, group=None, device=None):
+    """(local, shared) global group ids: groups whose members this rank holds
+    alone, and groups with members on more than one rank.  One MIN
+    all-reduce of 2 x G int64 (the lowest rank holding a member, minus the
+    highest)."""
     import torch
     import torch.distributed as dist
-    from . import abi
-    from .engine import DeviceResult
-
-    sz = engine.plan(spec, dbatch)
-    nb = int(sz.n_buckets)
-    GB = n_groups_global * nb
-    dev = dbatch.ts.device
-    parts = torch.zeros((max(GB, 1), PARTIAL_WORDS), dtype=torch.int64,
-                        device=dev)
-    emit = torch.zeros(max(GB, 1), dtype=torch.uint8, device=dev)
-    b = dbatch.as_abi()
-    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    engine._check(engine.lib.otsdb_agg_partials_device(
-        engine.ctx, C.byref(spec), C.byref(b), parts.data_ptr(),
-        emit.data_ptr(), stream))
-    gp, ge = all_gather_partials(parts[:GB], emit[:GB], group)
     world = dist.get_world_size(group)
-    res = DeviceResult(torch, n_groups_global, GB, dev)
-    r = res.as_abi()
-    engine._check(engine.lib.otsdb_agg_finalize_device(
-        engine.ctx, C.byref(spec), n_groups_global, nb, world,
-        gp.contiguous().data_ptr(), ge.contiguous().data_ptr(), C.byref(r),
-        stream))
-    return res
+    rank = dist.get_rank(group)
+    present = np.diff(np.asarray(group_offsets, np.int64)) > 0
+    mm = torch.from_numpy(np.stack([np.where(present, rank, world),
+                                    np.where(present, -rank, 1)]
+                                   ).astype(np.int64))
+    if device is not None:
+        mm = mm.to(device)
+    dist.all_reduce(mm, op=dist.ReduceOp.MIN, group=group)
+    mm = mm.cpu().numpy()
+    shared = mm[0] < -mm[1]
+    return np.nonzero(present & ~shared)[0], np.nonzero(shared)[0]
+
+
+class ShardPlan:
+    """Which of the G global groups this rank holds alone and which span
+    ranks, and the two sub-batches (same series arrays, restricted group
+    CSRs) the step runs: rank-local groups finish with otsdb_agg_run_device,
+    shared groups exchange 32-byte partials.  Built once per batch with one
+    all-reduce of 2 x G ints (min / max rank holding a member)."""
+
+    def __init__(self, engine, spec, dbatch, n_groups_global, group=None):
+        import torch
+        import torch.distributed as dist
+        from .engine import DeviceBatch
+        world = dist.get_world_size(group)
+        goff = dbatch.group_offsets.cpu().numpy()
+        mem = dbatch.group_members.cpu().numpy()
+        dev = dbatch.ts.device
+        self.local, self.shared = classify_groups(
+            goff, group, None if _staged(group) else dev)
+
+        def sub(ids):
+            off = [0]
+            m = []
+            for g in ids:
+                seg = mem[goff[g]:goff[g + 1]]
+                m.extend(seg.tolist())
+                off.append(len(m))
+            return DeviceBatch(dbatch.offsets, dbatch.ts, dbatch.val,
+                               torch.tensor(off, dtype=torch.int64, device=dev),
+                               torch.tensor(m if m else [0], dtype=torch.int64,
+                                            device=dev)[:len(m)],
+                               dbatch.is_float, dbatch.series_float)
+        self.local_batch = sub(self.local)
+        self.shared_batch = sub(self.shared)
+        sz = engine.plan(spec, self.local_batch)
+        self.nb = int(sz.n_buckets)
+        from .engine import DeviceResult
+        self.local_res = DeviceResult(torch, len(self.local),
+                                      int(sz.max_out_points), dev)
+        self.world = world
+
+
+class ShardedResult:
+    """Per-rank result of a sharded query: the groups this rank holds alone
+    (`local_ids`, `local`) and every group spanning ranks (`shared_ids`,
+    `shared`, identical on every rank); DeviceResult tensors."""
+
+    def __init__(self, local_ids, local, shared_ids, shared):
+        self.local_ids, self.local = local_ids, local
+        self.shared_ids, self.shared = shared_ids, shared
+
+    def n_points(self):
+        n = int(self.local.offsets[-1].item()) if len(self.local_ids) else 0
+        if len(self.shared_ids):
+            n += int(self.shared.offsets[-1].item())
+        return n
+
+
+_PLANS = {}
+
+
+def run_sharded(engine, spec, dbatch, n_groups_global, torch_mod=None,
+                group=None, plan=None):
+    """Runs one query over a rank's DeviceBatch whose group_offsets span all
+    `n_groups_global` groups (empty for groups with no local members).
+    Groups held by this rank alone finish locally (no collective); only the
+    groups whose members span ranks exchange partials: 32 B per (shared
+    group, bucket), all-gathered over RCCL and merged in rank (= series)
+    order.  Returns a ShardedResult."""
+    import ctypes as C
+    import torch
+    from .engine import DeviceResult, run_device
+
+    if plan is None:
+        key = (id(dbatch), id(engine), spec.agg_id, spec.ds_interval_ms)
+        plan = _PLANS.get(key)
+        if plan is None:
+            plan = _PLANS[key] = ShardPlan(engine, spec, dbatch,
+                                           n_groups_global, group)
+    if len(plan.local):
+        run_device(engine, spec, plan.local_batch, plan.local_res)
+    shared_res = None
+    n_sh = len(plan.shared)
+    if n_sh:
+        nb = plan.nb
+        GB = n_sh * nb
+        dev = dbatch.ts.device
+        parts = torch.zeros((max(GB, 1), PARTIAL_WORDS), dtype=torch.int64,
+                            device=dev)
+        emit = torch.zeros(max(GB, 1), dtype=torch.uint8, device=dev)
+        b = plan.shared_batch.as_abi()
+        stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        engine._check(engine.lib.otsdb_agg_partials_device(
+            engine.ctx, C.byref(spec), C.byref(b), parts.data_ptr(),
+            emit.data_ptr(), stream))
+        gp, ge = all_gather_partials(parts[:GB], emit[:GB], group)
+        shared_res = DeviceResult(torch, n_sh, GB, dev)
+        r = shared_res.as_abi()
+        engine._check(engine.lib.otsdb_agg_finalize_device(
+            engine.ctx, C.byref(spec), n_sh, nb, plan.world,
+            gp.contiguous().data_ptr(), ge.contiguous().data_ptr(),
+            C.byref(r), stream))
+    return ShardedResult(plan.local, plan.local_res, plan.shared, shared_res)
 
 
 class ShardedSelect:
@@ -189,11 +293,13 @@ def run_sharded_select(engine, spec, dbatch, n_groups_global, group=None):
     return sel.finish()
 
 
-def shard_host_batch(hb, world, rank):
-    """Rank `rank`'s contiguous series range of a HostBatch, with group
-    offsets over every global group (members renumbered locally)."""
+def shard_host_batch(hb, world, rank, by_points=True):
+    """Rank `rank`'s contiguous series range of a HostBatch (balanced by
+    point count), with group offsets over every global group (members
+    renumbered locally)."""
     from .batch import HostBatch
-    a, b = shard_range(hb.n_series, world, rank)
+    a, b = shard_range(hb.n_series, world, rank,
+                       hb.offsets if by_points else None)
     offs = hb.offsets[a:b + 1] - hb.offsets[a]
     p0, p1 = hb.offsets[a], hb.offsets[b]
     g_off = [0]
@@ -231,11 +337,22 @@ def to_device(hb, device="cuda"):
     return db
 
 
+class _SelResult:
+    def __init__(self, res):
+        self.res = res
+        self.offsets = res.offsets
+
+    def n_points(self):
+        return int(self.res.offsets[-1].item())
+
+
 def run_sharded_any(engine, spec, dbatch, n_groups_global, group=None):
     """Dispatch: selection aggregators take the histogram protocol, every
-    other aggregator the partial all-gather."""
+    other aggregator the shared-group partial exchange.  The result has
+    n_points()."""
     if spec.agg_id == 5 or spec.agg_id >= 17:  # median, p*, ep*
-        return run_sharded_select(engine, spec, dbatch, n_groups_global, group)
+        return _SelResult(run_sharded_select(engine, spec, dbatch,
+                                             n_groups_global, group))
     return run_sharded(engine, spec, dbatch, n_groups_global, group=group)
 
 

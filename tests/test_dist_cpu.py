@@ -102,7 +102,7 @@ def test_shard_host_batch_partitions_series_and_groups():
         pts = []
         for r in range(world):
             sh = odist.shard_host_batch(hb, world, r)
-            a, b = odist.shard_range(hb.n_series, world, r)
+            a, b = odist.shard_range(hb.n_series, world, r, hb.offsets)
             assert sh.n_series == b - a and sh.n_groups == hb.n_groups
             assert sh.offsets[0] == 0
             pts.append(sh.ts)
@@ -113,3 +113,79 @@ def test_shard_host_batch_partitions_series_and_groups():
         for g in range(hb.n_groups):
             exp = hb.group_members[hb.group_offsets[g]:hb.group_offsets[g + 1]]
             assert members[g] == exp.tolist()
+
+
+def test_shard_range_balances_points():
+    """Point-balanced contiguous shards: every rank's share of
+    the points is within one series of total / world, and the ranges tile
+    the series."""
+    rng = np.random.default_rng(3)
+    counts = rng.integers(0, 5000, 997)
+    counts[:50] = 40000  # heavy series at the front
+    off = np.concatenate([[0], np.cumsum(counts)])
+    for world in (1, 2, 3, 8):
+        cuts = [odist.shard_range(len(counts), world, r, off)
+                for r in range(world)]
+        assert cuts[0][0] == 0 and cuts[-1][1] == len(counts)
+        for (a0, b0), (a1, b1) in zip(cuts, cuts[1:]):
+            assert b0 == a1
+        share = off[-1] / world
+        for a, b in cuts:
+            assert abs((off[b] - off[a]) - share) <= counts.max()
+
+
+def _classify_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # 6 groups over 2 ranks: 0,1 only on rank 0; 2 on both; 3 only on rank 1;
+    # 4 on both; 5 on nobody
+    counts = {0: [3, 2, 1, 0, 4, 0], 1: [0, 0, 2, 5, 1, 0]}[rank]
+    goff = np.concatenate([[0], np.cumsum(counts)])
+    local, shared = odist.classify_groups(goff)
+    q.put((rank, local.tolist(), shared.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_classify_groups_gloo_world2():
+    """Only groups with members on several ranks are exchanged; the rest
+    finish where they live (no data-path collective for them)."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_classify_worker, args=(r, world, port, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict((r, (l, s)) for r, l, s in (q.get(timeout=120)
+                                          for _ in range(world)))
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got[0] == ([0, 1], [2, 4])
+    assert got[1] == ([3], [2, 4])
+
+
+def test_bench_spawns_ranks_dry_run():
+    """bench.py --gpus 2 outside a torch.distributed launch starts the two
+    ranks itself (torch.distributed.run, 127.0.0.1) and relays rank 0's line;
+    the dry run exercises the launcher, the process group and the
+    max-over-ranks timing without the HIP engine."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"),
+                        "--gpus", "2", "--config", "C3", "--steps", "3",
+                        "--warmup", "1", "--dry-run"], env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["steps"] == 3
