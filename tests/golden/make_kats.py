@@ -718,6 +718,473 @@ for _k, (_t, _iv, _u, _tz, _e) in enumerate(_PI):
         cite="test/utils/TestDateTime.java:548-963")
 
 
+# ------------------------------------------- TsdbQuery over BaseTsdbTest data
+# test/core/BaseTsdbTest.java:612-700 datasets (what tsdb.addPoint writes,
+# read back as one span per series) and the expectation loops of
+# test/core/TestTsdbQueryAggregators.java:44-1117 and
+# test/core/TestTsdbQueryQueries.java:1358-1519, transcribed loop for loop.
+# Every query is setStartTime(1356998400) / setEndTime(1357041600) with no
+# group-by tag: one group {web01, web02} in SpanCmp order.  The SpanGroup
+# window is getScanStart/EndTimeSeconds in ms (pinned by the scan_bounds
+# KATs above): [1356998400, 1357045200] s with or without a 1 s downsample.
+Q_WIN = dict(start_ms=1356998400000, end_ms=1357045200000,
+             query_start_ms=1356998400000, query_end_ms=1357041600000)
+
+
+def _long_seconds(offset):
+    """storeLongTimeSeriesSeconds(false, offset) :612-639"""
+    a, ts = [], 1356998400
+    for i in range(1, 301):
+        ts += 30
+        a.append(L(ts * 1000, i))
+    b, ts = [], (1356998415 if offset else 1356998400)
+    for i in range(300, 0, -1):
+        ts += 30
+        b.append(L(ts * 1000, i))
+    return [a, b]
+
+
+def _f32_steps(start, stop_incl, step, up):
+    """Java `for (float i = start; up ? i <= stop : i > stop; i += step)`
+    (0.25 multiples are exact in float: the loop values are exact doubles)"""
+    out, i = [], start
+    while (i <= stop_incl) if up else (i > stop_incl):
+        out.append(i)
+        i = i + step if up else i - step
+    return out
+
+
+def _float_seconds(offset):
+    """storeFloatTimeSeriesSeconds(false, offset) :679-706 (4-byte floats)"""
+    a, ts = [], 1356998400
+    for v in _f32_steps(1.25, 76.0, 0.25, True):
+        ts += 30
+        a.append(D(ts * 1000, v))
+    b, ts = [], (1356998415 if offset else 1356998400)
+    for v in _f32_steps(75.0, 0.0, 0.25, False):
+        ts += 30
+        b.append(D(ts * 1000, v))
+    return [a, b]
+
+
+def _missing_data():
+    """storeLongTimeSeriesWithMissingData() :649-676"""
+    a, ts = [], 1356998400
+    for i in range(300):
+        if i % 3 != 0:
+            a.append(L(ts * 1000, i + 1))
+        ts += 10
+    b, ts = [], 1356998400
+    for i in range(300, 0, -1):
+        if i % 2 != 0:
+            b.append(L(ts * 1000, i))
+        ts += 10
+    return [b, a][::-1]
+
+
+def _q(name, agg, groups, expect, tol, cite, **extra):
+    spec = dict(Q_WIN, agg=agg)
+    spec.update(extra)
+    add(kind="group_by", name=name, spec=spec, groups=[groups],
+        expect=[expect], tol=tol, cite=cite)
+
+
+TQA = "test/core/TestTsdbQueryAggregators.java"
+
+
+def _seq(n, step, f, ts0=1356998430000):
+    return [f(k, ts0 + step * k) for k in range(n)]
+
+
+# runZimSum :44-61, runZimSumFloat :63-81
+_q("tq_zimsum", "zimsum", _long_seconds(False),
+   _seq(300, 30000, lambda k, t: L(t, 301)), 0, TQA + ":44-61")
+_q("tq_zimsum_float", "zimsum", _float_seconds(False),
+   _seq(300, 30000, lambda k, t: D(t, 76.25)), 0.001, TQA + ":63-81")
+
+
+def _alt(v1, v2, d1, d2, mk, n=600, step=15000):
+    """counter % 2 == 0 -> v1 (then v1 += d1) else v2 (v2 += d2)"""
+    out = []
+    ts = 1356998430000
+    for c in range(n):
+        if c % 2 == 0:
+            out.append(mk(ts, v1))
+            v1 += d1
+        else:
+            out.append(mk(ts, v2))
+            v2 += d2
+        ts += step
+    return out
+
+
+# runZimSumOffset :83-111, runZimSumFloatOffset :113-141
+_q("tq_zimsum_offset", "zimsum", _long_seconds(True),
+   _alt(1, 300, 1, -1, L), 0, TQA + ":83-111")
+_q("tq_zimsum_float_offset", "zimsum", _float_seconds(True),
+   _alt(1.25, 75.0, 0.25, -0.25, D), 0.001, TQA + ":113-141")
+
+
+# runZimSumWithMissingData :143-199
+def _exp_missing():
+    out, i, ts = [], 0, 1356998400000
+    while len(out) < 250:
+        offset = i % 6
+        if offset == 0:
+            ts += 10000
+            i += 1
+            offset += 1
+        if offset in (1, 5):
+            v = 301
+        elif offset in (2, 4):
+            v = i + 1
+        else:
+            v = 300 - i
+        out.append(L(ts, v))
+        ts += 10000
+        i += 1
+    return out
+
+
+_q("tq_zimsum_missing", "zimsum", _missing_data(), _exp_missing(), 0,
+   TQA + ":143-199")
+
+
+def _updown(v, step, dec, turn, reset, mk, n=300, ts_step=30000, cmp="eq"):
+    """the min/max/dev/mimmin/mimmax loops: assert v, step it, and flip the
+    direction when it crosses `turn` (then set it to `reset`)"""
+    out, ts = [], 1356998430000
+    for _ in range(n):
+        out.append(mk(ts, v))
+        ts += ts_step
+        v = v - step if dec else v + step
+        hit = {"eq": v == turn, "gt": v > turn, "lt": v < turn}[cmp]
+        if hit:
+            v = reset
+            dec = not dec
+    return out
+
+
+# runMin :201-232 / runMimMin :718-749 (v == 151 -> 150, decrement)
+for nm, agg, cite in (("min", "min", ":201-232"), ("mimmin", "mimmin", ":718-749")):
+    _q("tq_" + nm, agg, _long_seconds(False),
+       _updown(1, 1, False, 151, 150, L), 0, TQA + cite)
+# runMinFloat :234-265 / runMimMinFloat :782-813 (v > 38 -> 38.0)
+for nm, agg, cite in (("min", "min", ":234-265"), ("mimmin", "mimmin", ":782-813")):
+    _q("tq_%s_float" % nm, agg, _float_seconds(False),
+       _updown(1.25, 0.25, False, 38, 38.0, D, cmp="gt"), 0.0001, TQA + cite)
+# runMax :334-365 / runMimMax :846-877 (v == 150 -> 151, increment)
+for nm, agg, cite in (("max", "max", ":334-365"), ("mimmax", "mimmax", ":846-877")):
+    _q("tq_" + nm, agg, _long_seconds(False),
+       _updown(300, 1, True, 150, 151, L), 0, TQA + cite)
+# runMaxFloat :367-398 / runMimMaxFloat :879-910 (v < 38.25 -> 38.25)
+for nm, agg, cite in (("max", "max", ":367-398"), ("mimmax", "mimmax", ":879-910")):
+    _q("tq_%s_float" % nm, agg, _float_seconds(False),
+       _updown(75.0, 0.25, True, 38.25, 38.25, D, cmp="lt"), 0.001, TQA + cite)
+
+
+# runMinOffset :267-300
+def _exp_min_offset():
+    out, v, ts, counter, dec = [], 1, 1356998430000, 0, False
+    while len(out) < 600:
+        out.append(L(ts, v))
+        ts += 15000
+        if counter % 2 != 0:
+            v = v - 1 if dec else v + 1
+        elif v == 151:
+            v = 150
+            dec = True
+            counter -= 1
+        counter += 1
+    return out
+
+
+_q("tq_min_offset", "min", _long_seconds(True), _exp_min_offset(), 0,
+   TQA + ":267-300")
+
+
+# runMinFloatOffset :302-332
+def _exp_min_float_offset():
+    out, v, ts, dec = [], 1.25, 1356998430000, False
+    for _ in range(600):
+        out.append(D(ts, v))
+        ts += 15000
+        v = v - 0.125 if dec else v + 0.125
+        if v > 38.125:
+            v = 38.125
+            dec = True
+    return out
+
+
+_q("tq_min_float_offset", "min", _float_seconds(True),
+   _exp_min_float_offset(), 0.001, TQA + ":302-332")
+
+
+# runMaxOffset :400-439
+def _exp_max_offset():
+    out, v, ts, counter, dec = [], 1, 1356998430000, 0, True
+    for _ in range(600):
+        out.append(L(ts, v))
+        t = ts
+        ts += 15000
+        if v == 1:
+            v = 300
+        elif t == 1357007400000:
+            v = 1
+        elif counter % 2 == 0:
+            v = v - 1 if dec else v + 1
+        if v == 150:
+            v = 151
+            dec = False
+            counter -= 1
+        counter += 1
+    return out
+
+
+_q("tq_max_offset", "max", _long_seconds(True), _exp_max_offset(), 0,
+   TQA + ":400-439")
+
+
+# runMaxFloatOffset :441-477
+def _exp_max_float_offset():
+    out, v, ts, dec = [], 1.25, 1356998430000, True
+    for _ in range(600):
+        out.append(D(ts, v))
+        t = ts
+        ts += 15000
+        if v == 1.25:
+            v = 75.0
+        elif t == 1357007400000:
+            v = 0.25
+        else:
+            v = v - 0.125 if dec else v + 0.125
+            if v < 38.25:
+                v = 38.25
+                dec = False
+    return out
+
+
+_q("tq_max_float_offset", "max", _float_seconds(True),
+   _exp_max_float_offset(), 0.0001, TQA + ":441-477")
+
+# runAvg :479-497, runAvgFloat :499-517
+_q("tq_avg", "avg", _long_seconds(False),
+   _seq(300, 30000, lambda k, t: L(t, 150)), 0, TQA + ":479-497")
+_q("tq_avg_float", "avg", _float_seconds(False),
+   _seq(300, 30000, lambda k, t: D(t, 38.125)), 0.001, TQA + ":499-517")
+
+
+# runAvgOffset :519-547
+def _exp_avg_offset():
+    out, v, ts = [], 1, 1356998430000
+    for _ in range(600):
+        out.append(L(ts, v))
+        t = ts
+        ts += 15000
+        if v == 1:
+            v = 150
+        elif t == 1357007400000:
+            v = 1
+        elif v == 150:
+            v = 151
+        else:
+            v = 150
+    return out
+
+
+_q("tq_avg_offset", "avg", _long_seconds(True), _exp_avg_offset(), 0,
+   TQA + ":519-547")
+
+
+# runAvgFloatOffset :549-573
+def _exp_avg_float_offset():
+    out, v, ts = [], 1.25, 1356998430000
+    for _ in range(600):
+        out.append(D(ts, v))
+        t = ts
+        ts += 15000
+        if v == 1.25:
+            v = 38.1875
+        elif t == 1357007400000:
+            v = 0.25
+    return out
+
+
+_q("tq_avg_float_offset", "avg", _float_seconds(True),
+   _exp_avg_float_offset(), 0.0001, TQA + ":549-573")
+
+# runDev :575-606 (v < 0 -> 0, increment), runDevFloat :608-639
+_q("tq_dev", "dev", _long_seconds(False),
+   _updown(149, 1, True, 0, 0, L, cmp="lt"), 0, TQA + ":575-606")
+_q("tq_dev_float", "dev", _float_seconds(False),
+   _updown(36.875, 0.25, True, 0.125, 0.125, D, cmp="lt"), 0.001,
+   TQA + ":608-639")
+
+
+# runDevOffset :641-679
+def _exp_dev_offset():
+    out, v, ts, counter, dec = [], 0, 1356998430000, 0, True
+    for _ in range(600):
+        out.append(L(ts, v))
+        t = ts
+        ts += 15000
+        if t == 1356998430000:
+            v = 149
+        elif t == 1357007400000:
+            v = 0
+        elif counter % 2 == 0:
+            v = v - 1 if dec else v + 1
+            if v < 0:
+                v = 0
+                dec = False
+                counter += 1
+        counter += 1
+    return out
+
+
+_q("tq_dev_offset", "dev", _long_seconds(True), _exp_dev_offset(), 0,
+   TQA + ":641-679")
+
+
+# runDevFloatOffset :681-716
+def _exp_dev_float_offset():
+    out, v, ts, dec = [], 0.0, 1356998430000, True
+    for _ in range(600):
+        out.append(D(ts, v))
+        t = ts
+        ts += 15000
+        if t == 1356998430000:
+            v = 36.8125
+        elif t == 1357007400000:
+            v = 0.0
+        else:
+            v = v - 0.125 if dec else v + 0.125
+            if v < 0.0625:
+                v = 0.0625
+                dec = False
+    return out
+
+
+_q("tq_dev_float_offset", "dev", _float_seconds(True),
+   _exp_dev_float_offset(), 0.0001, TQA + ":681-716")
+
+# runMimMinOffset :751-780, runMimMinFloatOffset :815-844,
+# runMimMaxOffset :912-941, runMimMaxFloatOffset :943-972
+_q("tq_mimmin_offset", "mimmin", _long_seconds(True),
+   _alt(1, 300, 1, -1, L), 0, TQA + ":751-780")
+_q("tq_mimmin_float_offset", "mimmin", _float_seconds(True),
+   _alt(1.25, 75.0, 0.25, -0.25, D), 0.001, TQA + ":815-844")
+_q("tq_mimmax_offset", "mimmax", _long_seconds(True),
+   _alt(1, 300, 1, -1, L), 0, TQA + ":912-941")
+_q("tq_mimmax_float_offset", "mimmax", _float_seconds(True),
+   _alt(1.25, 75.0, 0.25, -0.25, D), 0.001, TQA + ":943-972")
+
+# runPercentiles :974-996 + testPercentile :1099-1116 (value 150, delta 150:
+# the test pins the constructor path and the emission grid, not precision)
+for _p in ("p50", "p75", "p90", "p95", "p99", "p999", "ep50r3", "ep75r3",
+           "ep90r3", "ep95r3", "ep99r3", "ep999r3", "ep50r7", "ep75r7",
+           "ep90r7", "ep95r7", "ep99r7", "ep999r7"):
+    _q("tq_pct_" + _p, _p, _long_seconds(True),
+       _seq(600, 15000, lambda k, t: L(t, 150)), 150, TQA + ":974-996,1099-1116")
+
+# runCount :998-1013, runCountFloat :1015-1030 (doubleValue: a long
+# result read as a double), runCountOffset :1032-1053,
+# runCountFloatOffset :1055-1076
+_q("tq_count", "count", _long_seconds(False),
+   _seq(300, 30000, lambda k, t: L(t, 2)), 0, TQA + ":998-1013")
+_q("tq_count_float", "count", _float_seconds(False),
+   _seq(300, 30000, lambda k, t: [t, 2.0, 1]), 0.001, TQA + ":1015-1030")
+_q("tq_count_offset", "count", _long_seconds(True),
+   _seq(600, 15000, lambda k, t: L(t, 1 if k in (0, 599) else 2)), 0,
+   TQA + ":1032-1053")
+_q("tq_count_float_offset", "count", _float_seconds(True),
+   _seq(600, 15000, lambda k, t: [t, 1.0 if k in (0, 599) else 2.0, 1]),
+   0.0001, TQA + ":1055-1076")
+
+TQQ = "test/core/TestTsdbQueryQueries.java"
+
+
+# runInterpolationSeconds :1357-1392 (LERP, long): the offset dataset
+def _exp_interp_seconds():
+    out, v, ts = [], 1, 1356998430000
+    for _ in range(600):
+        out.append(L(ts, v))
+        t = ts
+        ts += 15000
+        if t == 1357007400000:
+            v = 1
+        elif v == 1 or v == 302:
+            v = 301
+        else:
+            v = 302
+    return out
+
+
+_q("tq_interp_seconds", "sum", _long_seconds(True), _exp_interp_seconds(), 0,
+   TQQ + ":1357-1392")
+
+
+# runInterpolationMs :1394-1429
+def _ms_series(t0, step, vals):
+    out, t = [], t0
+    for v in vals:
+        t += step
+        out.append(L(t, v))
+    return out
+
+
+def _exp_interp_ms():
+    out, v, ts = [], 1, 1356998400500
+    for _ in range(600):
+        out.append(L(ts, v))
+        t = ts
+        ts += 250
+        if t == 1356998550000:
+            v = 1
+        elif v == 1 or v == 302:
+            v = 301
+        else:
+            v = 302
+    return out
+
+
+_q("tq_interp_ms", "sum",
+   [_ms_series(1356998400000, 500, range(1, 301)),
+    _ms_series(1356998400250, 500, range(300, 0, -1))],
+   _exp_interp_ms(), 0, TQQ + ":1394-1429")
+
+
+# runInterpolationMsDownsampled :1431-1519 (1 s sum downsample, LERP of
+# the downsampled points, tolerance 1e-7)
+def _ds_ts1():
+    out, t = [], 1356998400000
+    for i in range(1, 121):
+        t += 500 if i <= 100 else 5000
+        out.append(L(t, i))
+    return out
+
+
+def _exp_interp_ms_ds():
+    out = []
+    ts = 1356998400000
+    for i in range(151):
+        if i == 0:
+            v = 301.0
+        elif i < 50:
+            v = 602.0
+        else:
+            v = 701 + (i - 50) * 0.2 - i * 4
+        out.append(D(ts, v))
+        ts += 1000
+    return out
+
+
+_q("tq_interp_ms_downsampled", "sum",
+   [_ds_ts1(), _ms_series(1356998400250, 500, range(300, 0, -1))],
+   _exp_interp_ms_ds(), 0.0000001, TQQ + ":1431-1519",
+   ds_interval_ms=1000, ds_agg="sum")
+
+
 def _enc(x):
     if isinstance(x, float):
         if math.isnan(x):
