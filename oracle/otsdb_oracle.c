@@ -1439,3 +1439,409 @@ int64_t or_gen_fill(const otsdb_gen_spec* g, int64_t s, int64_t* ts,
   }
   return c;
 }
+
+/* records an exception without unwinding (the compaction restatement
+ * returns through its own cleanup) */
+static void jraise(exc_t* e, int code, const char* fmt, ...) {
+  e->code = code;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(e->msg, sizeof(e->msg), fmt, ap);
+  va_end(ap);
+}
+
+/* ======================================================================
+ * Query-time compaction of one storage row — CompactionQueue.Compaction
+ * .compact (CompactionQueue.java:340-616) as TsdbQuery's scanner calls it
+ * (tsdb.compact(row), TSDB.java:2232-2235, SaltScanner.java:835+):
+ * buildHeapProcessAnnotations (:435-489) turns every column into a
+ * ColumnDatapointIterator (single-value 2-byte cells get the legacy fix-ups
+ * of ColumnDatapointIterator.checkForFixup, :73-87 / Internal.java:535-591;
+ * append columns 0x05 are parsed, sorted and de-duplicated first,
+ * AppendDataPoints.parseKeyValue :118-235; annotations / histograms / other
+ * odd qualifiers are skipped), then defaultMergeDataPoints (:549-584) pops
+ * the iterators from a PriorityQueue ordered by (time offset, newest column
+ * first) — restated here as "pick the least head each step" — keeping the
+ * first of equal offsets (differing values throw unless fix_duplicates), and
+ * buildCompactedColumn (:594-616) appends the meta byte to multi-value
+ * columns.  Columns with equal HBase timestamps tie in Java's heap in an
+ * unspecified order; here the later column wins the tie.
+ * ====================================================================== */
+typedef struct {
+  uint8_t* q;      /* qualifier bytes (owned copy: fix-ups / appends) */
+  int64_t qlen;
+  uint8_t* v;      /* value bytes (owned copy) */
+  int64_t vlen;
+  int64_t ts;      /* HBase cell timestamp */
+  int64_t idx;     /* column index (tie-break) */
+  int64_t qo, vo;  /* cursor */
+  int32_t cur_off; /* current point: offset ms, qualifier / value length */
+  int32_t cur_ql, cur_vl, is_ms;
+} cdi_t;
+
+static int32_t q_offset_ms(const uint8_t* q, int64_t o) {
+  if ((q[o] & 0xF0) == 0xF0) {
+    const uint32_t x = ((uint32_t)q[o] << 24) | ((uint32_t)q[o + 1] << 16) |
+                       ((uint32_t)q[o + 2] << 8) | q[o + 3];
+    return (int32_t)((x & 0x0FFFFFC0u) >> 6);
+  }
+  return (int32_t)((((uint32_t)q[o] << 8) | q[o + 1]) >> 4) * 1000;
+}
+static int q_len(const uint8_t* q, int64_t o) { return (q[o] & 0xF0) == 0xF0 ? 4 : 2; }
+static int q_vlen(const uint8_t* q, int64_t o) {
+  return (q[o + (q_len(q, o) - 1)] & 0x7) + 1;
+}
+
+/* ColumnDatapointIterator.update (:172-186) */
+static int cdi_update(cdi_t* c) {
+  if (c->qo >= c->qlen || c->vo >= c->vlen) return 0;
+  if (c->qo + q_len(c->q, c->qo) > c->qlen) return 0;
+  c->is_ms = (c->q[c->qo] & 0xF0) == 0xF0;
+  c->cur_ql = c->is_ms ? 4 : 2;
+  c->cur_off = q_offset_ms(c->q, c->qo);
+  c->cur_vl = q_vlen(c->q, c->qo);
+  return 1;
+}
+
+/* AppendDataPoints.parseKeyValue: cells keyed by offset, the later of equal
+ * offsets wins (TreeMap.put), emitted in offset order */
+static int append_parse(const uint8_t* v, int64_t vlen, cdi_t* c, exc_t* e) {
+  int64_t n = 0, i = 0;
+  while (i < vlen) {  /* count + validate */
+    const int ql = q_len(v, i);
+    if (i + ql > vlen) goto corrupt;
+    const int vl = q_vlen(v, i);
+    i += ql + vl;
+    if (i > vlen) goto corrupt;
+    n++;
+  }
+  {
+    int64_t* pos = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n ? n : 1));
+    int32_t* off = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n ? n : 1));
+    int64_t k = 0;
+    for (i = 0; i < vlen;) {
+      pos[k] = i;
+      off[k] = q_offset_ms(v, i);
+      i += q_len(v, i) + q_vlen(v, i);
+      k++;
+    }
+    /* keep the last occurrence of each offset; order by offset */
+    int64_t m = 0;
+    for (int64_t a = 0; a < n; a++) {
+      int dup = 0;
+      for (int64_t b = a + 1; b < n; b++)
+        if (off[b] == off[a]) dup = 1;
+      if (!dup) { pos[m] = pos[a]; off[m] = off[a]; m++; }
+    }
+    for (int64_t a = 1; a < m; a++) { /* insertion sort by offset */
+      int64_t p = pos[a];
+      int32_t o = off[a];
+      int64_t b = a - 1;
+      while (b >= 0 && off[b] > o) { pos[b + 1] = pos[b]; off[b + 1] = off[b]; b--; }
+      pos[b + 1] = p;
+      off[b + 1] = o;
+    }
+    int64_t qb = 0, vb = 0;
+    for (int64_t a = 0; a < m; a++) {
+      qb += q_len(v, pos[a]);
+      vb += q_vlen(v, pos[a]);
+    }
+    c->q = (uint8_t*)malloc((size_t)(qb ? qb : 1));
+    c->v = (uint8_t*)malloc((size_t)(vb ? vb : 1));
+    c->qlen = qb;
+    c->vlen = vb;
+    qb = vb = 0;
+    for (int64_t a = 0; a < m; a++) {
+      const int ql = q_len(v, pos[a]), vl = q_vlen(v, pos[a]);
+      memcpy(c->q + qb, v + pos[a], (size_t)ql);
+      memcpy(c->v + vb, v + pos[a] + ql, (size_t)vl);
+      qb += ql;
+      vb += vl;
+    }
+    free(pos);
+    free(off);
+  }
+  return 1;
+corrupt:
+  jraise(e, OTSDB_E_ILLEGAL_DATA,
+         "Corrupted value: couldn't break down into individual values");
+  return 0;
+}
+
+int or_compact_row(int64_t ncol, const int64_t* col_qoff, const uint8_t* qual,
+                   const int64_t* col_voff, const uint8_t* val,
+                   const int64_t* col_ts, int fix_duplicates,
+                   uint8_t* out_q, int64_t qcap, uint8_t* out_v, int64_t vcap,
+                   int64_t* out_qlen, int64_t* out_vlen, char* err,
+                   int errlen) {
+  exc_t e = {0};
+  cdi_t* it = (cdi_t*)calloc((size_t)(ncol ? ncol : 1), sizeof(cdi_t));
+  int64_t nit = 0;
+  int rc = OTSDB_OK;
+  *out_qlen = *out_vlen = 0;
+  for (int64_t c = 0; c < ncol && !e.code; c++) {
+    const uint8_t* q = qual + col_qoff[c];
+    const int64_t ql = col_qoff[c + 1] - col_qoff[c];
+    const uint8_t* v = val + col_voff[c];
+    const int64_t vl = col_voff[c + 1] - col_voff[c];
+    cdi_t x;
+    memset(&x, 0, sizeof(x));
+    x.ts = col_ts ? col_ts[c] : c;
+    x.idx = c;
+    if (ql == 0) continue;
+    if (ql & 1) {
+      if (q[0] == 0x05) {  /* append column */
+        if (ql != 3) {
+          jraise(&e, OTSDB_E_ILLEGAL_ARGUMENT,
+                 "Can not parse cell, it is not an appended cell");
+          break;
+        }
+        if (!append_parse(v, vl, &x, &e)) break;
+      } else {
+        continue;  /* annotation (0x01), histogram (0x06), unknown */
+      }
+    } else {
+      x.q = (uint8_t*)malloc((size_t)ql);
+      memcpy(x.q, q, (size_t)ql);
+      x.qlen = ql;
+      x.v = (uint8_t*)malloc((size_t)(vl ? vl : 1));
+      memcpy(x.v, v, (size_t)vl);
+      x.vlen = vl;
+    }
+    if (x.qlen == 2) {  /* checkForFixup */
+      const uint8_t f = x.q[1];
+      if ((f & 0x8) && (f & 0x7) == 0x3 && x.vlen == 8) {
+        if (x.v[0] || x.v[1] || x.v[2] || x.v[3]) {
+          jraise(&e, OTSDB_E_ILLEGAL_DATA, "Corrupted floating point value");
+          free(x.q);
+          free(x.v);
+          break;
+        }
+        memmove(x.v, x.v + 4, 4);
+        x.vlen = 4;
+      }
+      x.q[1] = (uint8_t)((f & ~0x7) | ((x.vlen - 1) & 0xFF));
+    }
+    if (cdi_update(&x)) it[nit++] = x;
+    else { free(x.q); free(x.v); }
+  }
+  int ms_in = 0, s_in = 0;
+  int64_t nseg = 0, qo = 0, vo = 0, last_vo = 0, last_vl = 0;
+  int32_t prev = -1;
+  while (!e.code) {
+    int64_t best = -1;
+    for (int64_t k = 0; k < nit; k++) {
+      if (it[k].qo >= it[k].qlen) continue;
+      if (best < 0 || it[k].cur_off < it[best].cur_off ||
+          (it[k].cur_off == it[best].cur_off &&
+           (it[k].ts > it[best].ts ||
+            (it[k].ts == it[best].ts && it[k].idx > it[best].idx))))
+        best = k;
+    }
+    if (best < 0) break;
+    cdi_t* c = &it[best];
+    if (c->vo + c->cur_vl > c->vlen) {
+      jraise(&e, OTSDB_E_ILLEGAL_DATA,
+             "Corrupted value: couldn't break down into individual values");
+      break;
+    }
+    if (c->cur_off == prev) {
+      const int differ = c->cur_vl != last_vl ||
+                         memcmp(out_v + last_vo, c->v + c->vo, (size_t)last_vl);
+      if (differ && !fix_duplicates) {
+        jraise(&e, OTSDB_E_ILLEGAL_DATA, "Duplicate timestamp, ms_offset=%d",
+               (int)prev);
+        break;
+      }
+    } else {
+      prev = c->cur_off;
+      if (qo + c->cur_ql > qcap || vo + c->cur_vl + 1 > vcap) {
+        jraise(&e, OTSDB_E_CAPACITY, "compaction output capacity");
+        break;
+      }
+      memcpy(out_q + qo, c->q + c->qo, (size_t)c->cur_ql);
+      memcpy(out_v + vo, c->v + c->vo, (size_t)c->cur_vl);
+      last_vo = vo;
+      last_vl = c->cur_vl;
+      qo += c->cur_ql;
+      vo += c->cur_vl;
+      nseg++;
+      if (c->is_ms) ms_in = 1; else s_in = 1;
+    }
+    c->qo += c->cur_ql;  /* advance */
+    c->vo += c->cur_vl;
+    if (!cdi_update(c)) c->qo = c->qlen;
+  }
+  if (!e.code && nseg > 1) out_v[vo++] = (uint8_t)((ms_in && s_in) ? 1 : 0);
+  for (int64_t k = 0; k < nit; k++) { free(it[k].q); free(it[k].v); }
+  free(it);
+  if (e.code) {
+    set_err(err, errlen, &e);
+    return e.code;
+  }
+  *out_qlen = qo;
+  *out_vlen = vo;
+  return rc;
+}
+
+/* ======================================================================
+ * Span assembly of one series' compacted rows in arrival order — Span.addRow
+ * (Span.java:177-220: a row whose first point is not after the last RowSeq's
+ * last point merges into the first RowSeq with the same key, else it starts
+ * a RowSeq), RowSeq.addRow (RowSeq.java:91-222: two-pointer merge by offset,
+ * the incoming duplicate dropped, meta byte = OR of both mixed bits) and
+ * checkRowOrder (:387-392: stable sort by base time).  RowSeq.size /
+ * timestamp(i) read the meta bit from the LAST value byte exactly as the
+ * reference does (:338-420).
+ * ====================================================================== */
+typedef struct {
+  int64_t base;
+  uint8_t* q;
+  int64_t qlen;
+  uint8_t* v;
+  int64_t vlen;
+} rseq_t;
+
+static int64_t rseq_size(const rseq_t* r) {
+  if (r->vlen > 0 && (r->v[r->vlen - 1] & 1)) {
+    int64_t n = 0;
+    for (int64_t i = 0; i < r->qlen; i += 2) {
+      if ((r->q[i] & 0xF0) == 0xF0) i += 2;
+      n++;
+    }
+    return n;
+  }
+  if (r->qlen > 0 && (r->q[0] & 0xF0) == 0xF0) return r->qlen / 4;
+  return r->qlen / 2;
+}
+
+static int64_t rseq_ts(const rseq_t* r, int64_t i) {
+  int64_t o = -1;
+  if (r->vlen > 0 && (r->v[r->vlen - 1] & 1)) {
+    int64_t k = 0;
+    for (int64_t idx = 0; idx < r->qlen; idx += 2) {
+      if (k == i) { o = idx; break; }
+      if ((r->q[idx] & 0xF0) == 0xF0) idx += 2;
+      k++;
+    }
+  } else if (r->qlen > 0 && (r->q[0] & 0xF0) == 0xF0) {
+    o = i * 4;
+  } else {
+    o = i * 2;
+  }
+  if (o < 0 || o + 2 > r->qlen) return INT64_MIN;
+  if ((r->q[o] & 0xF0) == 0xF0)
+    return r->base * 1000 + q_offset_ms(r->q, o);
+  return (r->base + (q_offset_ms(r->q, o) / 1000)) * 1000;
+}
+
+static void rseq_add(rseq_t* L, const uint8_t* rq, int64_t rql,
+                     const uint8_t* rv, int64_t rvl) {
+  uint8_t* mq = (uint8_t*)malloc((size_t)(L->qlen + rql + 1));
+  uint8_t* mv = (uint8_t*)malloc((size_t)(L->vlen + rvl + 2));
+  int64_t ri = 0, li = 0, mi = 0, rvi = 0, lvi = 0, mvi = 0;
+  while (ri < rql || li < L->qlen) {
+    if (ri >= rql) {
+      const int vl = q_vlen(L->q, li), ql = q_len(L->q, li);
+      memcpy(mv + mvi, L->v + lvi, (size_t)vl); lvi += vl; mvi += vl;
+      memcpy(mq + mi, L->q + li, (size_t)ql); li += ql; mi += ql;
+      continue;
+    }
+    if (li >= L->qlen) {
+      const int vl = q_vlen(rq, ri), ql = q_len(rq, ri);
+      memcpy(mv + mvi, rv + rvi, (size_t)vl); rvi += vl; mvi += vl;
+      memcpy(mq + mi, rq + ri, (size_t)ql); ri += ql; mi += ql;
+      continue;
+    }
+    const int32_t a = q_offset_ms(rq, ri), b = q_offset_ms(L->q, li);
+    if (a == b) {  /* duplicate: the incoming one is discarded */
+      rvi += q_vlen(rq, ri);
+      ri += q_len(rq, ri);
+      continue;
+    }
+    if (a < b) {
+      const int vl = q_vlen(rq, ri), ql = q_len(rq, ri);
+      memcpy(mv + mvi, rv + rvi, (size_t)vl); rvi += vl; mvi += vl;
+      memcpy(mq + mi, rq + ri, (size_t)ql); ri += ql; mi += ql;
+    } else {
+      const int vl = q_vlen(L->q, li), ql = q_len(L->q, li);
+      memcpy(mv + mvi, L->v + lvi, (size_t)vl); lvi += vl; mvi += vl;
+      memcpy(mq + mi, L->q + li, (size_t)ql); li += ql; mi += ql;
+    }
+  }
+  uint8_t meta = 0;
+  if ((L->vlen > 0 && (L->v[L->vlen - 1] & 1)) || (rvl > 0 && (rv[rvl - 1] & 1)))
+    meta = 1;
+  mv[mvi++] = meta;
+  free(L->q);
+  free(L->v);
+  L->q = mq;
+  L->qlen = mi;
+  L->v = mv;
+  L->vlen = mvi;
+}
+
+/* Rows [0, R) of one series in arrival order (row_base_s, per-row qualifier
+ * and value bytes).  Writes the span's rows in iteration order: out_base[k],
+ * out_qoff[k..k+1], out_voff[k..k+1] into out_q / out_v; *out_rows = count. */
+int or_span_assemble(int64_t R, const int64_t* row_base_s,
+                     const int64_t* qoff, const uint8_t* qual,
+                     const int64_t* voff, const uint8_t* val,
+                     int64_t* out_rows, int64_t* out_base, int64_t* out_qoff,
+                     uint8_t* out_q, int64_t* out_voff, uint8_t* out_v,
+                     char* err, int errlen) {
+  rseq_t* rs = (rseq_t*)calloc((size_t)(R ? R : 1), sizeof(rseq_t));
+  int64_t n = 0;
+  for (int64_t r = 0; r < R; r++) {
+    const uint8_t* q = qual + qoff[r];
+    const int64_t ql = qoff[r + 1] - qoff[r];
+    const uint8_t* v = val + voff[r];
+    const int64_t vl = voff[r + 1] - voff[r];
+    int64_t last_ts = 0;
+    if (n) {
+      const rseq_t* last = &rs[n - 1];
+      last_ts = rseq_ts(last, rseq_size(last) - 1);
+    }
+    rseq_t x = {row_base_s[r], NULL, ql, NULL, vl};
+    x.q = (uint8_t*)malloc((size_t)(ql ? ql : 1));
+    x.v = (uint8_t*)malloc((size_t)(vl ? vl : 1));
+    memcpy(x.q, q, (size_t)ql);
+    memcpy(x.v, v, (size_t)vl);
+    int merged = 0;
+    if (n && ql > 0 && last_ts >= rseq_ts(&x, 0)) {
+      for (int64_t k = 0; k < n; k++)
+        if (rs[k].base == x.base) {
+          rseq_add(&rs[k], q, ql, v, vl);
+          merged = 1;
+          break;
+        }
+    }
+    if (merged) {
+      free(x.q);
+      free(x.v);
+    } else {
+      rs[n++] = x;
+    }
+  }
+  for (int64_t a = 1; a < n; a++) {  /* stable sort by base time */
+    rseq_t x = rs[a];
+    int64_t b = a - 1;
+    while (b >= 0 && rs[b].base > x.base) { rs[b + 1] = rs[b]; b--; }
+    rs[b + 1] = x;
+  }
+  out_qoff[0] = out_voff[0] = 0;
+  for (int64_t k = 0; k < n; k++) {
+    out_base[k] = rs[k].base;
+    memcpy(out_q + out_qoff[k], rs[k].q, (size_t)rs[k].qlen);
+    memcpy(out_v + out_voff[k], rs[k].v, (size_t)rs[k].vlen);
+    out_qoff[k + 1] = out_qoff[k] + rs[k].qlen;
+    out_voff[k + 1] = out_voff[k] + rs[k].vlen;
+    free(rs[k].q);
+    free(rs[k].v);
+  }
+  free(rs);
+  *out_rows = n;
+  (void)err;
+  (void)errlen;
+  return OTSDB_OK;
+}

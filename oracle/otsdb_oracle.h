@@ -61,6 +61,26 @@ int or_decode_row(const uint8_t* qual, int64_t qlen, const uint8_t* vals,
                   int64_t vlen, int64_t base_time_s, or_point* out,
                   int64_t cap, int64_t* needed, char* err, int errlen);
 
+/* Query-time compaction of one storage row (CompactionQueue.Compaction
+ * .compact): columns [0, ncol) with qualifier / value byte ranges and HBase
+ * timestamps (NULL: column order).  Output: one compacted column (meta byte
+ * on multi-value columns); *out_qlen = 0 when the row holds no data point. */
+int or_compact_row(int64_t ncol, const int64_t* col_qoff, const uint8_t* qual,
+                   const int64_t* col_voff, const uint8_t* val,
+                   const int64_t* col_ts, int fix_duplicates,
+                   uint8_t* out_q, int64_t qcap, uint8_t* out_v, int64_t vcap,
+                   int64_t* out_qlen, int64_t* out_vlen, char* err,
+                   int errlen);
+
+/* Span assembly (Span.addRow + RowSeq.addRow + checkRowOrder) of one
+ * series' compacted rows in arrival order; output rows in iteration order. */
+int or_span_assemble(int64_t R, const int64_t* row_base_s,
+                     const int64_t* qoff, const uint8_t* qual,
+                     const int64_t* voff, const uint8_t* val,
+                     int64_t* out_rows, int64_t* out_base, int64_t* out_qoff,
+                     uint8_t* out_q, int64_t* out_voff, uint8_t* out_v,
+                     char* err, int errlen);
+
 /* Synthetic generator (SURVEY §8d as restated in DESIGN.md §Workload). */
 int64_t or_gen_count(const otsdb_gen_spec* g, int64_t s);
 int64_t or_gen_fill(const otsdb_gen_spec* g, int64_t s, int64_t* ts,

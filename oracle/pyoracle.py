@@ -37,6 +37,12 @@ def lib():
         l.or_run_long.argtypes = [i32, vp, i64, C.POINTER(i64), cp, C.c_int]
         l.or_decode_row.argtypes = [vp, i64, vp, i64, i64, vp, i64,
                                     C.POINTER(i64), cp, C.c_int]
+        l.or_compact_row.argtypes = [i64, vp, vp, vp, vp, vp, C.c_int, vp,
+                                     i64, vp, i64, C.POINTER(i64),
+                                     C.POINTER(i64), cp, C.c_int]
+        l.or_span_assemble.argtypes = [i64, vp, vp, vp, vp, vp,
+                                       C.POINTER(i64), vp, vp, vp, vp, vp,
+                                       cp, C.c_int]
         l.or_gen_count.argtypes = [vp, i64]
         l.or_gen_count.restype = i64
         l.or_gen_fill.argtypes = [vp, i64, vp, vp]
@@ -162,3 +168,67 @@ def gen_batch(gspec, series0, n_series, group_of=None):
     g_off, members = groups_from_ids(gid)
     return HostBatch(np.array(offs, np.int64), ts, val, None, sf, g_off,
                      members)
+
+
+def _u8(b):
+    return np.frombuffer(bytes(b), np.uint8) if len(b) else np.zeros(1, np.uint8)
+
+
+def compact_row(columns, col_ts=None, fix_duplicates=True):
+    """CompactionQueue.compact of one storage row: columns = [(qualifier
+    bytes, value bytes)].  Returns (qualifier bytes, value bytes), or None
+    when the row holds no data point."""
+    l = lib()
+    qs = b"".join(bytes(q) for q, _ in columns)
+    vs = b"".join(bytes(v) for _, v in columns)
+    qoff = np.cumsum([0] + [len(q) for q, _ in columns]).astype(np.int64)
+    voff = np.cumsum([0] + [len(v) for _, v in columns]).astype(np.int64)
+    qa, va = _u8(qs), _u8(vs)
+    ts = None if col_ts is None else np.asarray(col_ts, np.int64)
+    cap = len(qs) + len(vs) + 16
+    oq = np.zeros(cap, np.uint8)
+    ov = np.zeros(cap, np.uint8)
+    nq, nv = C.c_int64(), C.c_int64()
+    err = C.create_string_buffer(256)
+    st = l.or_compact_row(len(columns), qoff.ctypes.data, qa.ctypes.data,
+                          voff.ctypes.data, va.ctypes.data,
+                          None if ts is None else ts.ctypes.data,
+                          1 if fix_duplicates else 0, oq.ctypes.data, cap,
+                          ov.ctypes.data, cap, C.byref(nq), C.byref(nv), err,
+                          256)
+    if st:
+        raise OracleError(st, err.value.decode())
+    if nq.value == 0:
+        return None
+    return bytes(oq[:nq.value]), bytes(ov[:nv.value])
+
+
+def span_assemble(rows):
+    """Span.addRow over one series' compacted rows in arrival order: rows =
+    [(base_s, qualifier bytes, value bytes)].  Returns the span's rows in
+    iteration order as [(base_s, qualifier bytes, value bytes)]."""
+    l = lib()
+    R = len(rows)
+    base = np.asarray([r[0] for r in rows] or [0], np.int64)
+    qs = b"".join(bytes(r[1]) for r in rows)
+    vs = b"".join(bytes(r[2]) for r in rows)
+    qoff = np.cumsum([0] + [len(r[1]) for r in rows]).astype(np.int64)
+    voff = np.cumsum([0] + [len(r[2]) for r in rows]).astype(np.int64)
+    qa, va = _u8(qs), _u8(vs)
+    cap = len(qs) + len(vs) + R + 16
+    ob = np.zeros(max(R, 1), np.int64)
+    oqo = np.zeros(R + 1, np.int64)
+    ovo = np.zeros(R + 1, np.int64)
+    oq = np.zeros(cap, np.uint8)
+    ov = np.zeros(cap, np.uint8)
+    n = C.c_int64()
+    err = C.create_string_buffer(256)
+    st = l.or_span_assemble(R, base.ctypes.data, qoff.ctypes.data,
+                            qa.ctypes.data, voff.ctypes.data, va.ctypes.data,
+                            C.byref(n), ob.ctypes.data, oqo.ctypes.data,
+                            oq.ctypes.data, ovo.ctypes.data, ov.ctypes.data,
+                            err, 256)
+    if st:
+        raise OracleError(st, err.value.decode())
+    return [(int(ob[k]), bytes(oq[oqo[k]:oqo[k + 1]]),
+             bytes(ov[ovo[k]:ovo[k + 1]])) for k in range(n.value)]

@@ -1185,6 +1185,222 @@ _q("tq_interp_ms_downsampled", "sum",
    ds_interval_ms=1000, ds_agg="sum")
 
 
+# ------------------------------------------ query-time compaction (bytes)
+# test/core/TestCompactionQueue.java: each test's KeyValues (makekv stamps
+# them with increasing HBase timestamps, :1537-1539: the later cell is the
+# newer one) and the compacted column it asserts.  fix_duplicates is true
+# (:95-97) unless the test turns it off.  Hex strings.
+import struct as _st
+
+
+def _Lb(x):
+    return _st.pack(">q", x)
+
+
+def _Ib(x):
+    return _st.pack(">I", x & 0xFFFFFFFF)
+
+
+_ZB = b"\x00"
+_NOTE_Q = bytes([1, 0, 0])
+_NOTE = (b'{"tsuid":"ABCD","description":"Description","notes":"Notes",'
+         b'"custom":null,"endTime":1328140801,"startTime":1328140800}')
+_APPQ = bytes([0x05, 0x00, 0x00])
+TCQ = "test/core/TestCompactionQueue.java"
+
+
+def _cq(name, cols, expect, cite, fix=True, error=None):
+    c = dict(kind="compact", name=name,
+             columns=[[q.hex(), v.hex()] for q, v in cols],
+             fix_duplicates=fix, cite=TCQ + cite)
+    if error:
+        c["error"] = error
+    else:
+        c["expect"] = None if expect is None else [expect[0].hex(),
+                                                   expect[1].hex()]
+    add(**c)
+
+
+_q1, _q2 = bytes([0, 7]), bytes([0, 0x17])
+_cq("emptyRow", [], None, ":134-146")
+_cq("oneCellRow", [(_q1, _Lb(42))], (_q1, _Lb(42)), ":148-164")
+_cq("oneCellAppend", [(_APPQ, _q1 + _Lb(42))], (_q1, _Lb(42)), ":166-183")
+_cq("oneCellRowWAnnotation", [(_NOTE_Q, _NOTE), (_q1, _Lb(42))],
+    (_q1, _Lb(42)), ":185-203")
+_cq("oneCellAppendWAnnotation", [(_NOTE_Q, _NOTE), (_APPQ, _q1 + _Lb(42))],
+    (_q1, _Lb(42)), ":205-224")
+_cq("oneCellRowBadLength", [(bytes([0, 3]), _Lb(42))],
+    (bytes([0, 7]), _Lb(42)), ":246-262")
+_qm = bytes([0xF0, 0, 0, 7])
+_cq("oneCellRowMS", [(_qm, _Lb(42))], (_qm, _Lb(42)), ":264-280")
+_cq("twoCellRow", [(_q1, _Lb(4)), (_q2, _Lb(5))],
+    (_q1 + _q2, _Lb(4) + _Lb(5) + _ZB), ":282-302")
+_cq("twoCellAppend", [(_APPQ, _q1 + _Lb(42) + _q2 + _Lb(5))],
+    (_q1 + _q2, _Lb(42) + _Lb(5) + _ZB), ":304-323")
+_cq("twoCellRowWAnnotation", [(_NOTE_Q, _NOTE), (_q1, _Lb(4)), (_q2, _Lb(5))],
+    (_q1 + _q2, _Lb(4) + _Lb(5) + _ZB), ":325-347")
+_cq("twoCellAppendWAnnotations",
+    [(_NOTE_Q, _NOTE), (_APPQ, _q1 + _Lb(42) + _q2 + _Lb(5))],
+    (_q1 + _q2, _Lb(42) + _Lb(5) + _ZB), ":349-370")
+_fq = [_st.pack(">H", ((i << 4) | 0x07) & 0xFFFF) for i in range(3600)]
+_cq("fullRowSeconds", [(_fq[i], _Lb(i)) for i in range(3600)],
+    (b"".join(_fq), b"".join(_Lb(i) for i in range(3600)) + _ZB), ":372-397")
+_mq1, _mq2 = bytes([0xF0, 0, 0, 7]), bytes([0xF0, 0, 1, 7])
+_cq("twoCellRowMS", [(_mq1, _Lb(4)), (_mq2, _Lb(5))],
+    (_mq1 + _mq2, _Lb(4) + _Lb(5) + _ZB), ":425-445")
+_sq2, _sq3 = bytes([0xF0, 0, 2, 7]), bytes([0xF0, 0, 1, 7])
+_cq("sortMsAndS", [(_q1, _Lb(4)), (_sq2, _Lb(5)), (_sq3, _Lb(5))],
+    (_q1 + _sq3 + _sq2, _Lb(4) + _Lb(5) + _Lb(5) + b"\x01"), ":447-473")
+_o1, _o2, _o3 = bytes([2, 7]), bytes([0, 7]), bytes([1, 7])
+_cq("secondsOutOfOrder", [(_o1, _Lb(4)), (_o2, _Lb(5)), (_o3, _Lb(6))],
+    (_o2 + _o3 + _o1, _Lb(5) + _Lb(6) + _Lb(4) + _ZB), ":475-501")
+_m1, _m2, _m3 = (bytes([0xF0, 0, 2, 7]), bytes([0xF0, 0, 0, 7]),
+                 bytes([0xF0, 0, 1, 7]))
+_cq("msOutOfOrder", [(_m1, _Lb(4)), (_m2, _Lb(5)), (_m3, _Lb(6))],
+    (_m2 + _m3 + _m1, _Lb(5) + _Lb(6) + _Lb(4) + _ZB), ":503-530")
+_cq("secondAndMs", [(_q1, _Lb(4)), (_mq2, _Lb(5))],
+    (_q1 + _mq2, _Lb(4) + _Lb(5) + b"\x01"), ":532-553")
+_cq("secondAndMsWAnnotation", [(_NOTE_Q, _NOTE), (_q1, _Lb(4)), (_mq2, _Lb(5))],
+    (_q1 + _mq2, _Lb(4) + _Lb(5) + b"\x01"), ":555-578")
+_cq("msSameAsSecond", [(_q1, _Lb(4)), (_mq1, _Lb(5))], None, ":580-593",
+    fix=False, error="IllegalDataException")
+_cq("msSameAsSecondFix", [(_q1, _Lb(4)), (_mq1, _Lb(5))], (_mq1, _Lb(5)),
+    ":595-614")
+_cq("fixQualifierFlags", [(bytes([0, 3]), _Lb(4)), (_q2, _Lb(5))],
+    (bytes([0, 7]) + _q2, _Lb(4) + _Lb(5) + _ZB), ":616-639")
+_f42 = _st.unpack(">i", _st.pack(">f", 4.2))[0]
+_cq("fixFloatingPoint", [(_q1, _Lb(4)), (bytes([0, 0x1B]), _Lb(_f42))],
+    (_q1 + bytes([0, 0x1B]), _Lb(4) + _Ib(_f42) + _ZB), ":641-666")
+_cq("overlappingDataPoints", [(_q1, _Lb(4)), (bytes([0, 3]), _Ib(4))], None,
+    ":668-682", fix=False, error="IllegalDataException")
+_cq("overlappingDataPointsFix", [(_q1, _Lb(4)), (bytes([0, 3]), _Ib(4))],
+    (bytes([0, 3]), _Ib(4)), ":684-704")
+_cq("failedCompactNoop",
+    [(_q1, _Lb(4)), (_q2, _Lb(5)), (_q1 + _q2, _Lb(4) + _Lb(5) + _ZB)],
+    (_q1 + _q2, _Lb(4) + _Lb(5) + _ZB), ":706-731")
+_cq("annotationOnly", [(_NOTE_Q, _NOTE)], None, ":733-747")
+_cq("annotationsOnly", [(_NOTE_Q, _NOTE), (bytes([1, 0, 1]), _NOTE)], None,
+    ":749-766")
+_w2, _w3 = bytes([0, 0x27]), bytes([0, 0x17])
+_cq("weirdOverlappingCompactedCells",
+    [(_q1, _Lb(4)), (_q1 + _w2, _Lb(4) + _Lb(5) + _ZB),
+     (_q1 + _w3, _Lb(4) + _Lb(6) + _ZB), (_w3, _Lb(6)), (_w2, _Lb(5))],
+    (_q1 + _w3 + _w2, _Lb(4) + _Lb(6) + _Lb(5) + _ZB), ":1065-1101")
+_t = [bytes([0, (k << 4) | 7]) for k in (0, 2, 3, 4, 5, 6)]
+_tv = [_Lb(x) for x in (4, 5, 6, 7, 8, 9)]
+_cq("tripleCompacted",
+    [(_t[0] + _t[1], _tv[0] + _tv[1] + _ZB), (_t[2] + _t[3], _tv[2] + _tv[3] + _ZB),
+     (_t[4] + _t[5], _tv[4] + _tv[5] + _ZB)],
+    (b"".join(_t), b"".join(_tv) + _ZB), ":1103-1144")
+_cq("tripleCompactedOutOfOrder",
+    [(_t[0] + _t[1], _tv[0] + _tv[1] + _ZB), (_t[4] + _t[5], _tv[4] + _tv[5] + _ZB),
+     (_t[2] + _t[3], _tv[2] + _tv[3] + _ZB)],
+    (b"".join(_t), b"".join(_tv) + _ZB), ":1146-1187")
+_tm = [bytes([0xF0, 0, 0, 7]), bytes([0, 0x27]), bytes([0, 0x37]),
+       bytes([0xF0, 0x04, 0x65, 0x07]), bytes([0xF0, 0x05, 0x5F, 0x07]),
+       bytes([0, 0x67])]
+_cq("tripleCompactedSecondsAndMs",
+    [(_tm[0] + _tm[1], _tv[0] + _tv[1] + _ZB),
+     (_tm[2] + _tm[3], _tv[2] + _tv[3] + _ZB),
+     (_tm[4] + _tm[5], _tv[4] + _tv[5] + _ZB)],
+    (b"".join(_tm), b"".join(_tv) + b"\x01"), ":1189-1232")
+_a = [bytes([0, (k << 4) | 7]) for k in range(6)]
+_av = [_Lb(x) for x in (42, 5, 3, 2, 1, 0)]
+_cq("appendsAndLaterPuts",
+    [(_APPQ, _a[0] + _av[0] + _a[1] + _av[1]), (_a[2], _av[2]), (_a[3], _av[3])],
+    (b"".join(_a[:4]), b"".join(_av[:4]) + _ZB), ":1234-1261")
+_cq("appendsAndEarlierPuts",
+    [(_a[0], _av[0]), (_a[1], _av[1]), (_APPQ, _a[2] + _av[2] + _a[3] + _av[3])],
+    (b"".join(_a[:4]), b"".join(_av[:4]) + _ZB), ":1263-1290")
+_cq("appendsAndInterspersedPuts",
+    [(_a[0], _av[0]), (_a[2], _av[2]), (_APPQ, _a[1] + _av[1] + _a[3] + _av[3])],
+    (b"".join(_a[:4]), b"".join(_av[:4]) + _ZB), ":1292-1319")
+_cq("doubleAppends",
+    [(_APPQ, _a[0] + _av[0] + _a[1] + _av[1]),
+     (_APPQ, _a[2] + _av[2] + _a[3] + _av[3])],
+    (b"".join(_a[:4]), b"".join(_av[:4]) + _ZB), ":1321-1348")
+_cq("tripleAppends",
+    [(_APPQ, _a[0] + _av[0] + _a[1] + _av[1]),
+     (_APPQ, _a[2] + _av[2] + _a[3] + _av[3]),
+     (_APPQ, _a[4] + _av[4] + _a[5] + _av[5])],
+    (b"".join(_a), b"".join(_av) + _ZB), ":1350-1383")
+_cq("doubleAppendsAndPuts",
+    [(_APPQ, _a[0] + _av[0] + _a[1] + _av[1]), (_a[2], _av[2]), (_a[3], _av[3]),
+     (_APPQ, _a[4] + _av[4] + _a[5] + _av[5])],
+    (b"".join(_a), b"".join(_av) + _ZB), ":1385-1418")
+_cq("appendsAndCompacted",
+    [(_APPQ, _a[0] + _av[0] + _a[1] + _av[1]),
+     (_a[2] + _a[3], _av[2] + _av[3] + _ZB)],
+    (b"".join(_a[:4]), b"".join(_av[:4]) + _ZB), ":1420-1447")
+_cq("appendsAndCompactedAndPuts",
+    [(_APPQ, _a[0] + _av[0] + _a[1] + _av[1]),
+     (_a[2] + _a[3], _av[2] + _av[3] + _ZB), (_a[4], _av[4]), (_a[5], _av[5])],
+    (b"".join(_a), b"".join(_av) + _ZB), ":1449-1482")
+_cq("appendsDuplicatePuts",
+    [(_APPQ, _a[0] + _av[0] + _a[1] + _av[1]), (_a[0], _av[0]), (_a[1], _av[1])],
+    (_a[0] + _a[1], _av[0] + _av[1] + _ZB), ":1484-1505")
+_cq("appendsDuplicateCompacted",
+    [(_APPQ, _a[0] + _av[0] + _a[1] + _av[1]),
+     (_a[0] + _a[1], _av[0] + _av[1] + _ZB)],
+    (_a[0] + _a[1], _av[0] + _av[1] + _ZB), ":1507-1530")
+
+# ----------------------------------------------------- span assembly (bytes)
+# test/core/TestRowSeq.java:122-508: rows of one series handed to the span
+# in this order (setRow + addRow), and the data points the series yields
+# (timestamps, long values).  Base time 1356998400 (KEY).
+TRS = "test/core/TestRowSeq.java"
+_B = 1356998400
+
+
+def _sp(name, rows, expect, cite):
+    add(kind="span", name=name,
+        rows=[[b, q.hex(), v.hex()] for b, q, v in rows],
+        expect=[[t, x] for t, x in expect], cite=TRS + cite)
+
+
+def _sq(*ks):
+    return b"".join(bytes([0, (k << 4) | 7]) for k in ks)
+
+
+def _sv(*xs):
+    return b"".join(_Lb(x) for x in xs) + _ZB
+
+
+_E4 = [(1356998400000, 4), (1356998402000, 5), (1356998403000, 6),
+       (1356998404000, 7)]
+_sp("addRowMergeLater", [(_B, _sq(0, 2), _sv(4, 5)), (_B, _sq(3, 4), _sv(6, 7))],
+    _E4, ":122-150")
+_sp("addRowMergeEarlier", [(_B, _sq(3, 4), _sv(6, 7)), (_B, _sq(0, 2), _sv(4, 5))],
+    _E4, ":187-215")
+_sp("addRowMergeMiddle",
+    [(_B, _sq(0, 2), _sv(4, 5)), (_B, _sq(5, 6), _sv(8, 9)),
+     (_B, _sq(3, 4), _sv(6, 7))],
+    _E4 + [(1356998405000, 8), (1356998406000, 9)], ":252-292")
+_sp("addRowMergeDuplicateLater",
+    [(_B, _sq(0, 2, 3), _sv(4, 5, 6)), (_B, _sq(3, 4), _sv(6, 7))], _E4,
+    ":342-370")
+_sp("addRowMergeDuplicateEarlier",
+    [(_B, _sq(2, 3, 4), _sv(5, 6, 7)), (_B, _sq(0, 2), _sv(4, 5))], _E4,
+    ":372-400")
+_msq = lambda *ms: b"".join(_Ib((0xF << 28) | (m << 6) | 7) for m in ms)  # noqa
+_sp("addRowMergeMs",
+    [(_B, _msq(0, 8), _sv(4, 5)), (_B, _msq(28, 36), _sv(6, 7))],
+    [(1356998400000, 4), (1356998400008, 5), (1356998400028, 6),
+     (1356998400036, 7)], ":447-475")
+_sp("addRowMergeSecAndMs",
+    [(_B, _sq(0) + _msq(8), _Lb(4) + _Lb(5) + b"\x01"),
+     (_B, _sq(3) + _msq(1060), _Lb(6) + _Lb(7) + b"\x01")],
+    [(1356998400000, 4), (1356998400008, 5), (1356998403000, 6),
+     (1356998401060, 7)], ":477-507")
+# timestamp / iterate tests :523-696 (one row)
+_sp("timestamp", [(_B, _sq(0, 2), _sv(4, 5))],
+    [(1356998400000, 4), (1356998402000, 5)], ":523-538")
+_sp("timestampMs", [(_B, _msq(0, 8), _sv(4, 5))],
+    [(1356998400000, 4), (1356998400008, 5)], ":575-590")
+_sp("timestampMixedNormalized", [(_B, _sq(0) + _msq(8), _sv(4, 5))],
+    [(1356998400000, 4), (1356998400008, 5)], ":592-607")
+
+
 def _enc(x):
     if isinstance(x, float):
         if math.isnan(x):

@@ -116,3 +116,37 @@ def test_previous_interval(c):
     got = jcalendar.previous_interval(c["ts"], c["interval"], c["unit"],
                                       c["tz"])
     assert got == c["expect"], (got, c["expect"])
+
+
+@pytest.mark.parametrize("c", kat.load_cases("compact"), ids=lambda c: c["name"])
+def test_compact_row(c):
+    """Query-time compaction of one storage row (CompactionQueue.compact via
+    Span's scanner path) against TestCompactionQueue's asserted cells.  The
+    JUnit KeyValues carry increasing HBase timestamps (makekv, :1537), so the
+    column index is the cell timestamp."""
+    cols = [(bytes.fromhex(q), bytes.fromhex(v)) for q, v in c["columns"]]
+    ts = list(range(len(cols)))
+    if "error" in c:
+        with pytest.raises(pyoracle.OracleError) as ei:
+            pyoracle.compact_row(cols, ts, c["fix_duplicates"])
+        assert ei.value.status == EXC[c["error"]]
+        return
+    got = pyoracle.compact_row(cols, ts, c["fix_duplicates"])
+    if c["expect"] is None:
+        assert got is None
+    else:
+        assert got is not None
+        assert got[0].hex() == c["expect"][0]
+        assert got[1].hex() == c["expect"][1]
+
+
+@pytest.mark.parametrize("c", kat.load_cases("span"), ids=lambda c: c["name"])
+def test_span_assemble(c):
+    """Span/RowSeq.addRow merge of one series' rows in arrival order, then
+    the iteration the span yields, against TestRowSeq's asserted points."""
+    rows = [(b, bytes.fromhex(q), bytes.fromhex(v)) for b, q, v in c["rows"]]
+    got = []
+    for base, q, v in pyoracle.span_assemble(rows):
+        for p in pyoracle.decode_row(q, v, base):
+            got.append([int(p["ts"]), kat.point_value(p["bits"], p["is_int"])])
+    assert got == c["expect"]
