@@ -366,6 +366,75 @@ otsdb_status otsdb_agg_run_cells_device(otsdb_ctx* ctx,
                                         const otsdb_batch* batch,
                                         otsdb_result* out, void* hip_stream);
 
+/* ---- storage rows: query-time compaction + span assembly (§8a a3, a4) -- */
+/* The storage rows of a query exactly as the scanner returns them, before
+ * TSDB.compact (SaltScanner.java:849-881): each row (one series, one base
+ * hour) is a list of columns — single-point cells, compacted columns, append
+ * columns (qualifier {0x05,0,0}), annotations / histograms (skipped).        */
+typedef struct {
+  int64_t n_rows;               /* R                                        */
+  const int64_t* row_series;    /* [R] series index, nondecreasing; a series'
+                                 * rows in the order the scanner delivers them
+                                 * (the Span.addRow call order)            */
+  const int64_t* row_base_s;    /* [R] row base time, seconds (row key)     */
+  const int64_t* row_col_off;   /* [R+1] CSR into the columns               */
+  const int64_t* col_qual_off;  /* [C+1] offsets into qual                  */
+  const uint8_t* qual;          /* column qualifiers                        */
+  const int64_t* col_val_off;   /* [C+1] offsets into val                   */
+  const uint8_t* val;           /* column values                            */
+  const int64_t* col_ts;        /* [C] HBase cell timestamps (newest wins a
+                                 * duplicate); NULL = ascending column order */
+} otsdb_raw_rows;
+
+/* CompactionQueue.compact of every row (CompactionQueue.java:340-616, with
+ * ColumnDatapointIterator fix-ups :73-87 / Internal.java:535-591 and
+ * AppendDataPoints.parseKeyValue :118-236): one compacted column per row,
+ * rows without a data point dropped (as the scanner drops a null
+ * compaction), kept rows packed in input order into `out` (DEVICE pointers,
+ * caller-allocated: qual_capacity >= the input's qualifier + value bytes and
+ * val_capacity >= its value bytes + n_rows always suffice).  *n_out_rows =
+ * kept rows; out->qual_off[n] / val_off[n] hold the totals; out->row_series
+ * may be NULL.  out == NULL: sizes only.  Duplicate offsets with different
+ * values: OTSDB_E_ILLEGAL_DATA unless fix_duplicates
+ * (tsd.storage.fix_duplicates); corrupt cells / appends: OTSDB_E_ILLEGAL_DATA;
+ * an odd qualifier starting 0x05 that is not 3 bytes:
+ * OTSDB_E_ILLEGAL_ARGUMENT; a row needing a merge of more than 8192 points
+ * or 4096 data columns: OTSDB_E_UNSUPPORTED.  The first failing row (in row
+ * order) decides the status.                                               */
+otsdb_status otsdb_compact_rows_device(otsdb_ctx* ctx, const otsdb_raw_rows* raw,
+                                       int32_t fix_duplicates,
+                                       const otsdb_cells_out* out,
+                                       int64_t qual_capacity,
+                                       int64_t val_capacity,
+                                       int64_t* n_out_rows, void* hip_stream);
+
+/* Span.addRow of every series' compacted rows in arrival order
+ * (Span.java:177-220, RowSeq.addRow RowSeq.java:91-222, checkRowOrder
+ * :387-392): rows of the same key merge, rows end up sorted by base time.
+ * `cells` rows carry nondecreasing row_series; out (DEVICE, caller-allocated,
+ * capacities >= the input's bytes + n_rows) receives the span rows; NULL =
+ * sizes only.  A row without a qualifier is OTSDB_E_ILLEGAL_ARGUMENT.       */
+otsdb_status otsdb_span_assemble_device(otsdb_ctx* ctx, const otsdb_cells* cells,
+                                        int64_t n_series,
+                                        const otsdb_cells_out* out,
+                                        int64_t qual_capacity,
+                                        int64_t val_capacity,
+                                        int64_t* n_out_rows, void* hip_stream);
+
+/* The whole query from storage rows: compaction -> span assembly -> the
+ * fused decode + aggregation of otsdb_agg_run_cells_device.  `batch`
+ * supplies n_series and the groups.  _device: DEVICE pointers;
+ * otsdb_agg_run_raw: HOST pointers (the JNI entry), synchronous.            */
+otsdb_status otsdb_agg_run_raw_device(otsdb_ctx* ctx,
+                                      const otsdb_query_spec* spec,
+                                      const otsdb_raw_rows* raw,
+                                      int32_t fix_duplicates,
+                                      const otsdb_batch* batch,
+                                      otsdb_result* out, void* hip_stream);
+otsdb_status otsdb_agg_run_raw(otsdb_ctx* ctx, const otsdb_query_spec* spec,
+                               const otsdb_raw_rows* raw, int32_t fix_duplicates,
+                               const otsdb_batch* batch, otsdb_result* out);
+
 /* ---- stage timing (bench roofline) ------------------------------------- */
 /* When enabled, every query records HIP events around its pipeline stages
  * on the query's stream.  otsdb_prof_read returns, per stage, the summed

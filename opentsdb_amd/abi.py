@@ -103,6 +103,20 @@ class CellsOut(C.Structure):
                 ("val_off", C.c_void_p), ("val", C.c_void_p)]
 
 
+class RawRows(C.Structure):
+    _fields_ = [
+        ("n_rows", C.c_int64),
+        ("row_series", C.c_void_p),
+        ("row_base_s", C.c_void_p),
+        ("row_col_off", C.c_void_p),
+        ("col_qual_off", C.c_void_p),
+        ("qual", C.c_void_p),
+        ("col_val_off", C.c_void_p),
+        ("val", C.c_void_p),
+        ("col_ts", C.c_void_p),
+    ]
+
+
 class GenSpec(C.Structure):
     _fields_ = [
         ("seed", C.c_uint64),
@@ -124,6 +138,8 @@ EXPORTS = [
     "otsdb_decode_cells_device", "otsdb_sel_prepare_device",
     "otsdb_sel_hist_device", "otsdb_sel_finish_device",
     "otsdb_encode_cells_device", "otsdb_agg_run_cells_device",
+    "otsdb_compact_rows_device", "otsdb_span_assemble_device",
+    "otsdb_agg_run_raw_device", "otsdb_agg_run_raw",
 ]
 
 _lib = None
@@ -193,6 +209,17 @@ def load(path=None):
     lib.otsdb_agg_run_cells_device.argtypes = [vp, PS, C.POINTER(Cells), PB,
                                                PR, vp]
     lib.otsdb_agg_run_cells_device.restype = C.c_int
+    PW, PC, PCO = C.POINTER(RawRows), C.POINTER(Cells), C.POINTER(CellsOut)
+    lib.otsdb_compact_rows_device.argtypes = [vp, PW, i32, PCO, i64, i64,
+                                              C.POINTER(i64), vp]
+    lib.otsdb_compact_rows_device.restype = C.c_int
+    lib.otsdb_span_assemble_device.argtypes = [vp, PC, i64, PCO, i64, i64,
+                                               C.POINTER(i64), vp]
+    lib.otsdb_span_assemble_device.restype = C.c_int
+    lib.otsdb_agg_run_raw_device.argtypes = [vp, PS, PW, i32, PB, PR, vp]
+    lib.otsdb_agg_run_raw_device.restype = C.c_int
+    lib.otsdb_agg_run_raw.argtypes = [vp, PS, PW, i32, PB, PR]
+    lib.otsdb_agg_run_raw.restype = C.c_int
     lib.otsdb_prof_enable.argtypes = [vp, C.c_int]
     lib.otsdb_prof_enable.restype = C.c_int
     lib.otsdb_prof_read.argtypes = [vp, vp, vp, C.c_int, C.c_int]

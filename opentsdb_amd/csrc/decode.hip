@@ -825,7 +825,7 @@ __global__ __launch_bounds__(256, WAVES) void k_bucketize_cells(
         if (x == 42) Sk.rowv[0] = 1.0;
       } else if (hi > lo)
         reduce_step<M, K, 1>(P, Bd, 1, lo, hi, st0, st0 + (int64_t)K * lane,
-                             t, v, Sk, err, carry_key, carry);
+                             t, v, Sk, err, carry_key, carry, true);
       if (hi < st0 + n_st) {  // reached stop_ts inside this row
         stop_r = r;
         stop_i = hi;

@@ -25,6 +25,7 @@
 #include "select.hip"
 #include "decode.hip"
 #include "raw.hip"
+#include "rows.hip"
 #include "launch.h"
 
 using namespace otsdb;
@@ -160,6 +161,14 @@ struct otsdb_ctx {
   size_t dec_ws_cap = 0;
   void* ws2 = nullptr;     // raw group-by: candidates, sort, selection slab
   size_t ws2_cap = 0;
+  void* rows_ws = nullptr;  // storage-row compaction / span assembly: per-row
+  size_t rows_ws_cap = 0;   // and per-series plan arrays
+  void* rows_scr = nullptr;  // GENERAL-row cell records + staging / replay arenas
+  size_t rows_scr_cap = 0;
+  void* raw_cells[2] = {nullptr, nullptr};  // raw-row query: compacted rows,
+  size_t raw_cells_cap[2] = {0, 0};          // then the assembled spans
+  void* raw_stage = nullptr;  // otsdb_agg_run_raw: host rows staged in HBM
+  size_t raw_stage_cap = 0;
   // cross-rank selection session (otsdb_sel_*): lives in `ws` between calls
   struct {
     bool active = false;
@@ -1277,6 +1286,301 @@ otsdb_status run_cells_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
   return run_device_impl(c, spec, &cb, out, goff);
 }
 
+// ----------------------------------------- storage rows -> compacted rows
+otsdb_status row_status(otsdb_ctx*, unsigned long long fe, const char* what) {
+  if (fe == ~0ULL) return OTSDB_OK;
+  const int code = (int)(fe & 0xFF);
+  const long long row = (long long)(fe >> 8);
+  switch (code) {
+    case RS_ILLEGAL_ARGUMENT:
+      return fail(OTSDB_E_ILLEGAL_ARGUMENT,
+                  "%s row %lld: Can not parse cell, it is not an appended cell",
+                  what, row);
+    case RS_UNSUPPORTED:
+      return fail(OTSDB_E_UNSUPPORTED,
+                  "%s row %lld: more than %d points or %d data columns to "
+                  "merge, or appended points beside a column out of time order",
+                  what, row, kRowCellCap, kRowColCap);
+    default:
+      return fail(OTSDB_E_ILLEGAL_DATA,
+                  "%s row %lld: corrupted value or duplicate timestamp", what,
+                  row);
+  }
+}
+
+// one exclusive scan of n + 1 int64 (in[n] must be 0), on st
+otsdb_status scan_excl(void* tmp, size_t tmp_bytes, const int64_t* in,
+                       int64_t* out, int64_t n, hipStream_t st) {
+  size_t t = tmp_bytes;
+  HIP_TRY(rocprim::exclusive_scan(tmp, t, in, out, (int64_t)0, (size_t)(n + 1),
+                                  rocprim::plus<int64_t>(), st));
+  return OTSDB_OK;
+}
+
+size_t scan_tmp_bytes(int64_t n, hipStream_t st) {
+  size_t b = 0;
+  rocprim::exclusive_scan(nullptr, b, (const int64_t*)nullptr, (int64_t*)nullptr,
+                          (int64_t)0, (size_t)(n + 1), rocprim::plus<int64_t>(),
+                          st);
+  return (b + 255) & ~(size_t)255;
+}
+
+// CompactionQueue.compact of every storage row (rows.hip).  Output: the kept
+// rows' compacted columns packed in row order, *n_out rows; *qbytes / *vbytes
+// the bytes written.
+otsdb_status cells_buffer(otsdb_ctx* c, int which, int64_t R, int64_t qb,
+                          int64_t vb, otsdb_cells_out* o);
+
+// own >= 0: the output goes to the context's cells buffer `own`, returned in
+// *owned (o is ignored)
+otsdb_status compact_impl(otsdb_ctx* c, const otsdb_raw_rows* raw, int fix,
+                          const otsdb_cells_out* o, int64_t qcap, int64_t vcap,
+                          int64_t* n_out, int64_t* qbytes, int64_t* vbytes,
+                          hipStream_t st, int own = -1,
+                          otsdb_cells_out* owned = nullptr) {
+  const int64_t R = raw->n_rows;
+  if (R < 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "negative n_rows");
+  if (!raw->row_base_s || !raw->row_col_off || !raw->col_qual_off ||
+      !raw->col_val_off || (R > 0 && (!raw->qual || !raw->val)))
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null raw row array");
+  RawDev D{R, raw->row_col_off, raw->col_qual_off, raw->qual, raw->col_val_off,
+           raw->val, raw->col_ts};
+  const size_t tmpb = scan_tmp_bytes(R, st);
+  const size_t A = ((size_t)(R + 1) * 8 + 255) & ~(size_t)255;
+  // kind, lone, gen_n, gen_base, out_q, out_v, kept, oq_off, ov_off, k_off,
+  // first_err, scan temp
+  const size_t need = 10 * A + 256 + tmpb;
+  otsdb_status rc = ensure(&c->rows_ws, &c->rows_ws_cap, need);
+  if (rc) return rc;
+  char* w = (char*)c->rows_ws;
+  uint8_t* kind = (uint8_t*)w;
+  int64_t* lone = (int64_t*)(w + A);
+  int64_t* gen_n = (int64_t*)(w + 2 * A);
+  int64_t* gen_base = (int64_t*)(w + 3 * A);
+  int64_t* out_q = (int64_t*)(w + 4 * A);
+  int64_t* out_v = (int64_t*)(w + 5 * A);
+  int64_t* kept = (int64_t*)(w + 6 * A);
+  int64_t* oq_off = (int64_t*)(w + 7 * A);
+  int64_t* ov_off = (int64_t*)(w + 8 * A);
+  int64_t* k_off = (int64_t*)(w + 9 * A);
+  unsigned long long* first_err = (unsigned long long*)(w + 10 * A);
+  void* tmp = w + 10 * A + 256;
+  HIP_TRY(hipMemsetAsync(first_err, 0xFF, 8, st));
+  for (int64_t* a : {gen_n, out_q, out_v, kept})
+    HIP_TRY(hipMemsetAsync(a + R, 0, 8, st));
+  if (R > 0)
+    hipLaunchKernelGGL(k_rows_plan, dim3(blocks_for(R, 4)), dim3(256), 0, st,
+                       D, fix, kind, lone, gen_n, out_q, out_v, kept, first_err);
+  HIP_TRY(hipGetLastError());
+  if ((rc = scan_excl(tmp, tmpb, gen_n, gen_base, R, st))) return rc;
+  HIP_TRY(hipMemcpyAsync(&c->h_small[0], gen_base + R, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const int64_t ncell = c->h_small[0];
+  if (ncell > 0) {
+    const size_t recb = ((size_t)ncell * sizeof(CellRec) + 255) & ~(size_t)255;
+    const size_t qb = ((size_t)ncell * 4 + 255) & ~(size_t)255;
+    rc = ensure(&c->rows_scr, &c->rows_scr_cap, recb + qb + (size_t)ncell * 9 + 256);
+    if (rc) return rc;
+    CellRec* rec = (CellRec*)c->rows_scr;
+    uint8_t* stq = (uint8_t*)c->rows_scr + recb;
+    uint8_t* stv = stq + qb;
+    hipLaunchKernelGGL(k_rows_general, dim3((unsigned)R), dim3(64), 0, st, D, fix,
+                       (const uint8_t*)kind, (const int64_t*)gen_base, rec, stq,
+                       stv, out_q, out_v, first_err);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipMemcpyAsync(&c->h_small[1], first_err, 8, hipMemcpyDeviceToHost, st));
+  if ((rc = scan_excl(tmp, tmpb, out_q, oq_off, R, st))) return rc;
+  if ((rc = scan_excl(tmp, tmpb, out_v, ov_off, R, st))) return rc;
+  if ((rc = scan_excl(tmp, tmpb, kept, k_off, R, st))) return rc;
+  HIP_TRY(hipMemcpyAsync(&c->h_small[2], oq_off + R, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_small[3], ov_off + R, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_small[4], k_off + R, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  rc = row_status(c, (unsigned long long)c->h_small[1], "storage");
+  if (rc) return rc;
+  const int64_t tq = c->h_small[2], tv = c->h_small[3], nk = c->h_small[4];
+  *n_out = nk;
+  if (qbytes) *qbytes = tq;
+  if (vbytes) *vbytes = tv;
+  if (own >= 0) {
+    if ((rc = cells_buffer(c, own, nk, tq, tv, owned))) return rc;
+    o = owned;
+    qcap = tq;
+    vcap = tv;
+  }
+  if (!o) return OTSDB_OK;  // sizes only
+  if (tq > qcap || tv > vcap)
+    return fail(OTSDB_E_CAPACITY, "compaction output: %lld qualifier / %lld "
+                "value bytes, capacity %lld / %lld", (long long)tq,
+                (long long)tv, (long long)qcap, (long long)vcap);
+  if (!o->row_base_s || !o->qual_off || !o->val_off || !o->qual || !o->val)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null output array");
+  CellRec* rec = (CellRec*)c->rows_scr;
+  const size_t recb = ((size_t)ncell * sizeof(CellRec) + 255) & ~(size_t)255;
+  const size_t qb = ((size_t)ncell * 4 + 255) & ~(size_t)255;
+  const uint8_t* stq = ncell ? (uint8_t*)c->rows_scr + recb : nullptr;
+  const uint8_t* stv = ncell ? stq + qb : nullptr;
+  (void)rec;
+  if (R > 0 && nk > 0) {
+    // row_series is optional on the output
+    hipLaunchKernelGGL(k_rows_write, dim3(blocks_for(R, 4)), dim3(256), 0, st,
+                       D, fix, raw->row_series, raw->row_base_s,
+                       (const uint8_t*)kind, (const int64_t*)lone,
+                       (const int64_t*)gen_base, stq, stv,
+                       (const int64_t*)out_q, (const int64_t*)out_v,
+                       (const int64_t*)oq_off, (const int64_t*)ov_off,
+                       (const int64_t*)k_off, o->row_series, o->row_base_s, o->qual_off, o->qual, o->val_off, o->val);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipMemcpyAsync(o->qual_off + nk, oq_off + R, 8, hipMemcpyDeviceToDevice, st));
+  HIP_TRY(hipMemcpyAsync(o->val_off + nk, ov_off + R, 8, hipMemcpyDeviceToDevice, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return OTSDB_OK;
+}
+
+// Span.addRow over every series' compacted rows (rows.hip).  *identity: no
+// series needed the replay (the output then equals the input and, when
+// o == nullptr, nothing is written).
+otsdb_status span_impl(otsdb_ctx* c, const otsdb_cells* in, int64_t S,
+                       const otsdb_cells_out* o, int64_t qcap, int64_t vcap,
+                       int64_t* n_out, int64_t* qbytes, int64_t* vbytes,
+                       bool* identity, hipStream_t st, int own = -1,
+                       otsdb_cells_out* owned = nullptr) {
+  const int64_t R = in->n_rows;
+  if (R < 0 || S < 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
+  CellsDev C{R, in->row_series, in->row_base_s, in->qual_off, in->qual,
+             in->val_off, in->val};
+  const size_t tmpb = scan_tmp_bytes(S, st);
+  const size_t A = ((size_t)(S + 1) * 8 + 255) & ~(size_t)255;
+  // series_row, slow, arena_sz, arena_off, o_rows, o_q, o_v, row_off, q_off,
+  // v_off, err word, scan temp
+  const size_t need = 10 * A + 256 + tmpb;
+  otsdb_status rc = ensure(&c->rows_ws, &c->rows_ws_cap, need);
+  if (rc) return rc;
+  char* w = (char*)c->rows_ws;
+  int64_t* series_row = (int64_t*)w;
+  uint8_t* slow = (uint8_t*)(w + A);
+  int64_t* arena_sz = (int64_t*)(w + 2 * A);
+  int64_t* arena_off = (int64_t*)(w + 3 * A);
+  int64_t* o_rows = (int64_t*)(w + 4 * A);
+  int64_t* o_q = (int64_t*)(w + 5 * A);
+  int64_t* o_v = (int64_t*)(w + 6 * A);
+  int64_t* row_off = (int64_t*)(w + 7 * A);
+  int64_t* q_off = (int64_t*)(w + 8 * A);
+  int64_t* v_off = (int64_t*)(w + 9 * A);
+  int* err = (int*)(w + 10 * A);
+  void* tmp = w + 10 * A + 256;
+  HIP_TRY(hipMemsetAsync(err, 0, 4, st));
+  for (int64_t* a : {arena_sz, o_rows, o_q, o_v})
+    HIP_TRY(hipMemsetAsync(a + S, 0, 8, st));
+  hipLaunchKernelGGL(k_series_rows, dim3(blocks_for(R + 1, 256)), dim3(256), 0,
+                     st, R, S, in->row_series, series_row);
+  if (S > 0)
+    hipLaunchKernelGGL(k_span_plan, dim3(blocks_for(S, 4)), dim3(256), 0, st, C,
+                       S, (const int64_t*)series_row, slow, arena_sz, o_rows,
+                       o_q, o_v, err);
+  HIP_TRY(hipGetLastError());
+  if ((rc = scan_excl(tmp, tmpb, arena_sz, arena_off, S, st))) return rc;
+  HIP_TRY(hipMemcpyAsync(&c->h_small[0], arena_off + S, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_small[1], err, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if ((int)(c->h_small[1] & 0xFFFFFFFF))
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "a row without a data point");
+  const int64_t arena = c->h_small[0];
+  *identity = arena == 0;
+  if (arena > 0) {
+    rc = ensure(&c->rows_scr, &c->rows_scr_cap, (size_t)arena + 256);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_span_replay, dim3((unsigned)S), dim3(64), 0, st, C, S,
+                       (const int64_t*)series_row, (const uint8_t*)slow,
+                       (const int64_t*)arena_off, (uint8_t*)c->rows_scr, o_rows,
+                       o_q, o_v);
+    HIP_TRY(hipGetLastError());
+  }
+  if ((rc = scan_excl(tmp, tmpb, o_rows, row_off, S, st))) return rc;
+  if ((rc = scan_excl(tmp, tmpb, o_q, q_off, S, st))) return rc;
+  if ((rc = scan_excl(tmp, tmpb, o_v, v_off, S, st))) return rc;
+  HIP_TRY(hipMemcpyAsync(&c->h_small[2], row_off + S, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_small[3], q_off + S, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_small[4], v_off + S, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  *n_out = c->h_small[2];
+  if (qbytes) *qbytes = c->h_small[3];
+  if (vbytes) *vbytes = c->h_small[4];
+  if (own >= 0) {
+    if (*identity) return OTSDB_OK;  // the input is the span order
+    if ((rc = cells_buffer(c, own, *n_out, c->h_small[3], c->h_small[4], owned)))
+      return rc;
+    o = owned;
+    qcap = c->h_small[3];
+    vcap = c->h_small[4];
+  }
+  if (!o) return OTSDB_OK;
+  if (c->h_small[3] > qcap || c->h_small[4] > vcap)
+    return fail(OTSDB_E_CAPACITY, "span output capacity");
+  if (S > 0)
+    hipLaunchKernelGGL(k_span_write, dim3(blocks_for(S, 4)), dim3(256), 0, st,
+                       C, S, (const int64_t*)series_row, (const uint8_t*)slow,
+                       (const int64_t*)arena_off, (const uint8_t*)c->rows_scr,
+                       (const int64_t*)row_off, (const int64_t*)q_off,
+                       (const int64_t*)v_off, o->row_series, o->row_base_s,
+                       o->qual_off, o->qual, o->val_off, o->val);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(o->qual_off + *n_out, q_off + S, 8,
+                         hipMemcpyDeviceToDevice, st));
+  HIP_TRY(hipMemcpyAsync(o->val_off + *n_out, v_off + S, 8,
+                         hipMemcpyDeviceToDevice, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return OTSDB_OK;
+}
+
+// a context-owned cells buffer for R rows, qb / vb bytes
+otsdb_status cells_buffer(otsdb_ctx* c, int which, int64_t R, int64_t qb,
+                          int64_t vb, otsdb_cells_out* o) {
+  const size_t a = ((size_t)(R + 1) * 8 + 255) & ~(size_t)255;
+  const size_t q = ((size_t)qb + 256) & ~(size_t)255;
+  const size_t v = ((size_t)vb + 256) & ~(size_t)255;
+  otsdb_status rc =
+      ensure(&c->raw_cells[which], &c->raw_cells_cap[which], 4 * a + q + v);
+  if (rc) return rc;
+  char* p = (char*)c->raw_cells[which];
+  o->row_series = (int64_t*)p;
+  o->row_base_s = (int64_t*)(p + a);
+  o->qual_off = (int64_t*)(p + 2 * a);
+  o->val_off = (int64_t*)(p + 3 * a);
+  o->qual = (uint8_t*)(p + 4 * a);
+  o->val = (uint8_t*)(p + 4 * a + q);
+  return OTSDB_OK;
+}
+
+// The query from storage rows: compaction -> span assembly -> the cells
+// query (DEVICE pointers).
+otsdb_status run_raw_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
+                          const otsdb_raw_rows* raw, int fix,
+                          const otsdb_batch* b, otsdb_result* out,
+                          std::vector<int64_t>& goff) {
+  hipStream_t st = c->stream;
+  if (!raw->row_series) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null row_series");
+  int64_t nk = 0, tq = 0, tv = 0;
+  otsdb_cells_out co;
+  otsdb_status rc =
+      compact_impl(c, raw, fix, nullptr, 0, 0, &nk, &tq, &tv, st, 0, &co);
+  if (rc) return rc;
+  otsdb_cells cc{nk, co.row_series, co.row_base_s, co.qual_off, co.qual,
+                 co.val_off, co.val};
+  int64_t ns = 0, sq = 0, sv = 0;
+  bool identity = true;
+  otsdb_cells_out so;
+  rc = span_impl(c, &cc, b->n_series, nullptr, 0, 0, &ns, &sq, &sv, &identity,
+                 st, 1, &so);
+  if (rc) return rc;
+  if (!identity)
+    cc = otsdb_cells{ns, so.row_series, so.row_base_s, so.qual_off, so.qual,
+                     so.val_off, so.val};
+  return run_cells_impl(c, spec, &cc, b, out, goff);
+}
+
 }  // namespace
 
 // =========================================================================
@@ -1319,6 +1623,11 @@ void otsdb_ctx_destroy(otsdb_ctx* c) {
   if (c->cal) hipFree(c->cal);
   if (c->cells_ws) hipFree(c->cells_ws);
   if (c->cells_col) hipFree(c->cells_col);
+  if (c->rows_ws) hipFree(c->rows_ws);
+  if (c->rows_scr) hipFree(c->rows_scr);
+  for (void* p : c->raw_cells)
+    if (p) hipFree(p);
+  if (c->raw_stage) hipFree(c->raw_stage);
   if (c->d_tiles) hipFree(c->d_tiles);
   if (c->d_err) hipFree(c->d_err);
   for (auto e : c->ev_pool) hipEventDestroy(e);
@@ -1732,6 +2041,159 @@ otsdb_status otsdb_encode_cells_device(otsdb_ctx* c, const otsdb_batch* b,
                        o ? o->qual_off : nullptr, o ? o->val_off : nullptr,
                        o ? o->qual : nullptr, o ? o->val : nullptr);
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(st));
+  return OTSDB_OK;
+}
+
+otsdb_status otsdb_compact_rows_device(otsdb_ctx* c, const otsdb_raw_rows* raw,
+                                       int32_t fix_duplicates,
+                                       const otsdb_cells_out* out,
+                                       int64_t qual_capacity,
+                                       int64_t val_capacity, int64_t* n_out_rows,
+                                       void* hip_stream) {
+  if (!c || !raw || !n_out_rows) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  return compact_impl(c, raw, fix_duplicates != 0, out, qual_capacity,
+                      val_capacity, n_out_rows, nullptr, nullptr, st);
+}
+
+otsdb_status otsdb_span_assemble_device(otsdb_ctx* c, const otsdb_cells* cells,
+                                        int64_t n_series,
+                                        const otsdb_cells_out* out,
+                                        int64_t qual_capacity,
+                                        int64_t val_capacity,
+                                        int64_t* n_out_rows, void* hip_stream) {
+  if (!c || !cells || !n_out_rows) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  if (out && !out->row_series)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null output row_series");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
+  bool identity = true;
+  return span_impl(c, cells, n_series, out, qual_capacity, val_capacity,
+                   n_out_rows, nullptr, nullptr, &identity, st);
+}
+
+otsdb_status otsdb_agg_run_raw_device(otsdb_ctx* c, const otsdb_query_spec* spec,
+                                      const otsdb_raw_rows* raw,
+                                      int32_t fix_duplicates,
+                                      const otsdb_batch* b, otsdb_result* out,
+                                      void* hip_stream) {
+  if (!c || !spec || !raw || !b || !out)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  StreamBinding bind(c, hip_stream);
+  std::vector<int64_t> goff;
+  otsdb_status rc = read_goff(c, b, true, goff);
+  if (!rc) rc = check_spec(spec);
+  if (!rc) rc = run_raw_impl(c, spec, raw, fix_duplicates != 0, b, out, goff);
+  return rc;
+}
+
+otsdb_status otsdb_agg_run_raw(otsdb_ctx* c, const otsdb_query_spec* spec,
+                               const otsdb_raw_rows* raw, int32_t fix_duplicates,
+                               const otsdb_batch* b, otsdb_result* out) {
+  if (!c || !spec || !raw || !b || !out)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  otsdb_status rc = check_spec(spec);
+  if (rc) return rc;
+  std::vector<int64_t> goff;
+  if ((rc = read_goff(c, b, false, goff))) return rc;
+  const int64_t R = raw->n_rows, S = b->n_series, G = b->n_groups;
+  if (R < 0 || S < 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
+  if (!raw->row_series || !raw->row_base_s || !raw->row_col_off ||
+      !raw->col_qual_off || !raw->col_val_off)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null raw row array");
+  const int64_t M = goff.back();
+  for (int64_t r = 0; r < R; ++r)
+    if (raw->row_series[r] < 0 || raw->row_series[r] >= S ||
+        (r && raw->row_series[r] < raw->row_series[r - 1]))
+      return fail(OTSDB_E_ILLEGAL_ARGUMENT,
+                  "row_series must be nondecreasing series indices");
+  for (int64_t m = 0; m < M; ++m)
+    if (b->group_members[m] < 0 || b->group_members[m] >= S)
+      return fail(OTSDB_E_ILLEGAL_ARGUMENT, "group member out of range");
+  const int64_t C = raw->row_col_off[R];
+  const int64_t QB = raw->col_qual_off[C], VB = raw->col_val_off[C];
+  const int64_t cap = out->capacity;
+  auto carve = [&](char* base) {
+    Carve cv{base};
+    void* p[14];
+    p[0] = cv.take<int64_t>(R + 1);
+    p[1] = cv.take<int64_t>(R + 1);
+    p[2] = cv.take<int64_t>(R + 1);
+    p[3] = cv.take<int64_t>(C + 1);
+    p[4] = cv.take<uint8_t>(QB + 16);
+    p[5] = cv.take<int64_t>(C + 1);
+    p[6] = cv.take<uint8_t>(VB + 16);
+    p[7] = raw->col_ts ? cv.take<int64_t>(C + 1) : nullptr;
+    p[8] = cv.take<int64_t>(G + 1);
+    p[9] = cv.take<int64_t>(M + 1);
+    p[10] = cv.take<int64_t>(G + 1);
+    p[11] = cv.take<int64_t>(cap + 1);
+    p[12] = cv.take<int64_t>(cap + 1);
+    p[13] = cv.take<uint8_t>(cap + 1);
+    return std::make_pair(cv.off + 256, std::vector<void*>(p, p + 14));
+  };
+  rc = ensure(&c->raw_stage, &c->raw_stage_cap, carve(nullptr).first);
+  if (rc) return rc;
+  auto pp = carve((char*)c->raw_stage).second;
+  hipStream_t st = c->stream;
+  auto h2d = [&](void* d, const void* h, size_t n) -> otsdb_status {
+    if (n && h) HIP_TRY(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, st));
+    return OTSDB_OK;
+  };
+  if ((rc = h2d(pp[0], raw->row_series, 8 * R)) ||
+      (rc = h2d(pp[1], raw->row_base_s, 8 * R)) ||
+      (rc = h2d(pp[2], raw->row_col_off, 8 * (R + 1))) ||
+      (rc = h2d(pp[3], raw->col_qual_off, 8 * (C + 1))) ||
+      (rc = h2d(pp[4], raw->qual, QB)) ||
+      (rc = h2d(pp[5], raw->col_val_off, 8 * (C + 1))) ||
+      (rc = h2d(pp[6], raw->val, VB)) ||
+      (rc = h2d(pp[7], raw->col_ts, 8 * C)) ||
+      (rc = h2d(pp[8], b->group_offsets, 8 * (G + 1))) ||
+      (rc = h2d(pp[9], b->group_members, 8 * M)))
+    return rc;
+  otsdb_raw_rows dr{R,
+                    (const int64_t*)pp[0],
+                    (const int64_t*)pp[1],
+                    (const int64_t*)pp[2],
+                    (const int64_t*)pp[3],
+                    (const uint8_t*)pp[4],
+                    (const int64_t*)pp[5],
+                    (const uint8_t*)pp[6],
+                    (const int64_t*)pp[7]};
+  otsdb_batch db = *b;
+  db.n_points = 0;
+  db.offsets = nullptr;
+  db.ts_ms = nullptr;
+  db.val = nullptr;
+  db.is_float = nullptr;
+  db.series_float = nullptr;
+  db.group_offsets = (const int64_t*)pp[8];
+  db.group_members = (const int64_t*)pp[9];
+  otsdb_result dres;
+  dres.capacity = cap;
+  dres.offsets = (int64_t*)pp[10];
+  dres.ts = (int64_t*)pp[11];
+  dres.val = (int64_t*)pp[12];
+  dres.is_int = (uint8_t*)pp[13];
+  rc = run_raw_impl(c, spec, &dr, fix_duplicates != 0, &db, &dres, goff);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out->offsets, dres.offsets, 8 * (G + 1),
+                         hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const int64_t total = out->offsets[G];
+  if (total > 0) {
+    HIP_TRY(hipMemcpyAsync(out->ts, dres.ts, 8 * total, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(out->val, dres.val, 8 * total, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(out->is_int, dres.is_int, total, hipMemcpyDeviceToHost, st));
+  }
   HIP_TRY(hipStreamSynchronize(st));
   return OTSDB_OK;
 }

@@ -490,7 +490,7 @@ template <class M, int K, int DPP>
 DEV void reduce_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
                      int64_t hi, int64_t base, int64_t i0, const int64_t* t,
                      const int64_t* v, RowSink& S, int& err,
-                     int& carry_key, M& carry) {
+                     int& carry_key, M& carry, bool keep_open = false) {
   constexpr int PTS = 64 * K;
   const int lane = LANE;
   // ---- lane-local sequential fold (range checks only on the first and
@@ -533,6 +533,19 @@ DEV void reduce_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
     head_key = cur_key;
   } else if (nseg == 1) {
     head_key = cur_key;
+  }
+  if (keep_open) {
+    // more points may follow in a later call (the next storage row of the
+    // series): lanes past hi continue the last lane with points, so its
+    // bucket stays open and becomes the carry instead of being written
+    const uint64_t real = __ballot(nseg > 0);
+    const uint64_t below = real & ((1ULL << lane) - 1);
+    const int src = below ? 63 - __builtin_clzll(below) : lane;
+    const int k = __shfl(cur_key, src);
+    if (nseg == 0 && i0 >= lo && below) {
+      cur_key = k;
+      head_key = k;
+    }
   }
   // ---- previous step's open bucket
   if (lane == 0) {

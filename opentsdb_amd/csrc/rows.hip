@@ -1,0 +1,1239 @@
+// rows.hip — storage rows -> compacted columns -> spans.
+//
+// Query-time compaction.  The scanner hands every storage row to
+// CompactionQueue.compact (TSDB.compact, SaltScanner.java:849-881): the row's
+// columns — single-point cells, compacted columns, append columns (0x05),
+// annotations (0x01), histograms (0x06) — become ONE compacted column, the
+// form RowSeq reads.  Rules restated (oracle/otsdb_oracle.c or_compact_row
+// follows the same lines):
+//   * buildHeapProcessAnnotations (CompactionQueue.java:435-489): odd-length
+//     qualifiers are not data (append columns are parsed, the rest skipped);
+//     every data column becomes a ColumnDatapointIterator whose 2-byte
+//     single cells get the legacy fix-ups (ColumnDatapointIterator.java:73-87:
+//     8-byte "float" values whose high half is zero become 4-byte floats,
+//     Internal.fixFloatingPointValue :577-591; the qualifier's length bits are
+//     rewritten to the value length, Internal.fixQualifierFlags :535-545);
+//   * AppendDataPoints.parseKeyValue (AppendDataPoints.java:118-236): the
+//     (qualifier, value) pairs of an append column, keyed by time offset in a
+//     TreeMap — the later of equal offsets replaces the earlier — and emitted
+//     in offset order; a value that does not break down is
+//     IllegalDataException, a qualifier that is not exactly {0x05,0,0} is
+//     IllegalArgumentException;
+//   * noMergesOrFixups (:317-332): one heaped column holding one 2-byte cell
+//     that needs no fix-up, or one 4-byte ms cell, is returned as stored;
+//   * defaultMergeDataPoints (:549-584): the iterators pop from a
+//     PriorityQueue ordered by (time offset, newer HBase cell first,
+//     ColumnDatapointIterator.compareTo :192-199); the first cell of an offset
+//     is kept, later ones are compared with it and, when their bytes differ,
+//     raise IllegalDataException unless tsd.storage.fix_duplicates;
+//   * buildCompactedColumn (:594-616): one meta byte after the values of a
+//     multi-value column, bit 0 = seconds and ms cells mixed.
+// When every column's cells are in offset order (what the write path and
+// compaction produce) the heap order IS the stable sort by (offset, column
+// rank, position), rank = (HBase timestamp desc, column index desc), so a
+// wavefront sorts the row's cell keys in LDS (bitonic) and keeps the first of
+// each offset.  A row holding a column whose cells go back in time takes an
+// exact emulation of the heap (wave arg-min over the column heads per step).
+//
+// Kernels (one wavefront per storage row):
+//   k_rows_plan     classifies the row: EMPTY (no data point: dropped, like
+//                   the scanner drops a null compaction), VERBATIM (the
+//                   noMergesOrFixups case), LONE (one data column: its cells
+//                   in column order, consecutive equal offsets merged — a
+//                   one-iterator heap), or GENERAL (several columns or an
+//                   append column: cell count for the scratch records);
+//                   LONE/VERBATIM output sizes; construction errors in
+//                   column order;
+//   k_rows_general  GENERAL rows: cell records -> sort (or heap emulation) ->
+//                   merged column in a staging area;
+//   k_rows_write    packs every kept row at its scanned output offsets.
+//
+// Span assembly (Span.addRow, Span.java:177-220; RowSeq.addRow,
+// RowSeq.java:91-222; checkRowOrder :387-392): a series whose rows arrive
+// with strictly increasing base times (what one scanner delivers) is its
+// rows, unchanged.  Any other series (a row key seen twice, rows out of
+// order) is replayed exactly by one lane: the merge into the first RowSeq of
+// the same key when the row's first point is not after the last RowSeq's last
+// point (two-pointer merge by offset, the incoming duplicate dropped, meta
+// byte = OR of the two last bytes' bit 0), a new RowSeq otherwise, then the
+// stable sort by base time.  RowSeq.size / timestamp(i) read the mixed bit
+// from the last value byte exactly as the reference does (:338-420).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace otsdb {
+
+#ifndef OTSDB_DS_TU
+
+struct RawDev {
+  int64_t R;
+  const int64_t* row_col_off;  // [R+1]
+  const int64_t* col_qoff;     // [C+1]
+  const uint8_t* qual;
+  const int64_t* col_voff;     // [C+1]
+  const uint8_t* val;
+  const int64_t* col_ts;       // [C] or null (= column index)
+};
+
+// row status codes (otsdb_status values)
+enum : int { RS_ILLEGAL_DATA = 1, RS_ILLEGAL_ARGUMENT = 3, RS_UNSUPPORTED = 5 };
+enum : uint8_t { RK_EMPTY = 0, RK_VERBATIM = 1, RK_LONE = 2, RK_GENERAL = 3 };
+// column types
+enum : int { CT_SKIP = 0, CT_APPEND = 1, CT_ONE = 2, CT_MULTI = 3 };
+
+constexpr int kRowCellCap = 8192;  // GENERAL rows: cells sorted in LDS
+constexpr int kRowColCap = 4096;   // GENERAL rows: data columns ranked in LDS
+
+// one cell of a GENERAL row (scratch), 32 bytes
+struct CellRec {
+  int64_t qpos;   // qualifier bytes: index into qual (or val, RF_QINVAL)
+  int64_t vpos;   // value bytes: index into val
+  int32_t off;    // time offset, ms
+  int32_t col;    // column rank in the row
+  uint8_t ql, vl; // qualifier / value length of the point
+  uint8_t vav;    // value bytes present in the column (<= vl)
+  uint8_t flags;  // RF_*
+  uint8_t qfix;   // fixed second qualifier byte (RF_QFIX)
+  uint8_t pad[7];
+};
+enum : uint8_t {
+  RF_QFIX = 1, RF_QINVAL = 2, RF_MS = 4, RF_APPEND = 8, RF_OVERRUN = 16
+};
+
+DEV void row_error(unsigned long long* first_err, int64_t r, int code) {
+  atomicMin(first_err, ((unsigned long long)r << 8) | (unsigned)code);
+}
+
+DEV int32_t qual_off_ms(uint32_t qv, int ms) {
+  return ms ? (int32_t)((qv & 0x0FFFFFC0u) >> 6)
+            : (int32_t)((qv & 0xFFFFu) >> 4) * 1000;
+}
+
+DEV int lane_prev(uint64_t mask, int lane) {  // highest set bit below lane
+  const uint64_t m = mask & ((1ULL << lane) - 1);
+  return m ? 63 - __builtin_clzll(m) : -1;
+}
+DEV int lane_last_le(uint64_t mask, int lane) {  // highest set bit <= lane
+  const uint64_t m = lane == 63 ? mask : mask & ((2ULL << lane) - 1);
+  return m ? 63 - __builtin_clzll(m) : -1;
+}
+
+DEV int64_t wave_incl_scan(int64_t x) {
+  const int lane = LANE;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+DEV int64_t wave_sum_l(int64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+  return x;
+}
+
+DEV void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// AppendDataPoints.parseKeyValue's first loop: the number of (qualifier,
+// value) pairs, or -1 when the bytes do not break down
+DEV int64_t append_count(const uint8_t* v, int64_t vl) {
+  int64_t n = 0, i = 0;
+  while (i < vl) {
+    const int ql = (v[i] & 0xF0) == 0xF0 ? 4 : 2;
+    if (i + ql > vl) return -1;
+    i += ql + (v[i + ql - 1] & 0x7) + 1;
+    if (i > vl) return -1;
+    ++n;
+  }
+  return n;
+}
+
+// checkForFixup on a 2-byte cell: the fixed second qualifier byte and the
+// value bytes after the float fix (vskip = 4 when the high half is dropped);
+// bad = the high half is not zero
+DEV uint8_t fixup2(uint8_t f, const uint8_t* v, int64_t vl, int& vskip,
+                   int& bad) {
+  vskip = 0;
+  bad = 0;
+  if ((f & 0x8) && (f & 0x7) == 0x3 && vl == 8) {
+    if (v[0] | v[1] | v[2] | v[3]) bad = 1;
+    vskip = 4;
+  }
+  return (uint8_t)((f & ~0x7) | ((vl - vskip - 1) & 0xFF));
+}
+
+struct ColInfo {
+  int type;     // CT_*
+  int err;      // construction error (RS_*), 0 if none
+  int64_t cells;  // CT_ONE: 1, CT_APPEND: pairs, CT_MULTI: -1 (walk)
+  int fixed;    // CT_ONE 2-byte: checkForFixup changes the cell
+};
+
+// One column as buildHeapProcessAnnotations + the iterator constructor see
+// it (lane-level)
+DEV ColInfo col_info(const RawDev& D, int64_t c) {
+  ColInfo ci{CT_SKIP, 0, 0, 0};
+  const int64_t qo = D.col_qoff[c], ql = D.col_qoff[c + 1] - qo;
+  const int64_t vo = D.col_voff[c], vl = D.col_voff[c + 1] - vo;
+  if (ql == 0) return ci;
+  const uint8_t* q = D.qual + qo;
+  if (ql & 1) {
+    if (q[0] != 0x05) return ci;  // annotation / histogram / unknown
+    if (ql != 3) {
+      ci.err = RS_ILLEGAL_ARGUMENT;
+      return ci;
+    }
+    const int64_t n = append_count(D.val + vo, vl);
+    if (n < 0) ci.err = RS_ILLEGAL_DATA;
+    else if (n > 0) {
+      ci.type = CT_APPEND;
+      ci.cells = n;
+    }
+    return ci;
+  }
+  // a data column: no value bytes, or a first qualifier running past the
+  // column, is a corrupt cell (see the oracle)
+  if (vl == 0) {
+    ci.err = RS_ILLEGAL_DATA;
+    return ci;
+  }
+  const bool ms0 = (q[0] & 0xF0) == 0xF0;
+  if (ms0 && ql < 4) {
+    ci.err = RS_ILLEGAL_DATA;
+    return ci;
+  }
+  if (ql == 2) {
+    int vskip, bad;
+    const uint8_t nf = fixup2(q[1], D.val + vo, vl, vskip, bad);
+    if (bad) {
+      ci.err = RS_ILLEGAL_DATA;
+      return ci;
+    }
+    ci.type = CT_ONE;
+    ci.cells = 1;
+    ci.fixed = vskip != 0 || nf != q[1];
+    return ci;
+  }
+  if (ql == 4 && ms0) {
+    ci.type = CT_ONE;
+    ci.cells = 1;
+    return ci;
+  }
+  ci.type = CT_MULTI;
+  ci.cells = -1;
+  return ci;
+}
+
+// Wave walk over the points of one compacted column in column order
+// (ColumnDatapointIterator.update/advance :167-187): point starts are a scan
+// of the 2-/4-byte qualifier widths over 2-byte units (fmap recurrence of
+// decode.hip), value offsets a scan of the lengths; the column ends at the
+// first point whose value offset is past the value bytes.  A 4-byte
+// qualifier cut by the column end, when reached, is an error (trunc).
+struct ColWalk {
+  const uint8_t* q;
+  int64_t units, vlen;
+  int64_t u0 = 0, carry_n = 0, carry_vo = 0;
+  int carry_start = 1;
+  bool done = false;
+  // per-lane point of the current chunk
+  bool cell;
+  int ms, ql, vl, trunc;
+  int32_t off;
+  int64_t k, qo, vo;
+  uint64_t mask;
+
+  DEV ColWalk(const uint8_t* q_, int64_t qlen, int64_t vlen_)
+      : q(q_), units(qlen >> 1), vlen(vlen_) {}
+
+  DEV bool step() {
+    if (done || u0 >= units) return false;
+    const int lane = LANE;
+    const int64_t u = u0 + lane;
+    const bool in = u < units;
+    const uint8_t b0 = in ? q[2 * u] : 0;
+    const int msu = in && ((b0 & 0xF0) == 0xF0);
+    int F = in ? (msu ? 0x1 : 0x3) : 0x2;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int g = __shfl_up(F, d);
+      if (lane >= d) F = fmap_compose(F, g);
+    }
+    int Fex = __shfl_up(F, 1);
+    if (lane == 0) Fex = 0x2;
+    const int start = in && fmap_apply(Fex, carry_start);
+    const int tr = start && msu && (u + 1 >= units);
+    uint32_t qv = 0;
+    if (start && !tr)
+      qv = msu ? ((uint32_t)b0 << 24) | ((uint32_t)q[2 * u + 1] << 16) |
+                     ((uint32_t)q[2 * u + 2] << 8) | (uint32_t)q[2 * u + 3]
+               : ((uint32_t)b0 << 8) | (uint32_t)q[2 * u + 1];
+    const int l = (start && !tr) ? (int)(qv & 0x7) + 1 : 0;
+    const int64_t incl = wave_incl_scan(l);
+    vo = carry_vo + incl - l;
+    const bool reach = start && vo < vlen;
+    trunc = reach && tr;
+    cell = reach && !tr;
+    if (__ballot(start && (vo >= vlen || tr))) done = true;
+    mask = __ballot(cell);
+    k = carry_n + __popcll(mask & ((1ULL << lane) - 1));
+    ms = msu;
+    ql = msu ? 4 : 2;
+    vl = l;
+    qo = 2 * u;
+    off = qual_off_ms(qv, msu);
+    carry_n += __popcll(mask);
+    carry_vo += __shfl(incl, 63);
+    carry_start = fmap_apply(__shfl(F, 63), carry_start);
+    u0 += 64;
+    return true;
+  }
+};
+
+DEV bool bytes_equal_padded(const uint8_t* val, int64_t a, int la, int aav,
+                            int64_t b, int lb, int bav) {
+  if (la != lb) return false;
+  for (int i = 0; i < la; ++i) {
+    const uint8_t x = i < aav ? val[a + i] : 0;
+    const uint8_t y = i < bav ? val[b + i] : 0;
+    if (x != y) return false;
+  }
+  return true;
+}
+
+struct LoneOut {
+  int64_t nq, nv, kept;
+  int err;
+};
+
+// A row with one data column: the one-iterator heap.  Points in column
+// order; a point whose offset equals the previous point's is a duplicate of
+// the run's first (kept) point — compared byte for byte (Arrays.copyOfRange:
+// zero-padded past the column) and an error unless fix_duplicates.  WRITE:
+// the kept points' bytes go to oq / ov.
+template <bool WRITE>
+DEV LoneOut lone_walk(const RawDev& D, int64_t c, int fix, uint8_t* oq,
+                      uint8_t* ov) {
+  const int lane = LANE;
+  LoneOut o{0, 0, 0, 0};
+  const int64_t qb = D.col_qoff[c], ql = D.col_qoff[c + 1] - qb;
+  const int64_t vb = D.col_voff[c], vl = D.col_voff[c + 1] - vb;
+  const uint8_t* q = D.qual + qb;
+  if (ql == 2) {  // a fixed-up single cell (the unfixed one is VERBATIM)
+    int vskip, bad;
+    const uint8_t nf = fixup2(q[1], D.val + vb, vl, vskip, bad);
+    const int cur = (nf & 0x7) + 1;
+    if (cur > vl - vskip) {
+      o.err = RS_ILLEGAL_DATA;
+      return o;
+    }
+    o.nq = 2;
+    o.nv = cur;
+    o.kept = 1;
+    if (WRITE && lane == 0) {
+      oq[0] = q[0];
+      oq[1] = nf;
+      for (int i = 0; i < cur; ++i) ov[i] = D.val[vb + vskip + i];
+    }
+    return o;
+  }
+  ColWalk w(q, ql, vl);
+  bool have_prev = false;
+  int32_t prev_off = 0;
+  int64_t lvo = 0;  // the current run's kept point
+  int lvl = 0, lvav = 0;
+  int ms_in = 0, s_in = 0, bad = 0;
+  while (w.step()) {
+    const uint64_t m = w.mask;
+    if (w.trunc) bad = 1;
+    const int pl = lane_prev(m, lane);
+    int32_t poff = __shfl(w.off, pl < 0 ? 0 : pl);
+    const bool hp = pl >= 0 || have_prev;
+    if (pl < 0) poff = prev_off;
+    const bool dup = w.cell && hp && w.off == poff;
+    const bool lead = w.cell && !dup;
+    const int vav = (int)(w.vo + w.vl <= vl ? w.vl : vl - w.vo);
+    const uint64_t lm = __ballot(lead);
+    const int ll = lane_last_le(lm, lane);
+    int64_t rvo = __shfl(w.vo, ll < 0 ? 0 : ll);
+    int rvl = __shfl(w.vl, ll < 0 ? 0 : ll);
+    int rvav = __shfl(vav, ll < 0 ? 0 : ll);
+    if (ll < 0) {
+      rvo = lvo;
+      rvl = lvl;
+      rvav = lvav;
+    }
+    if (dup && !fix &&
+        !bytes_equal_padded(D.val, vb + w.vo, w.vl, vav, vb + rvo, rvl, rvav))
+      bad = 1;
+    if (lead && w.vo + w.vl > vl) bad = 1;  // a kept value past the column
+    const int64_t kq = lead ? w.ql : 0, kv = lead ? w.vl : 0;
+    const int64_t iq = wave_incl_scan(kq), iv = wave_incl_scan(kv);
+    if (WRITE && lead && !bad) {
+      uint8_t* dq = oq + o.nq + iq - kq;
+      uint8_t* dv = ov + o.nv + iv - kv;
+      for (int i = 0; i < w.ql; ++i) dq[i] = q[w.qo + i];
+      for (int i = 0; i < w.vl; ++i) dv[i] = D.val[vb + w.vo + i];
+    }
+    ms_in |= __ballot(lead && w.ms) != 0;
+    s_in |= __ballot(lead && !w.ms) != 0;
+    o.nq += __shfl(iq, 63);
+    o.nv += __shfl(iv, 63);
+    o.kept += __popcll(lm);
+    if (m) {
+      const int last = 63 - __builtin_clzll(m);
+      prev_off = __shfl(w.off, last);
+      have_prev = true;
+    }
+    if (lm) {
+      const int last = 63 - __builtin_clzll(lm);
+      lvo = __shfl(w.vo, last);
+      lvl = __shfl(w.vl, last);
+      lvav = __shfl(vav, last);
+    }
+    if (__ballot(bad)) {
+      o.err = RS_ILLEGAL_DATA;
+      return o;
+    }
+  }
+  if (o.kept > 1) {
+    if (WRITE && lane == 0) ov[o.nv] = (ms_in && s_in) ? 1 : 0;
+    o.nv += 1;
+  }
+  return o;
+}
+
+// ---------------------------------------------------------------- planning
+__global__ __launch_bounds__(256) void k_rows_plan(
+    RawDev D, int fix, uint8_t* __restrict__ kind, int64_t* __restrict__ lone,
+    int64_t* __restrict__ gen_n, int64_t* __restrict__ out_q,
+    int64_t* __restrict__ out_v, int64_t* __restrict__ kept,
+    unsigned long long* first_err) {
+  const int lane = LANE;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= D.R) return;
+  const int64_t c0 = D.row_col_off[r], c1 = D.row_col_off[r + 1];
+  int64_t n_data = 0, cells = 0, first_c = -1;
+  int first_type = CT_SKIP, first_fixed = 0, merge_bad = 0;
+  int err = 0;
+  for (int64_t cc = c0; cc < c1; cc += 64) {
+    const int64_t c = cc + lane;
+    ColInfo ci{CT_SKIP, 0, 0, 0};
+    if (c < c1) ci = col_info(D, c);
+    const uint64_t em = __ballot(ci.err != 0);
+    if (em) {  // the first failing column in column order
+      err = __shfl(ci.err, __builtin_ctzll(em));
+      break;
+    }
+    const uint64_t dm = __ballot(ci.type != CT_SKIP);
+    if (dm && first_c < 0) {
+      const int fl = __builtin_ctzll(dm);
+      first_c = cc + fl;
+      first_type = __shfl(ci.type, fl);
+      first_fixed = __shfl(ci.fixed, fl);
+    }
+    n_data += __popcll(dm);
+    cells += wave_sum_l(ci.type == CT_ONE || ci.type == CT_APPEND ? ci.cells : 0);
+    uint64_t mm = __ballot(ci.type == CT_MULTI);
+    // multi-point columns: counted by a wave walk (GENERAL rows only need
+    // the count; a lone column is walked below)
+    while (mm) {
+      const int b = __builtin_ctzll(mm);
+      mm &= mm - 1;
+      const int64_t col = cc + b;
+      const int64_t qb = D.col_qoff[col], vb = D.col_voff[col];
+      ColWalk w(D.qual + qb, D.col_qoff[col + 1] - qb, D.col_voff[col + 1] - vb);
+      int64_t n = 0;
+      while (w.step()) {
+        if (__ballot(w.trunc)) merge_bad = 1;
+        n += __popcll(w.mask);
+      }
+      cells += n;
+    }
+  }
+  auto put = [&](uint8_t k, int64_t nq, int64_t nv, int64_t g) {
+    if (lane == 0) {
+      kind[r] = k;
+      lone[r] = first_c;
+      gen_n[r] = g;
+      out_q[r] = nq;
+      out_v[r] = nv;
+      kept[r] = (k == RK_EMPTY) ? 0 : 1;
+    }
+  };
+  if (err) {
+    if (lane == 0) row_error(first_err, r, err);
+    put(RK_EMPTY, 0, 0, 0);
+    return;
+  }
+  if (n_data == 0) {
+    put(RK_EMPTY, 0, 0, 0);
+    return;
+  }
+  if (n_data == 1 && first_type != CT_APPEND) {
+    const int64_t ql = D.col_qoff[first_c + 1] - D.col_qoff[first_c];
+    const int64_t vl = D.col_voff[first_c + 1] - D.col_voff[first_c];
+    if (first_type == CT_ONE && !first_fixed) {  // noMergesOrFixups
+      put(RK_VERBATIM, ql, vl, 0);
+      return;
+    }
+    const LoneOut o = lone_walk<false>(D, first_c, fix, nullptr, nullptr);
+    if (o.err) {
+      if (lane == 0) row_error(first_err, r, o.err);
+      put(RK_EMPTY, 0, 0, 0);
+      return;
+    }
+    put(o.kept ? RK_LONE : RK_EMPTY, o.nq, o.nv, 0);
+    return;
+  }
+  if (merge_bad) {
+    if (lane == 0) row_error(first_err, r, RS_ILLEGAL_DATA);
+    put(RK_EMPTY, 0, 0, 0);
+    return;
+  }
+  if (cells > kRowCellCap || n_data > kRowColCap) {
+    if (lane == 0) row_error(first_err, r, RS_UNSUPPORTED);
+    put(RK_EMPTY, 0, 0, 0);
+    return;
+  }
+  put(RK_GENERAL, 0, 0, cells);
+}
+
+// ---------------------------------------------------------- GENERAL rows
+union GenLds {
+  uint64_t keys[kRowCellCap];
+  struct {
+    int64_t ts[kRowColCap];
+    int32_t cidx[kRowColCap];
+    int32_t base[kRowColCap + 1];
+  } col;
+  struct {
+    int32_t hoff[kRowColCap];
+    int32_t head[kRowColCap];
+    int32_t end[kRowColCap];
+  } hp;
+};
+
+DEV void write_cell(const RawDev& D, const CellRec& x, uint8_t* dq,
+                    uint8_t* dv) {
+  const uint8_t* qs = (x.flags & RF_QINVAL) ? D.val : D.qual;
+  for (int i = 0; i < x.ql; ++i)
+    dq[i] = (i == 1 && (x.flags & RF_QFIX)) ? x.qfix : qs[x.qpos + i];
+  for (int i = 0; i < x.vl; ++i) dv[i] = D.val[x.vpos + i];
+}
+
+__global__ __launch_bounds__(64) void k_rows_general(
+    RawDev D, int fix, const uint8_t* __restrict__ kind,
+    const int64_t* __restrict__ gen_base, CellRec* __restrict__ rec,
+    uint8_t* __restrict__ stq, uint8_t* __restrict__ stv,
+    int64_t* __restrict__ out_q, int64_t* __restrict__ out_v,
+    unsigned long long* first_err) {
+  __shared__ GenLds sm;
+  const int lane = LANE;
+  const int64_t r = blockIdx.x;
+  if (r >= D.R || kind[r] != RK_GENERAL) return;
+  const int64_t gb = gen_base[r];
+  CellRec* R = rec + gb;
+  uint8_t* sq = stq + 4 * gb;
+  uint8_t* sv = stv + 9 * gb;
+  const int64_t c0 = D.row_col_off[r], c1 = D.row_col_off[r + 1];
+  // 1. data columns in column order: HBase timestamp, index, point count
+  int k = 0;
+  for (int64_t cc = c0; cc < c1; cc += 64) {
+    const int64_t c = cc + lane;
+    ColInfo ci{CT_SKIP, 0, 0, 0};
+    if (c < c1) ci = col_info(D, c);
+    const uint64_t dm = __ballot(ci.type != CT_SKIP);
+    const int slot = k + __popcll(dm & ((1ULL << lane) - 1));
+    if (ci.type != CT_SKIP) {
+      sm.col.ts[slot] = D.col_ts ? D.col_ts[c] : c;
+      sm.col.cidx[slot] = (int32_t)(c - c0);
+      sm.col.base[slot] = (int32_t)(ci.type == CT_MULTI ? 0 : ci.cells);
+    }
+    uint64_t mm = __ballot(ci.type == CT_MULTI);
+    while (mm) {
+      const int b = __builtin_ctzll(mm);
+      mm &= mm - 1;
+      const int64_t col = cc + b;
+      const int64_t qb = D.col_qoff[col], vb = D.col_voff[col];
+      ColWalk w(D.qual + qb, D.col_qoff[col + 1] - qb, D.col_voff[col + 1] - vb);
+      int64_t n = 0;
+      while (w.step()) n += __popcll(w.mask);
+      if (lane == 0) sm.col.base[k + __popcll(dm & ((1ULL << b) - 1))] = (int32_t)n;
+    }
+    k += __popcll(dm);
+  }
+  int k2 = 1;
+  while (k2 < k) k2 <<= 1;
+  for (int i = k + lane; i < k2; i += 64) {
+    sm.col.ts[i] = INT64_MIN;
+    sm.col.cidx[i] = INT32_MIN;
+    sm.col.base[i] = 0;
+  }
+  wave_sync();
+  // 2. column rank: bitonic sort by (timestamp desc, index desc)
+  for (int kk = 2; kk <= k2; kk <<= 1)
+    for (int j = kk >> 1; j > 0; j >>= 1) {
+      for (int i = lane; i < k2; i += 64) {
+        const int l = i ^ j;
+        if (l <= i) continue;
+        const int64_t ti = sm.col.ts[i], tl = sm.col.ts[l];
+        const int32_t ci_ = sm.col.cidx[i], cl = sm.col.cidx[l];
+        // "before": newer first, then the later column
+        const bool l_before_i = tl > ti || (tl == ti && cl > ci_);
+        const bool i_before_l = ti > tl || (ti == tl && ci_ > cl);
+        const bool up = (i & kk) == 0;
+        if (up ? l_before_i : i_before_l) {
+          sm.col.ts[i] = tl;
+          sm.col.ts[l] = ti;
+          sm.col.cidx[i] = cl;
+          sm.col.cidx[l] = ci_;
+          const int32_t b = sm.col.base[i];
+          sm.col.base[i] = sm.col.base[l];
+          sm.col.base[l] = b;
+        }
+      }
+      wave_sync();
+    }
+  // 3. record bases in rank order (exclusive scan of the counts)
+  {
+    int32_t carry = 0;
+    for (int i0 = 0; i0 < k; i0 += 64) {
+      const int i = i0 + lane;
+      const int32_t n = i < k ? sm.col.base[i] : 0;
+      int32_t x = n;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+      }
+      if (i < k) sm.col.base[i] = carry + x - n;
+      carry += __shfl(x, 63);
+    }
+    if (lane == 0) sm.col.base[k] = carry;
+    wave_sync();
+  }
+  const int n = sm.col.base[k];
+  // 4. cell records, columns in rank order; append pairs in reverse arrival
+  //    (the later of equal offsets first); a multi-point column whose
+  //    offsets go back in time sends the row to the heap emulation
+  int unsorted = 0, has_append = 0;
+  for (int i0 = 0; i0 < k; i0 += 64) {
+    const int i = i0 + lane;
+    int type = CT_SKIP;
+    int64_t c = 0;
+    if (i < k) {
+      c = c0 + sm.col.cidx[i];
+      const int64_t ql = D.col_qoff[c + 1] - D.col_qoff[c];
+      const uint8_t q0 = D.qual[D.col_qoff[c]];
+      type = (ql & 1) ? CT_APPEND
+                      : (ql == 2 || (ql == 4 && (q0 & 0xF0) == 0xF0)) ? CT_ONE
+                                                                      : CT_MULTI;
+    }
+    if (type == CT_ONE) {  // one lane per single-point column
+      const int64_t qb = D.col_qoff[c], ql = D.col_qoff[c + 1] - qb;
+      const int64_t vb = D.col_voff[c], vl = D.col_voff[c + 1] - vb;
+      CellRec x;
+      x.col = i;
+      x.qpos = qb;
+      x.ql = (uint8_t)ql;
+      if (ql == 2) {
+        int vskip, bad;
+        const uint8_t nf = fixup2(D.qual[qb + 1], D.val + vb, vl, vskip, bad);
+        const int cur = (nf & 0x7) + 1;
+        x.flags = RF_QFIX;
+        x.qfix = nf;
+        x.vpos = vb + vskip;
+        x.vl = (uint8_t)cur;
+        x.vav = (uint8_t)(cur <= vl - vskip ? cur : vl - vskip);
+        if (cur > vl - vskip) x.flags |= RF_OVERRUN;
+        x.off = (int32_t)((((uint32_t)D.qual[qb] << 8) | nf) >> 4) * 1000;
+      } else {
+        const uint32_t qv = ((uint32_t)D.qual[qb] << 24) |
+                            ((uint32_t)D.qual[qb + 1] << 16) |
+                            ((uint32_t)D.qual[qb + 2] << 8) | D.qual[qb + 3];
+        const int cur = (int)(qv & 0x7) + 1;
+        x.flags = RF_MS;
+        x.qfix = 0;
+        x.vpos = vb;
+        x.vl = (uint8_t)cur;
+        x.vav = (uint8_t)(cur <= vl ? cur : vl);
+        if (cur > vl) x.flags |= RF_OVERRUN;
+        x.off = qual_off_ms(qv, 1);
+      }
+      R[sm.col.base[i]] = x;
+    }
+    uint64_t om = __ballot(type == CT_MULTI || type == CT_APPEND);
+    has_append |= __ballot(type == CT_APPEND) != 0;
+    while (om) {
+      const int b = __builtin_ctzll(om);
+      om &= om - 1;
+      const int ii = i0 + b;
+      const int64_t cb = c0 + sm.col.cidx[ii];
+      const int64_t qb = D.col_qoff[cb], vb = D.col_voff[cb];
+      const int64_t ql = D.col_qoff[cb + 1] - qb, vl = D.col_voff[cb + 1] - vb;
+      CellRec* out = R + sm.col.base[ii];
+      if (ql & 1) {  // append: lane 0 walks the pairs
+        if (lane == 0) {
+          const int64_t np = sm.col.base[ii + 1] - sm.col.base[ii];
+          int64_t p = 0;
+          for (int64_t j = 0; j < np; ++j) {
+            const uint8_t* e = D.val + vb + p;
+            const int eql = (e[0] & 0xF0) == 0xF0 ? 4 : 2;
+            uint32_t qv = 0;
+            for (int t = 0; t < eql; ++t) qv = (qv << 8) | e[t];
+            const int cur = (int)(qv & 0x7) + 1;
+            CellRec x;
+            x.qpos = vb + p;
+            x.vpos = vb + p + eql;
+            x.off = qual_off_ms(qv, eql == 4);
+            x.col = ii;
+            x.ql = (uint8_t)eql;
+            x.vl = x.vav = (uint8_t)cur;
+            x.flags = RF_QINVAL | RF_APPEND | (eql == 4 ? RF_MS : 0);
+            x.qfix = 0;
+            out[np - 1 - j] = x;
+            p += eql + cur;
+          }
+        }
+      } else {
+        ColWalk w(D.qual + qb, ql, vl);
+        bool hp = false;
+        int32_t prev = 0;
+        while (w.step()) {
+          const int pl = lane_prev(w.mask, lane);
+          int32_t po = __shfl(w.off, pl < 0 ? 0 : pl);
+          const bool have = pl >= 0 || hp;
+          if (pl < 0) po = prev;
+          if (__ballot(w.cell && have && w.off < po)) unsorted = 1;
+          if (w.cell) {
+            CellRec x;
+            x.qpos = qb + w.qo;
+            x.vpos = vb + w.vo;
+            x.off = w.off;
+            x.col = ii;
+            x.ql = (uint8_t)w.ql;
+            x.vl = (uint8_t)w.vl;
+            x.vav = (uint8_t)(w.vo + w.vl <= vl ? w.vl : vl - w.vo);
+            x.flags = (w.ms ? RF_MS : 0) |
+                      (w.vo + w.vl > vl ? RF_OVERRUN : 0);
+            x.qfix = 0;
+            out[w.k] = x;
+          }
+          if (w.mask) {
+            prev = __shfl(w.off, 63 - __builtin_clzll(w.mask));
+            hp = true;
+          }
+        }
+      }
+    }
+  }
+  // the records are read back by other lanes: device-scope fence (the
+  // write-through L1 is invalidated)
+  __threadfence();
+  wave_sync();
+  int64_t nq = 0, nv = 0, nk = 0;
+  int ms_in = 0, s_in = 0, bad = 0;
+  if (!unsorted) {
+    // 5a. the heap order = sort by (offset, rank, position)
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    for (int i = lane; i < n2; i += 64)
+      sm.keys[i] = i < n ? ((uint64_t)(uint32_t)R[i].off << 32) | (uint32_t)i
+                         : ~0ULL;
+    wave_sync();
+    for (int kk = 2; kk <= n2; kk <<= 1)
+      for (int j = kk >> 1; j > 0; j >>= 1) {
+        for (int i = lane; i < n2; i += 64) {
+          const int l = i ^ j;
+          if (l <= i) continue;
+          const uint64_t a = sm.keys[i], b = sm.keys[l];
+          const bool up = (i & kk) == 0;
+          if (up ? b < a : a < b) {
+            sm.keys[i] = b;
+            sm.keys[l] = a;
+          }
+        }
+        wave_sync();
+      }
+    int64_t lvpos = 0;
+    int lvl = 0, lvav = 0;
+    for (int p0 = 0; p0 < n; p0 += 64) {
+      const int p = p0 + lane;
+      const bool in = p < n;
+      CellRec x{};
+      bool lead = false, dup = false;
+      if (in) {
+        const uint64_t key = sm.keys[p];
+        x = R[(uint32_t)key];
+        if (p == 0 || (sm.keys[p - 1] >> 32) != (key >> 32)) {
+          lead = true;
+        } else {
+          const CellRec& y = R[(uint32_t)sm.keys[p - 1]];
+          // a pair an append column's TreeMap replaced: never popped
+          dup = !((x.flags & RF_APPEND) && y.col == x.col);
+        }
+      }
+      const uint64_t lm = __ballot(lead);
+      const int ll = lane_last_le(lm, lane);
+      int64_t rvpos = __shfl(x.vpos, ll < 0 ? 0 : ll);
+      int rvl = __shfl((int)x.vl, ll < 0 ? 0 : ll);
+      int rvav = __shfl((int)x.vav, ll < 0 ? 0 : ll);
+      if (ll < 0) {
+        rvpos = lvpos;
+        rvl = lvl;
+        rvav = lvav;
+      }
+      if (dup && !fix &&
+          !bytes_equal_padded(D.val, x.vpos, x.vl, x.vav, rvpos, rvl, rvav))
+        bad = 1;
+      if (lead && (x.flags & RF_OVERRUN)) bad = 1;
+      const int64_t kq = lead ? x.ql : 0, kv = lead ? x.vl : 0;
+      const int64_t iq = wave_incl_scan(kq), iv = wave_incl_scan(kv);
+      if (lead && !bad) write_cell(D, x, sq + nq + iq - kq, sv + nv + iv - kv);
+      ms_in |= __ballot(lead && (x.flags & RF_MS)) != 0;
+      s_in |= __ballot(lead && !(x.flags & RF_MS)) != 0;
+      nq += __shfl(iq, 63);
+      nv += __shfl(iv, 63);
+      nk += __popcll(lm);
+      if (lm) {
+        const int last = 63 - __builtin_clzll(lm);
+        lvpos = __shfl(x.vpos, last);
+        lvl = __shfl((int)x.vl, last);
+        lvav = __shfl((int)x.vav, last);
+      }
+      if (__ballot(bad)) break;
+    }
+  } else if (has_append) {
+    // not reached by the write path or compaction: appended pairs next to a
+    // compacted column whose offsets go back in time
+    if (lane == 0) row_error(first_err, r, RS_UNSUPPORTED);
+    if (lane == 0) {
+      out_q[r] = 0;
+      out_v[r] = 0;
+    }
+    return;
+  } else {
+    // 5b. heap emulation: per column head; each step the least (offset,
+    //     rank) head pops (wave arg-min), lane 0 merges it
+    for (int i = lane; i < k; i += 64) {
+      const int32_t b0 = sm.col.base[i], b1 = sm.col.base[i + 1];
+      sm.hp.head[i] = b0;
+      sm.hp.end[i] = b1;
+    }
+    wave_sync();
+    for (int i = lane; i < k; i += 64)
+      sm.hp.hoff[i] = sm.hp.head[i] < sm.hp.end[i] ? R[sm.hp.head[i]].off : -1;
+    wave_sync();
+    bool have_prev = false;
+    int32_t prev = 0;
+    int64_t lvpos = 0;
+    int lvl = 0, lvav = 0;
+    for (int step = 0; step < n; ++step) {
+      uint64_t best = ~0ULL;
+      for (int i = lane; i < k; i += 64) {
+        const int32_t o = sm.hp.hoff[i];
+        if (o >= 0) {
+          const uint64_t key = ((uint64_t)(uint32_t)o << 32) | (uint32_t)i;
+          best = key < best ? key : best;
+        }
+      }
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t y = __shfl_xor(best, d);
+        best = y < best ? y : best;
+      }
+      if (best == ~0ULL) break;
+      const int ci_ = (int)(uint32_t)best;
+      const CellRec x = R[sm.hp.head[ci_]];
+      if (lane == 0) {
+        if (have_prev && x.off == prev) {
+          if (!fix &&
+              !bytes_equal_padded(D.val, x.vpos, x.vl, x.vav, lvpos, lvl, lvav))
+            bad = 1;
+        } else if (x.flags & RF_OVERRUN) {
+          bad = 1;
+        } else {
+          write_cell(D, x, sq + nq, sv + nv);
+          nq += x.ql;
+          nv += x.vl;
+          nk += 1;
+          if (x.flags & RF_MS) ms_in = 1;
+          else s_in = 1;
+          prev = x.off;
+          have_prev = true;
+          lvpos = x.vpos;
+          lvl = x.vl;
+          lvav = x.vav;
+        }
+        const int32_t h = sm.hp.head[ci_] + 1;
+        sm.hp.head[ci_] = h;
+        sm.hp.hoff[ci_] = h < sm.hp.end[ci_] ? R[h].off : -1;
+      }
+      wave_sync();
+      if (__builtin_amdgcn_readfirstlane(bad)) break;
+    }
+    nq = readlane_l(nq, 0);
+    nv = readlane_l(nv, 0);
+    nk = readlane_l(nk, 0);
+    ms_in = __builtin_amdgcn_readfirstlane(ms_in);
+    s_in = __builtin_amdgcn_readfirstlane(s_in);
+    bad = __builtin_amdgcn_readfirstlane(bad);
+  }
+  if (__ballot(bad)) {
+    if (lane == 0) {
+      row_error(first_err, r, RS_ILLEGAL_DATA);
+      out_q[r] = 0;
+      out_v[r] = 0;
+    }
+    return;
+  }
+  if (nk > 1) {
+    if (lane == 0) sv[nv] = (ms_in && s_in) ? 1 : 0;
+    nv += 1;
+  }
+  if (lane == 0) {
+    out_q[r] = nq;
+    out_v[r] = nv;
+  }
+}
+
+// ------------------------------------------------------------------ pack
+DEV void wave_copy(uint8_t* dst, const uint8_t* src, int64_t n) {
+  for (int64_t i = LANE; i < n; i += 64) dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(256) void k_rows_write(
+    RawDev D, int fix, const int64_t* __restrict__ row_series,
+    const int64_t* __restrict__ row_base_s, const uint8_t* __restrict__ kind,
+    const int64_t* __restrict__ lone, const int64_t* __restrict__ gen_base,
+    const uint8_t* __restrict__ stq, const uint8_t* __restrict__ stv,
+    const int64_t* __restrict__ out_q, const int64_t* __restrict__ out_v,
+    const int64_t* __restrict__ oq_off, const int64_t* __restrict__ ov_off,
+    const int64_t* __restrict__ k_off, int64_t* __restrict__ o_series,
+    int64_t* __restrict__ o_base, int64_t* __restrict__ o_qoff,
+    uint8_t* __restrict__ o_qual, int64_t* __restrict__ o_voff,
+    uint8_t* __restrict__ o_val) {
+  const int lane = LANE;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= D.R) return;
+  const uint8_t kd = kind[r];
+  if (kd == RK_EMPTY) return;
+  const int64_t k = k_off[r];
+  uint8_t* dq = o_qual + oq_off[r];
+  uint8_t* dv = o_val + ov_off[r];
+  if (lane == 0) {
+    if (o_series) o_series[k] = row_series ? row_series[r] : 0;
+    o_base[k] = row_base_s[r];
+    o_qoff[k] = oq_off[r];
+    o_voff[k] = ov_off[r];
+  }
+  if (kd == RK_VERBATIM) {
+    const int64_t c = lone[r];
+    wave_copy(dq, D.qual + D.col_qoff[c], out_q[r]);
+    wave_copy(dv, D.val + D.col_voff[c], out_v[r]);
+  } else if (kd == RK_LONE) {
+    lone_walk<true>(D, lone[r], fix, dq, dv);
+  } else {
+    const int64_t gb = gen_base[r];
+    wave_copy(dq, stq + 4 * gb, out_q[r]);
+    wave_copy(dv, stv + 9 * gb, out_v[r]);
+  }
+}
+
+// ------------------------------------------------------------ span assembly
+// RowSeq.size / timestamp(i) over one compacted row (RowSeq.java:338-420)
+DEV int64_t rs_size(const uint8_t* q, int64_t ql, const uint8_t* v,
+                    int64_t vl) {
+  if (vl > 0 && (v[vl - 1] & 1)) {
+    int64_t n = 0;
+    for (int64_t i = 0; i < ql; i += 2) {
+      if ((q[i] & 0xF0) == 0xF0) i += 2;
+      ++n;
+    }
+    return n;
+  }
+  if (ql > 0 && (q[0] & 0xF0) == 0xF0) return ql / 4;
+  return ql / 2;
+}
+
+DEV int64_t rs_ts(int64_t base, const uint8_t* q, int64_t ql, const uint8_t* v,
+                  int64_t vl, int64_t i) {
+  int64_t o = -1;
+  if (vl > 0 && (v[vl - 1] & 1)) {
+    int64_t kk = 0;
+    for (int64_t idx = 0; idx < ql; idx += 2) {
+      if (kk == i) {
+        o = idx;
+        break;
+      }
+      if ((q[idx] & 0xF0) == 0xF0) idx += 2;
+      ++kk;
+    }
+  } else if (ql > 0 && (q[0] & 0xF0) == 0xF0) {
+    o = i * 4;
+  } else {
+    o = i * 2;
+  }
+  if (o < 0 || o + 2 > ql) return INT64_MIN;
+  if ((q[o] & 0xF0) == 0xF0) {
+    if (o + 4 > ql) return INT64_MIN;
+    const uint32_t x = ((uint32_t)q[o] << 24) | ((uint32_t)q[o + 1] << 16) |
+                       ((uint32_t)q[o + 2] << 8) | q[o + 3];
+    return base * 1000 + qual_off_ms(x, 1);
+  }
+  const uint32_t x = ((uint32_t)q[o] << 8) | q[o + 1];
+  return (base + qual_off_ms(x, 0) / 1000) * 1000;
+}
+
+// One RowSeq of a replayed span: its bytes live in the input or the arena
+struct SpanSeq {
+  int64_t base;
+  const uint8_t* q;
+  const uint8_t* v;
+  int64_t ql, vl;
+};
+
+// a series takes the replay unless its rows' base times strictly increase
+__global__ __launch_bounds__(256) void k_span_plan(
+    CellsDev C, int64_t S, const int64_t* __restrict__ series_row,
+    uint8_t* __restrict__ slow, int64_t* __restrict__ arena_sz,
+    int64_t* __restrict__ o_rows, int64_t* __restrict__ o_q,
+    int64_t* __restrict__ o_v, int* err_word) {
+  const int lane = LANE;
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= S) return;
+  const int64_t r0 = series_row[s], r1 = series_row[s + 1];
+  int bad_order = 0, empty = 0;
+  for (int64_t r = r0 + lane; r < r1; r += 64) {
+    if (C.qual_off[r + 1] - C.qual_off[r] < 2) empty = 1;
+    if (r > r0 && C.row_base_s[r] <= C.row_base_s[r - 1]) bad_order = 1;
+  }
+  const bool sl = __ballot(bad_order) != 0;
+  if (__ballot(empty) && lane == 0) atomicOr(err_word, 1);
+  if (lane == 0) {
+    const int64_t nr = r1 - r0;
+    const int64_t L = (C.qual_off[r1] - C.qual_off[r0]) +
+                      (C.val_off[r1] - C.val_off[r0]);
+    slow[s] = sl;
+    // two halves of 2 (L + rows) + 64 bytes, then the RowSeq table
+    arena_sz[s] = sl ? ((2 * (2 * (L + nr) + 64) + nr * (int64_t)sizeof(SpanSeq) +
+                         2 * nr * 8 + 255) & ~(int64_t)255)
+                     : 0;
+    o_rows[s] = nr;
+    o_q[s] = C.qual_off[r1] - C.qual_off[r0];
+    o_v[s] = C.val_off[r1] - C.val_off[r0];
+  }
+}
+
+// Span.addRow replay of one series by lane 0 (the rare path).  Merged
+// RowSeqs are allocated from the current half of the series' arena; when it
+// fills, the live ones move to the other half (live bytes <= input bytes +
+// one meta byte per merge, so a half always takes the next merge).
+__global__ __launch_bounds__(64) void k_span_replay(
+    CellsDev C, int64_t S, const int64_t* __restrict__ series_row,
+    const uint8_t* __restrict__ slow, const int64_t* __restrict__ arena_off,
+    uint8_t* __restrict__ arena, int64_t* __restrict__ o_rows,
+    int64_t* __restrict__ o_q, int64_t* __restrict__ o_v) {
+  const int64_t s = blockIdx.x;
+  if (s >= S || !slow[s] || threadIdx.x != 0) return;
+  const int64_t r0 = series_row[s], r1 = series_row[s + 1], nr = r1 - r0;
+  const int64_t L = (C.qual_off[r1] - C.qual_off[r0]) +
+                    (C.val_off[r1] - C.val_off[r0]);
+  const int64_t H = 2 * (L + nr) + 64;
+  uint8_t* A = arena + arena_off[s];
+  SpanSeq* rs = reinterpret_cast<SpanSeq*>(A + 2 * H);
+  int64_t* order = reinterpret_cast<int64_t*>(rs + nr);
+  int half = 0;
+  int64_t bump = 0;
+  auto in_half = [&](const uint8_t* p, int h) {
+    return p >= A + h * H && p < A + (h + 1) * H;
+  };
+  int64_t n = 0;
+  for (int64_t r = r0; r < r1; ++r) {
+    const uint8_t* q = C.qual + C.qual_off[r];
+    const int64_t ql = C.qual_off[r + 1] - C.qual_off[r];
+    const uint8_t* v = C.val + C.val_off[r];
+    const int64_t vl = C.val_off[r + 1] - C.val_off[r];
+    const int64_t base = C.row_base_s[r];
+    int64_t target = -1;
+    if (n) {
+      const SpanSeq& last = rs[n - 1];
+      const int64_t last_ts =
+          rs_ts(last.base, last.q, last.ql, last.v, last.vl,
+                rs_size(last.q, last.ql, last.v, last.vl) - 1);
+      if (last_ts >= rs_ts(base, q, ql, v, vl, 0))
+        for (int64_t j = 0; j < n; ++j)
+          if (rs[j].base == base) {
+            target = j;
+            break;
+          }
+    }
+    if (target < 0) {
+      rs[n++] = SpanSeq{base, q, v, ql, vl};
+      continue;
+    }
+    SpanSeq& T = rs[target];
+    const int64_t need = T.ql + ql + T.vl + vl + 2;
+    if (bump + need > H) {  // move the live RowSeqs to the other half
+      const int nh = half ^ 1;
+      int64_t nb = 0;
+      uint8_t* dst = A + nh * H;
+      for (int64_t j = 0; j < n; ++j) {
+        if (in_half(rs[j].q, half)) {
+          for (int64_t b = 0; b < rs[j].ql; ++b) dst[nb + b] = rs[j].q[b];
+          rs[j].q = dst + nb;
+          nb += rs[j].ql;
+        }
+        if (in_half(rs[j].v, half)) {
+          for (int64_t b = 0; b < rs[j].vl; ++b) dst[nb + b] = rs[j].v[b];
+          rs[j].v = dst + nb;
+          nb += rs[j].vl;
+        }
+      }
+      half = nh;
+      bump = nb;
+    }
+    uint8_t* mq = A + half * H + bump;
+    uint8_t* mv = mq + T.ql + ql;
+    // RowSeq.addRow: two-pointer merge by offset, the incoming duplicate
+    // dropped
+    int64_t ri = 0, li = 0, mi = 0, rvi = 0, lvi = 0, mvi = 0;
+    auto qlen_at = [](const uint8_t* qq, int64_t o) {
+      return (qq[o] & 0xF0) == 0xF0 ? 4 : 2;
+    };
+    auto vlen_at = [&](const uint8_t* qq, int64_t o) {
+      return (qq[o + qlen_at(qq, o) - 1] & 0x7) + 1;
+    };
+    auto off_at = [&](const uint8_t* qq, int64_t o) -> int32_t {
+      if ((qq[o] & 0xF0) == 0xF0)
+        return qual_off_ms(((uint32_t)qq[o] << 24) | ((uint32_t)qq[o + 1] << 16) |
+                               ((uint32_t)qq[o + 2] << 8) | qq[o + 3],
+                           1);
+      return qual_off_ms(((uint32_t)qq[o] << 8) | qq[o + 1], 0);
+    };
+    auto take = [&](const uint8_t* qq, int64_t& qi, const uint8_t* vv,
+                    int64_t& vi) {
+      const int a = qlen_at(qq, qi), b = vlen_at(qq, qi);
+      for (int t = 0; t < b; ++t) mv[mvi + t] = vv[vi + t];
+      for (int t = 0; t < a; ++t) mq[mi + t] = qq[qi + t];
+      vi += b;
+      mvi += b;
+      qi += a;
+      mi += a;
+    };
+    int64_t guard = 0;
+    while ((ri < ql || li < T.ql) && guard++ < ql + T.ql + 4) {
+      if (ri >= ql) {
+        take(T.q, li, T.v, lvi);
+      } else if (li >= T.ql) {
+        take(q, ri, v, rvi);
+      } else {
+        const int32_t a = off_at(q, ri), b = off_at(T.q, li);
+        if (a == b) {
+          rvi += vlen_at(q, ri);
+          ri += qlen_at(q, ri);
+        } else if (a < b) {
+          take(q, ri, v, rvi);
+        } else {
+          take(T.q, li, T.v, lvi);
+        }
+      }
+    }
+    const uint8_t meta =
+        ((T.vl > 0 && (T.v[T.vl - 1] & 1)) || (vl > 0 && (v[vl - 1] & 1))) ? 1
+                                                                          : 0;
+    // values were laid out after the qualifier bytes of both inputs: move
+    // them up behind the merged qualifiers
+    uint8_t* fv = mq + mi;
+    for (int64_t t = 0; t < mvi; ++t) fv[t] = mv[t];
+    fv[mvi] = meta;
+    T.q = mq;
+    T.ql = mi;
+    T.v = fv;
+    T.vl = mvi + 1;
+    bump += mi + mvi + 1;
+  }
+  // checkRowOrder: stable sort by base time
+  for (int64_t j = 0; j < n; ++j) order[j] = j;
+  for (int64_t a = 1; a < n; ++a) {
+    const int64_t x = order[a];
+    int64_t b = a - 1;
+    while (b >= 0 && rs[order[b]].base > rs[x].base) {
+      order[b + 1] = order[b];
+      --b;
+    }
+    order[b + 1] = x;
+  }
+  int64_t tq = 0, tv = 0;
+  for (int64_t j = 0; j < n; ++j) {
+    tq += rs[j].ql;
+    tv += rs[j].vl;
+  }
+  o_rows[s] = n;
+  o_q[s] = tq;
+  o_v[s] = tv;
+}
+
+// rows of every series at their scanned output positions
+__global__ __launch_bounds__(256) void k_span_write(
+    CellsDev C, int64_t S, const int64_t* __restrict__ series_row,
+    const uint8_t* __restrict__ slow, const int64_t* __restrict__ arena_off,
+    const uint8_t* __restrict__ arena, const int64_t* __restrict__ row_off,
+    const int64_t* __restrict__ q_off, const int64_t* __restrict__ v_off,
+    int64_t* __restrict__ o_series, int64_t* __restrict__ o_base,
+    int64_t* __restrict__ o_qoff, uint8_t* __restrict__ o_qual,
+    int64_t* __restrict__ o_voff, uint8_t* __restrict__ o_val) {
+  const int lane = LANE;
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= S) return;
+  const int64_t r0 = series_row[s], r1 = series_row[s + 1];
+  int64_t k = row_off[s], qo = q_off[s], vo = v_off[s];
+  if (!slow[s]) {
+    const int64_t dq = qo - C.qual_off[r0], dv = vo - C.val_off[r0];
+    for (int64_t r = r0 + lane; r < r1; r += 64) {
+      o_series[k + r - r0] = s;
+      o_base[k + r - r0] = C.row_base_s[r];
+      o_qoff[k + r - r0] = C.qual_off[r] + dq;
+      o_voff[k + r - r0] = C.val_off[r] + dv;
+    }
+    wave_copy(o_qual + qo, C.qual + C.qual_off[r0],
+              C.qual_off[r1] - C.qual_off[r0]);
+    wave_copy(o_val + vo, C.val + C.val_off[r0], C.val_off[r1] - C.val_off[r0]);
+    return;
+  }
+  const int64_t nr = r1 - r0;
+  const int64_t L = (C.qual_off[r1] - C.qual_off[r0]) +
+                    (C.val_off[r1] - C.val_off[r0]);
+  const int64_t H = 2 * (L + nr) + 64;
+  const uint8_t* A = arena + arena_off[s];
+  const SpanSeq* rs = reinterpret_cast<const SpanSeq*>(A + 2 * H);
+  const int64_t* order = reinterpret_cast<const int64_t*>(rs + nr);
+  // the replay's row count is this series' share of row_off
+  const int64_t n = row_off[s + 1] - row_off[s];
+  for (int64_t j = 0; j < n; ++j) {
+    const SpanSeq x = rs[order[j]];
+    if (lane == 0) {
+      o_series[k + j] = s;
+      o_base[k + j] = x.base;
+      o_qoff[k + j] = qo;
+      o_voff[k + j] = vo;
+    }
+    wave_copy(o_qual + qo, x.q, x.ql);
+    wave_copy(o_val + vo, x.v, x.vl);
+    qo += x.ql;
+    vo += x.vl;
+  }
+}
+
+#endif  // OTSDB_DS_TU
+
+}  // namespace otsdb

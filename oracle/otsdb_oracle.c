@@ -1477,6 +1477,7 @@ typedef struct {
   int64_t qo, vo;  /* cursor */
   int32_t cur_off; /* current point: offset ms, qualifier / value length */
   int32_t cur_ql, cur_vl, is_ms;
+  int32_t fixed, appended; /* checkForFixup changed it / an append column */
 } cdi_t;
 
 static int32_t q_offset_ms(const uint8_t* q, int64_t o) {
@@ -1493,9 +1494,14 @@ static int q_vlen(const uint8_t* q, int64_t o) {
 }
 
 /* ColumnDatapointIterator.update (:172-186) */
-static int cdi_update(cdi_t* c) {
+static int cdi_update(cdi_t* c, exc_t* e) {
   if (c->qo >= c->qlen || c->vo >= c->vlen) return 0;
-  if (c->qo + q_len(c->q, c->qo) > c->qlen) return 0;
+  if (c->qo + q_len(c->q, c->qo) > c->qlen) {
+    /* a 4-byte qualifier running past the column: the reference's
+     * getOffsetFromQualifier reads past the array (a RuntimeException) */
+    jraise(e, OTSDB_E_ILLEGAL_DATA, "Corrupted qualifier: truncated");
+    return 0;
+  }
   c->is_ms = (c->q[c->qo] & 0xF0) == 0xF0;
   c->cur_ql = c->is_ms ? 4 : 2;
   c->cur_off = q_offset_ms(c->q, c->qo);
@@ -1608,6 +1614,7 @@ int or_compact_row(int64_t ncol, const int64_t* col_qoff, const uint8_t* qual,
       memcpy(x.v, v, (size_t)vl);
       x.vlen = vl;
     }
+    int fixed = 0, appended = q[0] == 0x05 && (ql & 1);
     if (x.qlen == 2) {  /* checkForFixup */
       const uint8_t f = x.q[1];
       if ((f & 0x8) && (f & 0x7) == 0x3 && x.vlen == 8) {
@@ -1619,11 +1626,43 @@ int or_compact_row(int64_t ncol, const int64_t* col_qoff, const uint8_t* qual,
         }
         memmove(x.v, x.v + 4, 4);
         x.vlen = 4;
+        fixed = 1;
       }
-      x.q[1] = (uint8_t)((f & ~0x7) | ((x.vlen - 1) & 0xFF));
+      const uint8_t nf = (uint8_t)((f & ~0x7) | ((x.vlen - 1) & 0xFF));
+      if (nf != f) fixed = 1;
+      x.q[1] = nf;
     }
-    if (cdi_update(&x)) it[nit++] = x;
+    /* a data column with qualifiers but no value bytes: the reference heaps
+     * it with no current point (hasMoreData only looks at the qualifier) and
+     * emits an empty segment; treated as a corrupt cell here */
+    if (x.qlen > 0 && x.vlen == 0) {
+      jraise(&e, OTSDB_E_ILLEGAL_DATA, "Corrupted value: empty value");
+      free(x.q);
+      free(x.v);
+      break;
+    }
+    x.fixed = fixed;
+    x.appended = appended;
+    if (cdi_update(&x, &e)) it[nit++] = x;
     else { free(x.q); free(x.v); }
+  }
+  /* noMergesOrFixups (CompactionQueue.java:317-332, :352-357): one heaped
+   * column with a lone 2-byte or 4-byte ms qualifier and no fix-up is
+   * returned as it is stored */
+  if (!e.code && nit == 1 && !it[0].fixed && !it[0].appended &&
+      (it[0].qlen == 2 || (it[0].qlen == 4 && it[0].is_ms))) {
+    if (it[0].qlen > qcap || it[0].vlen > vcap) {
+      jraise(&e, OTSDB_E_CAPACITY, "compaction output capacity");
+    } else {
+      memcpy(out_q, it[0].q, (size_t)it[0].qlen);
+      memcpy(out_v, it[0].v, (size_t)it[0].vlen);
+      *out_qlen = it[0].qlen;
+      *out_vlen = it[0].vlen;
+      free(it[0].q);
+      free(it[0].v);
+      free(it);
+      return OTSDB_OK;
+    }
   }
   int ms_in = 0, s_in = 0;
   int64_t nseg = 0, qo = 0, vo = 0, last_vo = 0, last_vl = 0;
@@ -1640,20 +1679,26 @@ int or_compact_row(int64_t ncol, const int64_t* col_qoff, const uint8_t* qual,
     }
     if (best < 0) break;
     cdi_t* c = &it[best];
-    if (c->vo + c->cur_vl > c->vlen) {
-      jraise(&e, OTSDB_E_ILLEGAL_DATA,
-             "Corrupted value: couldn't break down into individual values");
-      break;
-    }
     if (c->cur_off == prev) {
-      const int differ = c->cur_vl != last_vl ||
-                         memcmp(out_v + last_vo, c->v + c->vo, (size_t)last_vl);
+      /* getCopyOfCurrentValue: Arrays.copyOfRange, zero-padded past the end */
+      int differ = c->cur_vl != last_vl;
+      for (int b = 0; !differ && b < last_vl; b++) {
+        const uint8_t x = c->vo + b < c->vlen ? c->v[c->vo + b] : 0;
+        differ = x != out_v[last_vo + b];
+      }
       if (differ && !fix_duplicates) {
         jraise(&e, OTSDB_E_ILLEGAL_DATA, "Duplicate timestamp, ms_offset=%d",
                (int)prev);
         break;
       }
     } else {
+      /* a kept value running past its column: ByteBufferList.toBytes copies
+       * past the array */
+      if (c->vo + c->cur_vl > c->vlen) {
+        jraise(&e, OTSDB_E_ILLEGAL_DATA,
+               "Corrupted value: couldn't break down into individual values");
+        break;
+      }
       prev = c->cur_off;
       if (qo + c->cur_ql > qcap || vo + c->cur_vl + 1 > vcap) {
         jraise(&e, OTSDB_E_CAPACITY, "compaction output capacity");
@@ -1670,7 +1715,7 @@ int or_compact_row(int64_t ncol, const int64_t* col_qoff, const uint8_t* qual,
     }
     c->qo += c->cur_ql;  /* advance */
     c->vo += c->cur_vl;
-    if (!cdi_update(c)) c->qo = c->qlen;
+    if (!cdi_update(c, &e)) c->qo = c->qlen;
   }
   if (!e.code && nseg > 1) out_v[vo++] = (uint8_t)((ms_in && s_in) ? 1 : 0);
   for (int64_t k = 0; k < nit; k++) { free(it[k].q); free(it[k].v); }

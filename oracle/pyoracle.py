@@ -24,8 +24,7 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB):
-            build()
+        build()  # make: a no-op unless the restatement changed
         l = C.CDLL(LIB)
         vp, i64, i32, cp = C.c_void_p, C.c_int64, C.c_int32, C.c_char_p
         l.or_group_by.argtypes = [vp, vp, vp, i64, vp, C.POINTER(i64), cp,

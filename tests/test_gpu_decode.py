@@ -181,7 +181,11 @@ FUSED = [("sum", "1m-avg", False), ("zimsum", "5m-sum", False),
          ("count", "2m-count", False), ("max", "1m-first-nan", False),
          ("min", "1m-last-zero", False), ("p99", "1m-avg", False),
          ("mimmax", "30s-max", False), ("sum", "1m-sum", True),
-         ("sum", "1hc-avg", False)]
+         ("sum", "1hc-avg", False),
+         # buckets spanning storage rows (intervals that do not divide an
+         # hour): the open bucket carries from one row to the next
+         ("sum", "7m-avg", False), ("avg", "90m-sum", False),
+         ("zimsum", "7m-count", False)]
 
 
 @pytest.mark.parametrize("agg,ds,rate", FUSED,

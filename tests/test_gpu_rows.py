@@ -1,0 +1,311 @@
+"""Query-time compaction and span assembly on the GPU (rows.hip, through the
+C-ABI) against the oracle's restatement (or_compact_row / or_span_assemble,
+pinned by the TestCompactionQueue / TestRowSeq vectors) and against the
+reference's own known answers: bit-exact bytes, same exceptions.  Needs an
+MI355X."""
+import numpy as np
+import pytest
+
+from opentsdb_amd import core, storage
+from oracle import pyoracle
+from tests import datasets, kat, rows_fuzz
+
+pytestmark = pytest.mark.gpu
+
+EXC = {"IllegalDataException": core.IllegalDataException,
+       "IllegalArgumentException": core.IllegalArgumentException}
+STATUS_EXC = {1: core.IllegalDataException, 3: core.IllegalArgumentException,
+              5: core.UnsupportedOperationException}
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from opentsdb_amd.engine import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def _gpu_compact(engine, rows, fix=True, with_ts=True):
+    """rows: [(series, base, [(q, v, ts)])] -> [(series, base, q, v)]"""
+    raw = storage.HostRawRows(rows, with_ts=with_ts).to_device()
+    return storage.cells_rows(storage.compact_rows_device(engine, raw, fix))
+
+
+def test_compaction_queue_kats(engine):
+    """Every TestCompactionQueue vector with an answer, one row each, in one
+    call: the kept rows' bytes are the asserted column."""
+    cases = [c for c in kat.load_cases("compact") if "error" not in c]
+    rows = []
+    for i, c in enumerate(cases):
+        cols = [(bytes.fromhex(q), bytes.fromhex(v), j)
+                for j, (q, v) in enumerate(c["columns"])]
+        assert c["fix_duplicates"]
+        rows.append((i, 1356998400, cols))
+    got = {s: (q, v) for s, _, q, v in _gpu_compact(engine, rows)}
+    for i, c in enumerate(cases):
+        if c["expect"] is None:
+            assert i not in got, c["name"]
+        else:
+            assert got[i][0].hex() == c["expect"][0], c["name"]
+            assert got[i][1].hex() == c["expect"][1], c["name"]
+
+
+@pytest.mark.parametrize("c", [c for c in kat.load_cases("compact")
+                               if "error" in c], ids=lambda c: c["name"])
+def test_compaction_queue_errors(engine, c):
+    cols = [(bytes.fromhex(q), bytes.fromhex(v), j)
+            for j, (q, v) in enumerate(c["columns"])]
+    with pytest.raises(EXC[c["error"]]):
+        _gpu_compact(engine, [(0, 1356998400, cols)], c["fix_duplicates"])
+
+
+def _oracle_rows(rows, fix):
+    out = []
+    for s, b, cols in rows:
+        r = pyoracle.compact_row([(q, v) for q, v, _ in cols],
+                                 [t for _, _, t in cols], fix)
+        if r is not None:
+            out.append((s, b, r[0], r[1]))
+    return out
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_compaction_fuzz_matches_oracle(engine, seed):
+    """Random rows (single cells, compacted columns in and out of time
+    order, appends, duplicates across columns, annotations, legacy fix-ups),
+    fix_duplicates on: every row's bytes equal the oracle's."""
+    rng = np.random.default_rng(seed)
+    rows, s = [], 0
+    while len(rows) < 400:
+        cols = rows_fuzz.random_row(rng)
+        if rows_fuzz.heap_with_append(cols):
+            continue
+        try:
+            pyoracle.compact_row([(q, v) for q, v, _ in cols],
+                                 [t for _, _, t in cols], True)
+        except pyoracle.OracleError:
+            continue  # corrupt inputs are covered below
+        rows.append((s, rows_fuzz.BASE + 3600 * (s % 5), cols))
+        s += 1
+    got = _gpu_compact(engine, rows)
+    ref = _oracle_rows(rows, True)
+    assert len(got) == len(ref)
+    for g, r in zip(got, ref):
+        assert g == r, (g, r)
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_compaction_fuzz_errors_match_oracle(engine, seed):
+    """Corrupt and duplicate-with-different-value rows, fix_duplicates off:
+    the GPU raises the oracle's exception (one row per call), or returns its
+    bytes."""
+    rng = np.random.default_rng(seed)
+    n_err = n_ok = 0
+    for i in range(60):
+        cols = rows_fuzz.random_row(rng, corrupt=0.5)
+        if rows_fuzz.heap_with_append(cols):
+            continue
+        try:
+            ref = pyoracle.compact_row([(q, v) for q, v, _ in cols],
+                                       [t for _, _, t in cols], False)
+            err = None
+        except pyoracle.OracleError as e:
+            err = e.status
+        if err is None:
+            got = _gpu_compact(engine, [(0, rows_fuzz.BASE, cols)], fix=False)
+            assert got == ([] if ref is None else
+                           [(0, rows_fuzz.BASE, ref[0], ref[1])])
+            n_ok += 1
+        else:
+            with pytest.raises(STATUS_EXC[err]):
+                _gpu_compact(engine, [(0, rows_fuzz.BASE, cols)], fix=False)
+            n_err += 1
+    assert n_err > 5 and n_ok > 5
+
+
+def test_compaction_first_failing_row_decides(engine):
+    """The first failing row in row order decides the exception (the
+    scanner compacts rows in order)."""
+    bad_arg = (bytes([5, 0, 0, 0, 0]), b"", 0)
+    bad_data = (rows_fuzz.sec_qual(7, 0xB), b"\1\0\0\0\0\0\0\1", 0)
+    ok = (rows_fuzz.sec_qual(1, 0x7), b"\0" * 7 + b"\1", 0)
+    rows = [(0, rows_fuzz.BASE, [ok]), (1, rows_fuzz.BASE, [bad_data]),
+            (2, rows_fuzz.BASE, [bad_arg])]
+    with pytest.raises(core.IllegalDataException):
+        _gpu_compact(engine, rows)
+    rows[1], rows[2] = (1, rows_fuzz.BASE, [bad_arg]), (2, rows_fuzz.BASE, [bad_data])
+    with pytest.raises(core.IllegalArgumentException):
+        _gpu_compact(engine, rows)
+
+
+def test_compaction_uncompacted_hour(engine):
+    """A row never compacted: 3600 single-second cells in column (qualifier)
+    order, plus a few repeats with newer HBase timestamps and equal bytes —
+    the LDS sort path at its size."""
+    rng = np.random.default_rng(5)
+    pts = [rows_fuzz.cell(rng, 1000 * k, False) for k in range(3600)]
+    cols = [(q, v, k) for k, (q, v) in enumerate(pts)]
+    for k in rng.integers(0, 3600, size=20):
+        cols.append((pts[k][0], pts[k][1], 5000 + int(k)))
+    got = _gpu_compact(engine, [(0, rows_fuzz.BASE, cols)])
+    q, v = rows_fuzz.compacted(pts)
+    assert got == [(0, rows_fuzz.BASE, q, v)]
+
+
+def test_compaction_unsupported_beyond_caps(engine):
+    """More than 8192 points to merge in one row: UnsupportedOperation (the
+    caller keeps the reference's compaction for that row)."""
+    rng = np.random.default_rng(6)
+    a = rows_fuzz.compacted([rows_fuzz.cell(rng, k, True) for k in range(5000)])
+    b = rows_fuzz.compacted([rows_fuzz.cell(rng, k, True) for k in range(5000)])
+    with pytest.raises(core.UnsupportedOperationException):
+        _gpu_compact(engine, [(0, rows_fuzz.BASE, [a + (0,), b + (1,)])])
+
+
+def test_row_seq_kats(engine):
+    """TestRowSeq's merge vectors: the span's rows decode to the asserted
+    points."""
+    cases = kat.load_cases("span")
+    rows = []
+    for i, c in enumerate(cases):
+        for b, q, v in c["rows"]:
+            rows.append((i, b, bytes.fromhex(q), bytes.fromhex(v)))
+    got = _gpu_span(engine, rows, len(cases))
+    for i, c in enumerate(cases):
+        pts = []
+        for s, b, q, v in got:
+            if s != i:
+                continue
+            for p in pyoracle.decode_row(q, v, b):
+                pts.append([int(p["ts"]), kat.point_value(p["bits"], p["is_int"])])
+        assert pts == c["expect"], c["name"]
+
+
+def _gpu_span(engine, rows, n_series):
+    """rows: [(series, base, q, v)] in arrival order -> span rows"""
+    import torch
+    from opentsdb_amd.workload import DeviceCells
+    qo = np.cumsum([0] + [len(r[2]) for r in rows]).astype(np.int64)
+    vo = np.cumsum([0] + [len(r[3]) for r in rows]).astype(np.int64)
+    t = dict(row_series=np.asarray([r[0] for r in rows], np.int64),
+             row_base_s=np.asarray([r[1] for r in rows], np.int64),
+             qual_off=qo, val_off=vo,
+             qual=np.frombuffer(b"".join(r[2] for r in rows) + b"\0" * 16,
+                                np.uint8),
+             val=np.frombuffer(b"".join(r[3] for r in rows) + b"\0" * 16,
+                               np.uint8))
+    t = {k: torch.from_numpy(np.ascontiguousarray(x)).cuda() for k, x in t.items()}
+    cells = DeviceCells(t, n_series)
+    return storage.cells_rows(storage.span_assemble_device(engine, cells))
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_span_fuzz_matches_oracle(engine, seed):
+    """Series whose rows arrive in any order, with repeated row keys
+    (overlapping and disjoint in time): the span rows' bytes equal the
+    oracle's Span.addRow replay; in-order series pass through unchanged."""
+    rng = np.random.default_rng(seed)
+    rows, ref = [], []
+    S = 120
+    for s in range(S):
+        n = int(rng.integers(1, 7))
+        if s % 3 == 0:  # the scanner's order: strictly increasing bases
+            bases = sorted(rng.choice(24, size=n, replace=False))
+        else:
+            bases = list(rng.integers(0, 4, size=n))
+        rs = []
+        for b in bases:
+            q, v = rows_fuzz.random_compacted_row(rng, pool_s=600)
+            rs.append((rows_fuzz.BASE + 3600 * int(b), q, v))
+        rows += [(s, b, q, v) for b, q, v in rs]
+        ref += [(s, b, q, v) for b, q, v in pyoracle.span_assemble(rs)]
+    got = _gpu_span(engine, rows, S)
+    assert got == ref
+
+
+def _raw_from_hb(rng, hb, split=0.3):
+    """Storage rows holding exactly hb's points, scattered over columns the
+    way uncompacted / partially compacted / appended rows hold them, some
+    hours split over two rows of the same key arriving in either order."""
+    from tests import cells as C
+    rows = []
+    isf = hb.is_float
+    for s in range(hb.n_series):
+        a, b = hb.offsets[s], hb.offsets[s + 1]
+        f = isf[a:b] if isf is not None else np.ones(b - a, np.uint8)
+        for base, q, v in C.encode_series(hb.ts[a:b], hb.val[a:b], f):
+            pts = rows_fuzz.split_points(q, v)
+            if len(pts) > 3 and rng.random() < split:
+                m = rng.random() < 0.5  # interleaved or consecutive halves
+                p1 = pts[0::2] if m else pts[:len(pts) // 2]
+                p2 = pts[1::2] if m else pts[len(pts) // 2:]
+                parts = [p1, p2] if rng.random() < 0.5 else [p2, p1]
+            else:
+                parts = [pts]
+            for p in parts:
+                rows.append((s, base, rows_fuzz.scatter_row(rng, p)))
+    return rows
+
+
+@pytest.mark.parametrize("agg,ds", [("sum", "1m-avg"), ("zimsum", "5m-sum"),
+                                    ("max", "1m-first"), ("p99", "1m-avg")])
+@pytest.mark.parametrize("kind", ["float", "int"])
+def test_query_from_storage_rows(engine, agg, ds, kind):
+    """otsdb_agg_run_raw_device: storage rows (cells, compacted pieces,
+    appends, repeats, split row keys) -> compaction -> spans -> the fused
+    query equals the oracle's query over the same points."""
+    import torch
+    from opentsdb_amd.engine import DeviceResult
+    from tests.test_gpu_parity import compare, cancel_floor
+    from tests.test_gpu_decode import _device_batch, _result_points
+    rng = np.random.default_rng(hash((agg, ds, kind)) % 2**31)
+    hb = datasets.random_batch(41, n_series=30, n_groups=3, span_ms=3 * 3600000,
+                               value_kind=kind, cadence_ms=10000)
+    hb.ts[:] = hb.ts - hb.ts % 1000
+    isf = 1 if kind == "float" else 0
+    hb.is_float = np.full(len(hb.ts), isf, np.uint8)
+    raw = storage.HostRawRows(_raw_from_hb(rng, hb), with_ts=True).to_device()
+    raw.n_series = hb.n_series
+    db = _device_batch(hb, kind)
+    t0, t1 = datasets.T0 + 600000, datasets.T0 + 3 * 3600000
+    spec = core.make_spec(t0, t1, core.Aggregators.get(agg),
+                          core.DownsamplingSpecification(ds), t0, t1)
+    ref = pyoracle.group_by(spec, hb)
+    res = DeviceResult(torch, db.n_groups, 4 * len(hb.ts) + 64, "cuda")
+    storage.run_raw_device(engine, spec, raw, db, res)
+    got = _result_points(res, db.n_groups)
+    exact = ds.endswith(("max", "first")) and agg in ("max", "p99")
+    compare(got, ref, exact, where="raw/%s/%s" % (agg, ds),
+            floor=cancel_floor(hb, 60) if kind == "int" else 0.0)
+
+
+def test_query_from_storage_rows_host_entry(engine):
+    """otsdb_agg_run_raw (host buffers, the JNI entry) = the device entry."""
+    import torch
+    from opentsdb_amd.engine import DeviceResult
+    from tests.test_gpu_decode import _device_batch, _result_points
+    rng = np.random.default_rng(3)
+    hb = datasets.random_batch(43, n_series=20, n_groups=4, span_ms=2 * 3600000,
+                               cadence_ms=10000)
+    hb.ts[:] = hb.ts - hb.ts % 1000
+    hb.is_float = np.ones(len(hb.ts), np.uint8)
+    rows = _raw_from_hb(rng, hb)
+    hraw = storage.HostRawRows(rows, with_ts=True)
+    hraw.n_series = hb.n_series
+    draw = hraw.to_device()
+    draw.n_series = hb.n_series
+    db = _device_batch(hb, "float")
+    spec = core.make_spec(datasets.T0, datasets.T0 + 2 * 3600000,
+                          core.Aggregators.SUM,
+                          core.DownsamplingSpecification("1m-avg"))
+    res = DeviceResult(torch, db.n_groups, 4 * len(hb.ts) + 64, "cuda")
+    storage.run_raw_device(engine, spec, draw, db, res)
+    dev = _result_points(res, db.n_groups)
+    offs, ts, val, isi = storage.run_raw(engine, spec, hraw, hb.group_offsets,
+                                         hb.group_members, 4 * len(hb.ts) + 64)
+    for g in range(db.n_groups):
+        a, b = offs[g], offs[g + 1]
+        assert np.array_equal(dev[g].ts, ts[a:b])
+        assert np.array_equal(dev[g].bits, val[a:b])
+        assert np.array_equal(dev[g].is_int, isi[a:b])
