@@ -1340,6 +1340,9 @@ int or_decode_row(const uint8_t* q, int64_t qlen, const uint8_t* v,
     if (produced < cap && out) out[produced] = p;
     produced++;
   }
+  /* every value byte used, the meta byte of a multi-value column aside
+   * (Internal.extractDataPoints, Internal.java:314-321) */
+  if (vi + (produced > 1 ? 1 : 0) != vlen) goto bad;
   if (needed) *needed = produced;
   return produced > cap ? OTSDB_E_CAPACITY : OTSDB_OK;
 bad:

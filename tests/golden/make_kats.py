@@ -1344,6 +1344,82 @@ _cq("appendsDuplicateCompacted",
      (_a[0] + _a[1], _av[0] + _av[1] + _ZB)],
     (_a[0] + _a[1], _av[0] + _av[1] + _ZB), ":1507-1530")
 
+# TestInternal.extractDataPoints (test/core/TestInternal.java:43-286): the
+# per-cell fix-ups and breakdown it asserts, restated as the compaction of
+# the same columns (distinct, increasing offsets: the compacted column is
+# the asserted cells concatenated, meta byte 1 iff seconds and ms mix).
+TIN = "test/core/TestInternal.java"
+_B = 1356998400
+
+
+def _ci(name, cols, cells, cite, error=None):
+    if error:
+        add(kind="compact", name=name, columns=[[q.hex(), v.hex()] for q, v in cols],
+            fix_duplicates=True, error=error, cite=TIN + cite)
+        return
+    mixed = len({len(q) for q, _ in cells}) > 1
+    q = b"".join(c[0] for c in cells)
+    v = b"".join(c[1] for c in cells) + (bytes([1 if mixed else 0])
+                                        if len(cells) > 1 else b"")
+    add(kind="compact", name=name, columns=[[a.hex(), b.hex()] for a, b in cols],
+        fix_duplicates=True, expect=[q.hex(), v.hex()], cite=TIN + cite)
+
+
+_ci("extractDataPointsFixQualifierFlags",
+    [(bytes([0, 0x07]), _Lb(4)), (bytes([0, 0x27]), _Ib(5)),
+     (bytes([0, 0x43]), _Lb(6))],
+    [(bytes([0, 0x07]), _Lb(4)), (bytes([0, 0x23]), _Ib(5)),
+     (bytes([0, 0x47]), _Lb(6))], ":43-64")
+_ci("extractDataPointsFixFloatingPointValue",
+    [(bytes([0, 0x0F]), bytes(7) + b"\1"), (bytes([0, 0x2B]), bytes(7) + b"\1"),
+     (bytes([0, 0x4B]), bytes(3) + b"\1")],
+    [(bytes([0, 0x0F]), bytes(7) + b"\1"), (bytes([0, 0x2B]), bytes(3) + b"\1"),
+     (bytes([0, 0x4B]), bytes(3) + b"\1")], ":67-88")
+_ci("extractDataPointsFixFloatingPointValueCorrupt",
+    [(bytes([0, 0x0F]), bytes(7) + b"\1"),
+     (bytes([0, 0x2B]), b"\0\2" + bytes(5) + b"\1"),
+     (bytes([0, 0x4B]), bytes(3) + b"\1")], None, ":91-105",
+    error="IllegalDataException")
+_ci("extractDataPointsMixSecondsMs",
+    [(bytes([0, 0x27]), _Lb(4)), (bytes([1, 0, 2]), b"Annotation"),
+     (bytes([0, 0x47]), _Lb(6))],
+    [(bytes([0, 0x27]), _Lb(4)), (bytes([0, 0x47]), _Lb(6))], ":108-125")
+_ms2 = bytes([0xF0, 0, 2, 7])
+_ci("extractDataPointsWithNonDataColumns",
+    [(bytes([0, 0x07]), _Lb(4)), (_ms2, _Lb(5)), (bytes([0, 0x47]), _Lb(6))],
+    [(bytes([0, 0x07]), _Lb(4)), (_ms2, _Lb(5)), (bytes([0, 0x47]), _Lb(6))],
+    ":128-147")
+_ci("extractDataPointsWithNonDataColumnsSort",
+    [(bytes([0, 0x47]), _Lb(6)), (_ms2, _Lb(5)), (bytes([0, 0x07]), _Lb(4))],
+    [(bytes([0, 0x07]), _Lb(4)), (_ms2, _Lb(5)), (bytes([0, 0x47]), _Lb(6))],
+    ":150-169")
+
+# compacted columns broken down by the decode (RowSeq / extractDataPoints
+# agree on a sorted column): points (ts ms, long value) or the exception
+def _dk(name, q, v, expect, cite, error=None):
+    c = dict(kind="decode", name=name, qual=q.hex(), val=v.hex(), base=_B,
+             cite=TIN + cite)
+    if error:
+        c["error"] = error
+    else:
+        c["expect"] = expect
+    add(**c)
+
+
+_dk("extractDataPointsCompactSeconds", bytes([0, 7, 0, 0x27, 0, 0x47]),
+    _Lb(4) + _Lb(5) + _Lb(6) + _ZB,
+    [[_B * 1000, 4], [_B * 1000 + 2000, 5], [_B * 1000 + 4000, 6]], ":172-193")
+_dk("extractDataPointsCompactMs",
+    bytes([0xF0, 0, 0, 7, 0xF0, 0, 2, 7, 0xF0, 0, 7, 7]),
+    _Lb(4) + _Lb(5) + _Lb(6) + _ZB,
+    [[_B * 1000, 4], [_B * 1000 + 8, 5], [_B * 1000 + 28, 6]], ":220-244")
+_dk("extractDataPointsCompactSecAndMs",
+    bytes([0, 7, 0xF0, 0, 2, 7, 0, 0x47]), _Lb(4) + _Lb(5) + _Lb(6) + _ZB,
+    [[_B * 1000, 4], [_B * 1000 + 8, 5], [_B * 1000 + 4000, 6]], ":247-269")
+_dk("extractDataPointsCompactCorrupt",
+    bytes([0, 7, 0xF0, 0, 2, 7, 0, 0x41]), _Lb(4) + _Lb(5) + _Lb(6) + _ZB,
+    None, ":272-286", error="IllegalDataException")
+
 # ----------------------------------------------------- span assembly (bytes)
 # test/core/TestRowSeq.java:122-508: rows of one series handed to the span
 # in this order (setRow + addRow), and the data points the series yields

@@ -150,3 +150,18 @@ def test_span_assemble(c):
         for p in pyoracle.decode_row(q, v, base):
             got.append([int(p["ts"]), kat.point_value(p["bits"], p["is_int"])])
     assert got == c["expect"]
+
+
+@pytest.mark.parametrize("c", kat.load_cases("decode"), ids=lambda c: c["name"])
+def test_decode_kat(c):
+    """Compacted columns broken down point by point (RowSeq.Iterator,
+    Internal.extractDataPoints) against TestInternal's asserted cells."""
+    q, v = bytes.fromhex(c["qual"]), bytes.fromhex(c["val"])
+    if "error" in c:
+        with pytest.raises(pyoracle.OracleError) as ei:
+            pyoracle.decode_row(q, v, c["base"])
+        assert ei.value.status == EXC[c["error"]]
+        return
+    got = pyoracle.decode_row(q, v, c["base"])
+    assert [[int(p["ts"]), kat.point_value(p["bits"], p["is_int"])]
+            for p in got] == c["expect"]
