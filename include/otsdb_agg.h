@@ -365,6 +365,12 @@ otsdb_status otsdb_agg_run_cells_device(otsdb_ctx* ctx,
                                         const otsdb_cells* cells,
                                         const otsdb_batch* batch,
                                         otsdb_result* out, void* hip_stream);
+/* The same with HOST pointers (the JNI entry at the TsdbQuery seam: the
+ * Spans' RowSeq bytes, SpanGroup members); copies in, runs, copies the
+ * result out.  Synchronous.  row_series must be nondecreasing.            */
+otsdb_status otsdb_agg_run_cells(otsdb_ctx* ctx, const otsdb_query_spec* spec,
+                                 const otsdb_cells* cells,
+                                 const otsdb_batch* batch, otsdb_result* out);
 
 /* ---- storage rows: query-time compaction + span assembly (§8a a3, a4) -- */
 /* The storage rows of a query exactly as the scanner returns them, before

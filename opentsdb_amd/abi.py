@@ -139,7 +139,7 @@ EXPORTS = [
     "otsdb_sel_hist_device", "otsdb_sel_finish_device",
     "otsdb_encode_cells_device", "otsdb_agg_run_cells_device",
     "otsdb_compact_rows_device", "otsdb_span_assemble_device",
-    "otsdb_agg_run_raw_device", "otsdb_agg_run_raw",
+    "otsdb_agg_run_raw_device", "otsdb_agg_run_raw", "otsdb_agg_run_cells",
 ]
 
 _lib = None
@@ -220,6 +220,8 @@ def load(path=None):
     lib.otsdb_agg_run_raw_device.restype = C.c_int
     lib.otsdb_agg_run_raw.argtypes = [vp, PS, PW, i32, PB, PR]
     lib.otsdb_agg_run_raw.restype = C.c_int
+    lib.otsdb_agg_run_cells.argtypes = [vp, PS, PC, PB, PR]
+    lib.otsdb_agg_run_cells.restype = C.c_int
     lib.otsdb_prof_enable.argtypes = [vp, C.c_int]
     lib.otsdb_prof_enable.restype = C.c_int
     lib.otsdb_prof_read.argtypes = [vp, vp, vp, C.c_int, C.c_int]

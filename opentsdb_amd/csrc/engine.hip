@@ -2198,6 +2198,105 @@ otsdb_status otsdb_agg_run_raw(otsdb_ctx* c, const otsdb_query_spec* spec,
   return OTSDB_OK;
 }
 
+otsdb_status otsdb_agg_run_cells(otsdb_ctx* c, const otsdb_query_spec* spec,
+                                 const otsdb_cells* cells, const otsdb_batch* b,
+                                 otsdb_result* out) {
+  if (!c || !spec || !cells || !b || !out)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipSetDevice(c->device));
+  otsdb_status rc = check_spec(spec);
+  if (rc) return rc;
+  std::vector<int64_t> goff;
+  if ((rc = read_goff(c, b, false, goff))) return rc;
+  const int64_t R = cells->n_rows, S = b->n_series, G = b->n_groups;
+  if (R < 0 || S < 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
+  if (R > 0 && (!cells->row_series || !cells->row_base_s || !cells->qual_off ||
+                !cells->val_off || !cells->qual || !cells->val))
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null cells array");
+  for (int64_t r = 0; r < R; ++r)
+    if (cells->row_series[r] < 0 || cells->row_series[r] >= S ||
+        (r && cells->row_series[r] < cells->row_series[r - 1]))
+      return fail(OTSDB_E_ILLEGAL_ARGUMENT,
+                  "row_series must be nondecreasing series indices");
+  const int64_t M = goff.back();
+  for (int64_t m = 0; m < M; ++m)
+    if (b->group_members[m] < 0 || b->group_members[m] >= S)
+      return fail(OTSDB_E_ILLEGAL_ARGUMENT, "group member out of range");
+  const int64_t QB = R ? cells->qual_off[R] : 0, VB = R ? cells->val_off[R] : 0;
+  const int64_t cap = out->capacity;
+  auto carve = [&](char* base) {
+    Carve cv{base};
+    void* p[11];
+    p[0] = cv.take<int64_t>(R + 1);
+    p[1] = cv.take<int64_t>(R + 1);
+    p[2] = cv.take<int64_t>(R + 1);
+    p[3] = cv.take<uint8_t>(QB + 32);
+    p[4] = cv.take<int64_t>(R + 1);
+    p[5] = cv.take<uint8_t>(VB + 32);
+    p[6] = cv.take<int64_t>(G + 1);
+    p[7] = cv.take<int64_t>(M + 1);
+    p[8] = cv.take<int64_t>(G + 1);
+    p[9] = cv.take<int64_t>(2 * (cap + 1));
+    p[10] = cv.take<uint8_t>(cap + 1);
+    return std::make_pair(cv.off + 256, std::vector<void*>(p, p + 11));
+  };
+  rc = ensure(&c->raw_stage, &c->raw_stage_cap, carve(nullptr).first);
+  if (rc) return rc;
+  auto pp = carve((char*)c->raw_stage).second;
+  hipStream_t st = c->stream;
+  auto h2d = [&](void* d, const void* h, size_t n) -> otsdb_status {
+    if (n && h) HIP_TRY(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, st));
+    return OTSDB_OK;
+  };
+  if ((rc = h2d(pp[0], cells->row_series, 8 * R)) ||
+      (rc = h2d(pp[1], cells->row_base_s, 8 * R)) ||
+      (rc = h2d(pp[2], cells->qual_off, 8 * (R + 1))) ||
+      (rc = h2d(pp[3], cells->qual, QB)) ||
+      (rc = h2d(pp[4], cells->val_off, 8 * (R + 1))) ||
+      (rc = h2d(pp[5], cells->val, VB)) ||
+      (rc = h2d(pp[6], b->group_offsets, 8 * (G + 1))) ||
+      (rc = h2d(pp[7], b->group_members, 8 * M)))
+    return rc;
+  if (R == 0) HIP_TRY(hipMemsetAsync(pp[2], 0, 8, st));
+  if (R == 0) HIP_TRY(hipMemsetAsync(pp[4], 0, 8, st));
+  otsdb_cells dc{R,
+                 (const int64_t*)pp[0],
+                 (const int64_t*)pp[1],
+                 (const int64_t*)pp[2],
+                 (const uint8_t*)pp[3],
+                 (const int64_t*)pp[4],
+                 (const uint8_t*)pp[5]};
+  otsdb_batch db = *b;
+  db.n_points = 0;
+  db.offsets = nullptr;
+  db.ts_ms = nullptr;
+  db.val = nullptr;
+  db.is_float = nullptr;
+  db.series_float = nullptr;
+  db.group_offsets = (const int64_t*)pp[6];
+  db.group_members = (const int64_t*)pp[7];
+  otsdb_result dres;
+  dres.capacity = cap;
+  dres.offsets = (int64_t*)pp[8];
+  dres.ts = (int64_t*)pp[9];
+  dres.val = (int64_t*)pp[9] + (cap + 1);
+  dres.is_int = (uint8_t*)pp[10];
+  rc = run_cells_impl(c, spec, &dc, &db, &dres, goff);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out->offsets, dres.offsets, 8 * (G + 1),
+                         hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const int64_t total = out->offsets[G];
+  if (total > 0) {
+    HIP_TRY(hipMemcpyAsync(out->ts, dres.ts, 8 * total, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(out->val, dres.val, 8 * total, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(out->is_int, dres.is_int, total, hipMemcpyDeviceToHost, st));
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  return OTSDB_OK;
+}
+
 otsdb_status otsdb_prof_enable(otsdb_ctx* c, int enable) {
   if (!c) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
   std::lock_guard<std::mutex> lk(c->mu);

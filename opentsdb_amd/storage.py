@@ -186,3 +186,33 @@ def run_raw(engine, spec, raw, group_offsets, group_members, capacity,
         C.byref(b), C.byref(res)))
     n = int(offs[-1])
     return offs, ts[:n], val[:n], isi[:n]
+
+
+def run_cells(engine, spec, cells, n_series, group_offsets, group_members,
+              capacity):
+    """otsdb_agg_run_cells (host buffers: the JNI entry at the TsdbQuery
+    seam).  cells: dict of numpy arrays (row_series, row_base_s, qual_off,
+    qual, val_off, val) -> (offsets, ts, val, is_int)."""
+    R = len(cells["row_series"])
+    arr = {k: np.ascontiguousarray(v) for k, v in cells.items()}
+    c = abi.Cells(R, arr["row_series"].ctypes.data, arr["row_base_s"].ctypes.data,
+                  arr["qual_off"].ctypes.data, arr["qual"].ctypes.data,
+                  arr["val_off"].ctypes.data, arr["val"].ctypes.data)
+    go = np.ascontiguousarray(group_offsets, np.int64)
+    gm = np.ascontiguousarray(group_members, np.int64)
+    b = abi.Batch()
+    b.n_series = n_series
+    b.n_points = 0
+    b.n_groups = len(go) - 1
+    b.group_offsets = go.ctypes.data
+    b.group_members = gm.ctypes.data if len(gm) else None
+    offs = np.zeros(len(go), np.int64)
+    ts = np.zeros(max(capacity, 1), np.int64)
+    val = np.zeros(max(capacity, 1), np.int64)
+    isi = np.zeros(max(capacity, 1), np.uint8)
+    res = abi.Result(capacity, offs.ctypes.data, ts.ctypes.data, val.ctypes.data,
+                     isi.ctypes.data)
+    engine._check(engine.lib.otsdb_agg_run_cells(
+        engine.ctx, C.byref(spec), C.byref(c), C.byref(b), C.byref(res)))
+    n = int(offs[-1])
+    return offs, ts[:n], val[:n], isi[:n]

@@ -332,3 +332,27 @@ def test_decode_kats(engine, c):
     offs, ts, val, isf = workload.decode_cells_device(engine, cells)
     got = [[int(a), int(b)] for a, b in zip(ts.cpu().numpy(), val.cpu().numpy())]
     assert got == c["expect"] and not isf.any()
+
+
+@pytest.mark.parametrize("agg,ds", [("sum", "1m-avg"), ("max", "5m-max"),
+                                    ("p95", "1m-avg"), ("zimsum", None)])
+def test_host_cells_entry_matches_oracle(engine, agg, ds):
+    """otsdb_agg_run_cells (host buffers: what GpuAggregation.java passes
+    through the JNI shim) against the oracle on the same points."""
+    from opentsdb_amd.engine import DataPoints
+    from tests import cells as CC
+    from tests.test_gpu_parity import compare
+    hb = datasets.random_batch(47, n_series=25, n_groups=5, span_ms=3 * 3600000,
+                               cadence_ms=10000)
+    hb.ts[:] = hb.ts - hb.ts % 1000
+    hb.is_float = np.ones(len(hb.ts), np.uint8)
+    t0, t1 = datasets.T0 + 600000, datasets.T0 + 3 * 3600000
+    d = core.DownsamplingSpecification(ds) if ds else None
+    spec = core.make_spec(t0, t1, core.Aggregators.get(agg), d, t0, t1)
+    ref = pyoracle.group_by(spec, hb)
+    offs, ts, val, isi = storage.run_cells(
+        engine, spec, CC.encode_batch(hb), hb.n_series, hb.group_offsets,
+        hb.group_members, 8 * len(hb.ts) + 64)
+    got = [DataPoints(ts[offs[g]:offs[g + 1]], val[offs[g]:offs[g + 1]],
+                      isi[offs[g]:offs[g + 1]]) for g in range(len(offs) - 1)]
+    compare(got, ref, agg in ("max",) and ds == "5m-max", where="host-cells")
