@@ -168,8 +168,24 @@ class ShardedResult:
             n += int(self.shared.offsets[-1].item())
         return n
 
+    def host_groups(self):
+        """{global group id: (ts, value bits, is_int)} numpy arrays of the
+        groups this rank holds the result of (its own and the shared ones)."""
+        out = {}
+        for ids, res in ((self.local_ids, self.local),
+                         (self.shared_ids, self.shared)):
+            if not len(ids):
+                continue
+            out.update(_host_slices(ids, res))
+        return out
 
-_PLANS = {}
+
+def _host_slices(ids, res):
+    offs = res.offsets.cpu().numpy()
+    ts, val, ii = (res.ts.cpu().numpy(), res.val.cpu().numpy(),
+                   res.is_int.cpu().numpy())
+    return {int(g): (ts[offs[k]:offs[k + 1]], val[offs[k]:offs[k + 1]],
+                     ii[offs[k]:offs[k + 1]]) for k, g in enumerate(ids)}
 
 
 def run_sharded(engine, spec, dbatch, n_groups_global, torch_mod=None,
@@ -185,11 +201,17 @@ def run_sharded(engine, spec, dbatch, n_groups_global, torch_mod=None,
     from .engine import DeviceResult, run_device
 
     if plan is None:
-        key = (id(dbatch), id(engine), spec.agg_id, spec.ds_interval_ms)
-        plan = _PLANS.get(key)
+        # cached on the batch itself (an id()-keyed cache can hand a freed
+        # batch's plan to a new one on one rank only, which then skips the
+        # classification all-reduce the other ranks wait in)
+        plans = getattr(dbatch, "_shard_plans", None)
+        if plans is None:
+            plans = dbatch._shard_plans = {}
+        key = (id(engine), bytes(memoryview(spec).cast("B")), n_groups_global)
+        plan = plans.get(key)
         if plan is None:
-            plan = _PLANS[key] = ShardPlan(engine, spec, dbatch,
-                                           n_groups_global, group)
+            plan = plans[key] = ShardPlan(engine, spec, dbatch,
+                                          n_groups_global, group)
     if len(plan.local):
         run_device(engine, spec, plan.local_batch, plan.local_res)
     shared_res = None
@@ -344,6 +366,9 @@ class _SelResult:
 
     def n_points(self):
         return int(self.res.offsets[-1].item())
+
+    def host_groups(self):
+        return _host_slices(range(len(self.res.offsets) - 1), self.res)
 
 
 def run_sharded_any(engine, spec, dbatch, n_groups_global, group=None):

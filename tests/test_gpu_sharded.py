@@ -156,10 +156,10 @@ def _rank_main(rank, world, port, q):
         db = odist.to_device(odist.shard_host_batch(hb, world, rank))
         res = odist.run_sharded_any(e, spec, db, hb.n_groups)
         torch.cuda.synchronize()
-        out.append([(d.ts.copy(), d.bits.copy(), d.is_int.copy())
-                    for d in _host(res, hb.n_groups)])
-    if rank == 0:
-        q.put(out)
+        # each rank holds its own groups and the shared ones
+        out.append({g: tuple(a.copy() for a in v)
+                    for g, v in res.host_groups().items()})
+    q.put((rank, out))
     tdist.barrier()
     tdist.destroy_process_group()
     e.close()
@@ -175,13 +175,27 @@ def test_two_processes_gloo():
           for r in range(world)]
     for p in ps:
         p.start()
-    out = q.get(timeout=240)
+    import queue
+    import time
+    outs = []
+    deadline = time.time() + 240
+    while len(outs) < world:  # stop early if a rank died
+        assert time.time() < deadline, "ranks did not report"
+        try:
+            outs.append(q.get(timeout=5))
+        except queue.Empty:
+            assert all(p.is_alive() or p.exitcode == 0 for p in ps), \
+                [p.exitcode for p in ps]
     for p in ps:
         p.join(timeout=120)
         assert p.exitcode == 0
     hb = datasets.random_batch(205, n_series=50, n_groups=3, nan_frac=0.02)
-    for (agg, ds, fill), groups in zip(QUERIES, out):
+    for k, (agg, ds, fill) in enumerate(QUERIES):
         ref = pyoracle.group_by(_spec(agg, ds, fill), hb)
-        got = [DataPoints(t, b, i) for t, b, i in groups]
+        merged = {}
+        for _, out in outs:
+            merged.update(out[k])
+        assert sorted(merged) == list(range(hb.n_groups))
+        got = [DataPoints(*merged[g]) for g in range(hb.n_groups)]
         compare(got, ref, ds == "max" and agg not in ("sum", "dev"),
                 where="gloo/%s" % agg)
