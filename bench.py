@@ -48,6 +48,9 @@ def parse():
                     help="skip the secondary compacted-cell figures")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the named-query and PCIe-inclusive figures")
+    ap.add_argument("--named-query", action="store_true",
+                    help="profiling: time BASELINE's sum:1m-avg (LERP) shape "
+                         "over the config's series instead of its query")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / collective rehearsal without the HIP "
                          "engine (CPU tests): times a gloo all-reduce")
@@ -107,21 +110,41 @@ def stage_reader(eng):
     return read
 
 
-def named_query_figure(eng, db, config, warm=3, reps=10):
-    """Secondary figure: the metric's own query shape, sum:1m-avg{host=*}
-    (LERP interpolation), over the same resident C2 series — the ordered
-    group fold with 10,080 one-minute buckets in 5 LDS windows."""
+def named_spec(config):
+    """BASELINE's metric shape, sum:1m-avg{host=*} (LERP), over config's
+    window."""
     from opentsdb_amd import core, workload
-    from opentsdb_amd.engine import DeviceResult, run_device
-    import torch
     c = workload.CONFIGS[config]
     ds = core.DownsamplingSpecification("1m-avg")
     q0 = workload.T0_S
     q1 = q0 + c["days"] * 86400 - 1
-    spec = core.make_spec(core.get_scan_start_time_seconds(q0, ds),
+    return core.make_spec(core.get_scan_start_time_seconds(q0, ds),
                           core.get_scan_end_time_seconds(q1, ds),
                           core.Aggregators.get("sum"), ds, q0 * 1000,
                           q1 * 1000, normalize=True)
+
+
+def pmc_traffic(name):
+    """HBM bytes per launch of the dominant kernel measured by
+    scripts/gpu_pmc.sh for this workload (profiles/pmc_<name>.json)."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % name)
+    if not os.path.exists(pmc):
+        return None
+    with open(pmc) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch",
+                 d.get("k_bucketize_hbm_bytes_per_launch"))
+
+
+def named_query_figure(eng, db, config, warm=3, reps=10):
+    """Secondary figure: the metric's own query shape, sum:1m-avg{host=*}
+    (LERP interpolation), over the same resident C2 series — the ordered
+    group fold with 10,080 one-minute buckets in 5 LDS windows."""
+    from opentsdb_amd import workload
+    from opentsdb_amd.engine import DeviceResult, run_device
+    import torch
+    c = workload.CONFIGS[config]
+    spec = named_spec(config)
     sz = eng.plan(spec, db)
     res = DeviceResult(torch, db.n_groups, int(sz.max_out_points), "cuda")
     read = stage_reader(eng)
@@ -139,7 +162,10 @@ def named_query_figure(eng, db, config, warm=3, reps=10):
            "ms_mean": mean * 1e3,
            "stage_ms": {"fold": st[0], "prep": st[3], "compact": st[4]},
            "kernel": "k_fold (+ k_fold_prep)",
-           "achieved_GBs": BYTES_PER_POINT * n / kf / 1e9 if kf else None}
+           "achieved_GBs": BYTES_PER_POINT * n / kf / 1e9 if kf else None,
+           "algorithmic_bytes_per_launch": BYTES_PER_POINT * n,
+           # scripts/gpu_pmc.sh with bench.py --named-query
+           "traffic": pmc_traffic(config + "_named")}
     out["frac"] = out["achieved_GBs"] / HBM_PEAK_GBS if kf else None
     del res
     return out
@@ -362,7 +388,8 @@ def main():
                                   n_groups=G_glob)
     t_gen = time.perf_counter() - t_gen
     n_points = db.n_points_total
-    spec = workload.query_spec(args.config)
+    spec = (named_spec(args.config) if args.named_query
+            else workload.query_spec(args.config))
     sz = eng.plan(spec, db)
     res = DeviceResult(torch, db.n_groups, int(sz.max_out_points), "cuda")
     last = [None]
@@ -424,10 +451,8 @@ def main():
     # PMC traffic of this exact workload (scripts/gpu_pmc.sh, default size,
     # one GPU, the shipped kernels), per launch of the dominant kernel
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
-    if os.path.exists(pmc) and not args.series and world == 1:
-        with open(pmc) as f:
-            traffic = json.load(f).get("k_bucketize_hbm_bytes_per_launch")
+    if not args.series and world == 1 and not args.named_query:
+        traffic = pmc_traffic(args.config)
 
     extra = {}
     if rank == 0 and world == 1:

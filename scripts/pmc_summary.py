@@ -41,12 +41,15 @@ def main(root):
             d["hbm_write_bytes"] = d["WRITE_SIZE"] * 1024
         out[k[:160]] = d
     # the figure bench.py reports as roofline.traffic: HBM bytes (read,
-    # corrected, + written) per k_bucketize launch, of the busiest variant
-    best = max(out.values(), key=lambda d: d.get("dispatches", 0), default={})
+    # corrected, + written) per launch of the dominant kernel (the most
+    # dispatched downsample / fold variant)
+    best_k = max(out, key=lambda k: (out[k].get("dispatches", 0),
+                                     out[k].get("FETCH_SIZE", 0)), default=None)
+    best = out.get(best_k, {})
     if "hbm_read_bytes_corrected" in best and "hbm_write_bytes" in best:
-        out = {"k_bucketize_hbm_bytes_per_launch":
+        out = {"hbm_bytes_per_launch":
                best["hbm_read_bytes_corrected"] + best["hbm_write_bytes"],
-               "kernels": out}
+               "kernel": best_k, "kernels": out}
     json.dump(out, sys.stdout, indent=1)
     print()
 
