@@ -31,7 +31,8 @@ def main(root):
                 acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     out = {}
     for k, cs in acc.items():
-        if "bucketize" not in k and "k_fold" not in k:
+        if ("bucketize" not in k and "k_fold" not in k
+                and "k_decode" not in k):
             continue
         d = {c: sum(v) / len(v) for c, v in cs.items()}
         d["dispatches"] = max(len(v) for v in cs.values())

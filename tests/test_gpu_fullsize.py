@@ -14,7 +14,7 @@ increase, stay on the grid and inside the window.
 import numpy as np
 import pytest
 
-from opentsdb_amd import workload
+from opentsdb_amd import core, workload
 from opentsdb_amd.batch import HostBatch, groups_from_ids
 from opentsdb_amd.engine import DataPoints, DeviceResult, run_device
 from oracle import pyoracle
@@ -113,11 +113,14 @@ def test_full_size_own_groups(engine, config, n_check):  # noqa: F811
     _free()
 
 
-@pytest.mark.parametrize("config,n_sub", [("C4", 1500), ("C5", 3000)])
-def test_full_size_subset_group(engine, config, n_sub):  # noqa: F811
+@pytest.mark.parametrize("config,n_sub,agg", [("C4", 1500, None),
+                                              ("C5", 3000, None),
+                                              ("C5", 3000, "p999")])
+def test_full_size_subset_group(engine, config, n_sub, agg):  # noqa: F811
     """One-group configurations: every series of the configuration is
     aggregated; a seeded random subset of full-length series forms group 0
-    (checked against the oracle), the rest group 1."""
+    (checked against the oracle), the rest group 1.  C5 names p99 and p999
+    (SURVEY §8d): both run at the full per-GPU size."""
     import torch
     n = workload.default_series_per_gpu(config)
     g = workload.gen_spec(config)
@@ -130,6 +133,8 @@ def test_full_size_subset_group(engine, config, n_sub):  # noqa: F811
     db.group_offsets = torch.from_numpy(g_off).cuda()
     db.group_members = torch.from_numpy(members).cuda()
     spec = workload.query_spec(config)
+    if agg:
+        spec.agg_id = core.Aggregators.get(agg).id
     res, nb = _run(engine, spec, db)
     _check_grid(res, spec, nb)
     hb = _series_to_host(db, sub, np.zeros(n_sub, np.int64))
