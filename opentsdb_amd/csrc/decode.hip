@@ -825,7 +825,12 @@ __global__ __launch_bounds__(256, WAVES) void k_bucketize_cells(
         if (x == 42) Sk.rowv[0] = 1.0;
       } else if (hi > lo)
         reduce_step<M, K, 1>(P, Bd, 1, lo, hi, st0, st0 + (int64_t)K * lane,
-                             t, v, Sk, err, carry_key, carry, true);
+                             t, v, Sk, err, carry_key, carry,
+#ifdef OTSDB_CELLS_NOKEEP  // timing ablation (wrong across rows)
+                             false);
+#else
+                             true);
+#endif
       if (hi < st0 + n_st) {  // reached stop_ts inside this row
         stop_r = r;
         stop_i = hi;

@@ -3,6 +3,13 @@
 // thirteen compilations in parallel; the engine links them).  Non-template
 // kernels are compiled only in engine.hip (OTSDB_DS_TU hides them here).
 #define OTSDB_DS_TU 1
+// fused cells kernel shape (tuning builds override)
+#ifndef OTSDB_CELLS_K
+#define OTSDB_CELLS_K 6
+#endif
+#ifndef OTSDB_CELLS_WAVES
+#define OTSDB_CELLS_WAVES 1
+#endif
 #include "kernels.hip"
 #include "decode.hip"
 #include "fold.hip"
@@ -37,7 +44,8 @@ bool launch_ds(DsKernel k, const DsLaunch& a) {
                          a.SM, a.R);
       return true;
     case DS_CELLS:
-      hipLaunchKernelGGL((k_bucketize_cells<M, 6>), dim3(ds_blocks(S, 4)),
+      hipLaunchKernelGGL((k_bucketize_cells<M, OTSDB_CELLS_K, OTSDB_CELLS_WAVES>),
+                         dim3(ds_blocks(S, 4)),
                          dim3(256), 0, a.st, a.P, a.cells, a.series_row, S,
                          a.SM, a.R, a.err);
       return true;

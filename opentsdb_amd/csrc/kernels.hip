@@ -537,14 +537,17 @@ DEV void reduce_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
   if (keep_open) {
     // more points may follow in a later call (the next storage row of the
     // series): lanes past hi continue the last lane with points, so its
-    // bucket stays open and becomes the carry instead of being written
+    // bucket stays open and becomes the carry instead of being written.
+    // Lanes holding points are contiguous; the ones after the last of them
+    // are exactly the lanes past hi.
     const uint64_t real = __ballot(nseg > 0);
-    const uint64_t below = real & ((1ULL << lane) - 1);
-    const int src = below ? 63 - __builtin_clzll(below) : lane;
-    const int k = __shfl(cur_key, src);
-    if (nseg == 0 && i0 >= lo && below) {
-      cur_key = k;
-      head_key = k;
+    if (real) {
+      const int L = 63 - __builtin_clzll(real);
+      const int k = __builtin_amdgcn_readlane(cur_key, L);
+      if (lane > L) {
+        cur_key = k;
+        head_key = k;
+      }
     }
   }
   // ---- previous step's open bucket
