@@ -171,6 +171,32 @@ def named_query_figure(eng, db, config, warm=3, reps=10):
     return out
 
 
+def p999_figure(eng, db, config, warm=2, reps=5):
+    """C5 names p99 and p999: the p999 query over the same
+    resident series, timed like the headline."""
+    from opentsdb_amd import core, workload
+    from opentsdb_amd.engine import DeviceResult, run_device
+    import torch
+    spec = workload.query_spec(config)
+    spec.agg_id = core.Aggregators.get("p999").id
+    sz = eng.plan(spec, db)
+    res = DeviceResult(torch, db.n_groups, int(sz.max_out_points), "cuda")
+    read = stage_reader(eng)
+    eng.lib.otsdb_prof_enable(eng.ctx, 1)
+    read()
+    med, mean = timed_reps(lambda: run_device(eng, spec, db, res), warm, reps)
+    st = read()
+    eng.lib.otsdb_prof_enable(eng.ctx, 0)
+    n = db.n_points_total
+    del res
+    return {"query": "p999:1m-avg-nan over the same series", "value": n / med,
+            "unit": "data points/s", "ms_median": med * 1e3,
+            "ms_mean": mean * 1e3,
+            "stage_ms": {"downsample": st[0], "transform": st[1],
+                         "group_select": st[2], "prep": st[3],
+                         "compact": st[4]}}
+
+
 def pcie_figure(eng, config):
     """PCIe-inclusive rate (not the headline): otsdb_agg_run from host
     buffers — H2D of the columns, the query, D2H of the result — at C1 and
@@ -460,6 +486,8 @@ def main():
             extra["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
         if not args.no_extra and args.config == "C2":
             extra["named_query"] = named_query_figure(eng, db, args.config)
+        if not args.no_extra and args.config == "C5":
+            extra["p999"] = p999_figure(eng, db, args.config)
         if not args.no_extra:
             extra["pcie_inclusive"] = pcie_figure(eng, args.config)
 
@@ -519,7 +547,7 @@ def main():
             },
             "cpu_baseline": extra.get("cpu_baseline"),
         }
-        for k in ("named_query", "pcie_inclusive", "decode"):
+        for k in ("named_query", "p999", "pcie_inclusive", "decode"):
             if k in extra:
                 line[k] = extra[k]
         print(json.dumps(line), flush=True)

@@ -518,19 +518,34 @@ __global__ __launch_bounds__(SS_THREADS) void k_seg_select(
   double r = qnan();
   const uint64_t* col = keys + b * M + lg_off[lg];
   const int64_t k = lg_k[lg];
-  // every key of the segment, 4 independent loads in flight per thread
+  // every key of the segment: 16-byte loads (two keys), 4 in flight per
+  // thread; a key before the first 16-byte boundary and an odd last one
+  // singly
   auto for_keys = [&](auto&& f) {
+    const int64_t head = ((uintptr_t)col & 15) ? 1 : 0;
+    if (head && k > 0 && tid == 0) f(col[0]);
+    const int64_t np = (k - head) >> 1;  // pairs
+    const ulonglong2* c2 = reinterpret_cast<const ulonglong2*>(col + head);
     int64_t i = tid;
-    for (; i + 3 * SS_THREADS < k; i += 4 * SS_THREADS) {
-      const uint64_t a0 = col[i], a1 = col[i + SS_THREADS],
-                     a2 = col[i + 2 * SS_THREADS],
-                     a3 = col[i + 3 * SS_THREADS];
-      f(a0);
-      f(a1);
-      f(a2);
-      f(a3);
+    for (; i + 3 * SS_THREADS < np; i += 4 * SS_THREADS) {
+      const ulonglong2 a0 = c2[i], a1 = c2[i + SS_THREADS],
+                       a2 = c2[i + 2 * SS_THREADS],
+                       a3 = c2[i + 3 * SS_THREADS];
+      f(a0.x);
+      f(a0.y);
+      f(a1.x);
+      f(a1.y);
+      f(a2.x);
+      f(a2.y);
+      f(a3.x);
+      f(a3.y);
     }
-    for (; i < k; i += SS_THREADS) f(col[i]);
+    for (; i < np; i += SS_THREADS) {
+      const ulonglong2 a = c2[i];
+      f(a.x);
+      f(a.y);
+    }
+    if (((k - head) & 1) && tid == 0) f(col[k - 1]);
   };
   // (1) min / max (fused: and count) over the non-NONE keys: from
   // k_keys_transpose's per-(64-member tile, bucket) partials for the tiles
@@ -581,14 +596,29 @@ __global__ __launch_bounds__(SS_THREADS) void k_seg_select(
       const int w = shift < SS_BITS ? shift : SS_BITS;
       shift -= w;
       const uint32_t dm = (1u << w) - 1;
-      for (int j = tid; j < 2 * SS_BINS; j += SS_THREADS) (&h[0][0])[j] = 0;
+      // targets still sharing their prefix (the two order statistics of an
+      // interpolating estimator usually do) share one histogram
+      const bool two = nt == 2 && prefix[1] != prefix[0];
+      for (int j = tid; j < (two ? 2 : 1) * SS_BINS; j += SS_THREADS)
+        (&h[0][0])[j] = 0;
       __syncthreads();
-      for_keys([&](uint64_t key) {
-        if (key == KEY_NONE) return;
-        const uint32_t d = (uint32_t)(key >> shift) & dm;
-        if ((key & mask[0]) == prefix[0]) atomicAdd(&h[0][d], 1u);
-        if (nt == 2 && (key & mask[1]) == prefix[1]) atomicAdd(&h[1][d], 1u);
-      });
+      if (two) {
+        for_keys([&](uint64_t key) {
+          if (key == KEY_NONE) return;
+          const uint32_t d = (uint32_t)(key >> shift) & dm;
+          if ((key & mask[0]) == prefix[0]) atomicAdd(&h[0][d], 1u);
+          if ((key & mask[1]) == prefix[1]) atomicAdd(&h[1][d], 1u);
+        });
+      } else {
+        for_keys([&](uint64_t key) {
+          if (key == KEY_NONE) return;
+          if ((key & mask[0]) == prefix[0])
+            atomicAdd(&h[0][(uint32_t)(key >> shift) & dm], 1u);
+        });
+      }
+      __syncthreads();
+      if (nt == 2 && !two)
+        for (int j = tid; j < SS_BINS; j += SS_THREADS) h[1][j] = h[0][j];
       __syncthreads();
       // per target: the digit whose cumulative count passes the rank (one
       // wave per target scans its bins, 32 per lane)
@@ -635,11 +665,13 @@ __global__ __launch_bounds__(SS_THREADS) void k_seg_select(
       else need[t] = true;
     }
     if (need[0] || need[1]) {
+      // targets with the same remaining prefix gather one candidate set
+      const bool same = need[0] && need[1] && prefix[0] == prefix[1];
       if (tid < 2) s_nc[tid] = 0;
       __syncthreads();
       for_keys([&](uint64_t key) {
         if (key == KEY_NONE) return;
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < (same ? 1 : 2); ++t) {
           if (need[t] && (key & mask[t]) == prefix[t]) {
             const uint32_t q = atomicAdd(&s_nc[t], 1u);
             if (q < SS_CAP) cand[t][q] = key;
@@ -649,14 +681,15 @@ __global__ __launch_bounds__(SS_THREADS) void k_seg_select(
       __syncthreads();
       for (int t = 0; t < 2; ++t) {
         if (!need[t]) continue;
-        const int nc = (int)(s_nc[t] < SS_CAP ? s_nc[t] : SS_CAP);
+        const int src = same ? 0 : t;
+        const int nc = (int)(s_nc[src] < SS_CAP ? s_nc[src] : SS_CAP);
         const int64_t rr = rank[t];
         for (int j = tid; j < nc; j += SS_THREADS) {
-          const uint64_t x = cand[t][j];
+          const uint64_t x = cand[src][j];
           int less = 0, eq = 0;
           for (int q = 0; q < nc; ++q) {
-            less += cand[t][q] < x;
-            eq += cand[t][q] == x;
+            less += cand[src][q] < x;
+            eq += cand[src][q] == x;
           }
           if (rr >= less && rr < less + eq) s_pick[t] = x;  // ties: same key
         }
