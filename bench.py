@@ -271,10 +271,11 @@ def decode_figure(eng, config, n_series, reps=5):
                     "(17 B/point); not part of the headline value",
             "fused_query": {
                 "what": "the same C2 query straight from the cells, decode "
-                        "fused into the downsample (k_bucketize_cells)",
+                        "fused into the ordered group fold",
+                "kernel": "k_fold<cells> (+ k_cells_prep)",
                 "value": n / dq, "unit": "data points/s",
                 "ms_per_query": dq * 1e3,
-                "k_bucketize_cells_ms": kb * 1e3,
+                "kernel_ms": kb * 1e3,
                 "achieved_GBs_compacted": cb / kb / 1e9 if kb else None,
                 "frac_of_8TBs": cb / kb / 8e12 if kb else None}}
 

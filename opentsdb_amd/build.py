@@ -5,8 +5,9 @@ resulting .so travels to the GPU box with the repository snapshot.
 
 The device code is split over translation units compiled in parallel: the
 engine (host code, the non-template kernels and the aggregator-templated
-ones) and one unit per downsampling monoid (csrc/ds_tu.hip with
--DOTSDB_DS_MONOID=n: the downsample / ordered-fold kernels of that monoid).
+ones) and two units per downsampling monoid (csrc/ds_tu.hip with
+-DOTSDB_DS_MONOID=n: the downsample / ordered-fold kernels of that monoid,
+and with -DOTSDB_DS_PART=1 the cells fold of that monoid).
 """
 import glob
 import os
@@ -46,10 +47,13 @@ def _units(out_dir, defines):
     d = ["-D" + x for x in defines]
     units = [(os.path.join(CSRC, "engine.hip"), d,
               os.path.join(out_dir, "engine.o"))]
-    for m in range(N_DS_MONOIDS):
-        units.append((os.path.join(CSRC, "ds_tu.hip"),
-                      d + ["-DOTSDB_DS_MONOID=%d" % m],
-                      os.path.join(out_dir, "ds_%d.o" % m)))
+    # part 1 (the cells fold, cellfold.hip) first: its units are the longest
+    for part in (1, 0):
+        for m in range(N_DS_MONOIDS):
+            units.append((os.path.join(CSRC, "ds_tu.hip"),
+                          d + ["-DOTSDB_DS_MONOID=%d" % m,
+                               "-DOTSDB_DS_PART=%d" % part],
+                          os.path.join(out_dir, "ds_%d_%d.o" % (part, m))))
     return units
 
 
@@ -81,9 +85,20 @@ def build(force=False, verbose=False, jobs=None, defines=(), out=None):
         return obj
 
     units = _units(out_dir, defines)
-    # the engine unit is the longest: start it first
+    # incremental: a unit is rebuilt when a source it may include is newer
+    # than its object (only part-1 units include cellfold.hip)
+    def stale(u):
+        src, extra, obj = u
+        if force or not os.path.exists(obj):
+            return True
+        t = os.path.getmtime(obj)
+        part1 = "-DOTSDB_DS_PART=1" in extra
+        return any(os.path.getmtime(d) > t for d in DEPS
+                   if part1 or not d.endswith("cellfold.hip"))
+    todo = [u for u in units if stale(u)]
     with ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(compile_unit, units))
+        list(ex.map(compile_unit, todo))
+    objs = [u[2] for u in units]
     cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o",
            OUT_ + ".tmp"] + objs
     if verbose:

@@ -21,7 +21,7 @@
 namespace otsdb {
 
 
-enum : int { ERR_CORRUPT_CELL = 16 };
+enum : int { ERR_CORRUPT_CELL = 1 << 21 };  // (16 is ERR_X1_MASK)
 
 // map {0,1}->{0,1} as 2 bits: bit0 = f(0), bit1 = f(1)
 DEV int fmap_apply(int f, int s) { return (f >> s) & 1; }

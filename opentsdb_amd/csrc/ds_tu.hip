@@ -10,9 +10,15 @@
 #ifndef OTSDB_CELLS_WAVES
 #define OTSDB_CELLS_WAVES 1
 #endif
+#ifndef OTSDB_DS_PART
+#define OTSDB_DS_PART 0  // 0: launch_ds kernels, 1: the cells fold
+#endif
 #include "kernels.hip"
 #include "decode.hip"
 #include "fold.hip"
+#if OTSDB_DS_PART == 1
+#include "cellfold.hip"
+#endif
 
 namespace otsdb {
 
@@ -22,6 +28,36 @@ inline unsigned ds_blocks(int64_t n, int per) {
 }
 }  // namespace
 
+#if OTSDB_DS_PART == 1
+// the cells fold: prep + k_fold<M, A, 8, 1> x every aggregator
+template <class M>
+bool launch_cells(DsKernel k, const DsLaunch& a) {
+  const int64_t S = a.B.S;
+  switch (k) {
+    case DS_CELLS_PREP:
+      if (S > 0)
+        hipLaunchKernelGGL(k_cells_prep<M>, dim3(ds_blocks(S, 256)), dim3(256),
+                           0, a.st, a.P, a.cf, S, a.SM, a.err);
+      OTSDB_DBG(a.st, "k_cells_prep");
+      return true;
+    case DS_CELLS_FOLD:
+      return with_monoid(a.agg_id, [&](auto tag) {
+        using A = decltype(tag);
+        hipLaunchKernelGGL((k_fold<M, A, 8, 1>),
+                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(256), 0,
+                           a.st, a.P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
+                           a.tm1, a.single, a.members, a.wc, a.NW, a.partial,
+                           a.tile_emit, a.out_val, a.out_emit, a.err,
+                           a.always_partial, a.cf);
+        OTSDB_DBG(a.st, "k_fold<cells>");
+      });
+    default:
+      return false;
+  }
+}
+#define OTSDB_LAUNCH launch_cells
+#else
+#define OTSDB_LAUNCH launch_ds
 template <class M>
 bool launch_ds(DsKernel k, const DsLaunch& a) {
   const int64_t S = a.B.S;
@@ -63,40 +99,41 @@ bool launch_ds(DsKernel k, const DsLaunch& a) {
                            a.st, a.P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
                            a.tm1, a.single, a.members, a.wc, a.NW, a.partial,
                            a.tile_emit, a.out_val, a.out_emit, a.err,
-                           a.always_partial);
+                           a.always_partial, a.cf);
         OTSDB_DBG(a.st, "k_fold");
       });
   }
   return false;
 }
+#endif
 
 #ifndef OTSDB_DS_MONOID
 #error "compile with -DOTSDB_DS_MONOID=<0..12>"
 #endif
 #if OTSDB_DS_MONOID == 0
-template bool launch_ds<MSum<0>>(DsKernel, const DsLaunch&);
+template bool OTSDB_LAUNCH<MSum<0>>(DsKernel, const DsLaunch&);
 #elif OTSDB_DS_MONOID == 1
-template bool launch_ds<MSum<1>>(DsKernel, const DsLaunch&);
+template bool OTSDB_LAUNCH<MSum<1>>(DsKernel, const DsLaunch&);
 #elif OTSDB_DS_MONOID == 2
-template bool launch_ds<MSum<2>>(DsKernel, const DsLaunch&);
+template bool OTSDB_LAUNCH<MSum<2>>(DsKernel, const DsLaunch&);
 #elif OTSDB_DS_MONOID == 3
-template bool launch_ds<MSum<3>>(DsKernel, const DsLaunch&);
+template bool OTSDB_LAUNCH<MSum<3>>(DsKernel, const DsLaunch&);
 #elif OTSDB_DS_MONOID == 4
-template bool launch_ds<MMinMax<false>>(DsKernel, const DsLaunch&);
+template bool OTSDB_LAUNCH<MMinMax<false>>(DsKernel, const DsLaunch&);
 #elif OTSDB_DS_MONOID == 5
-template bool launch_ds<MMinMax<true>>(DsKernel, const DsLaunch&);
+template bool OTSDB_LAUNCH<MMinMax<true>>(DsKernel, const DsLaunch&);
 #elif OTSDB_DS_MONOID == 6
-template bool launch_ds<MDev>(DsKernel, const DsLaunch&);
+template bool OTSDB_LAUNCH<MDev>(DsKernel, const DsLaunch&);
 #elif OTSDB_DS_MONOID == 7
-template bool launch_ds<MFirstLast<false>>(DsKernel, const DsLaunch&);
+template bool OTSDB_LAUNCH<MFirstLast<false>>(DsKernel, const DsLaunch&);
 #elif OTSDB_DS_MONOID == 8
-template bool launch_ds<MFirstLast<true>>(DsKernel, const DsLaunch&);
+template bool OTSDB_LAUNCH<MFirstLast<true>>(DsKernel, const DsLaunch&);
 #elif OTSDB_DS_MONOID == 9
-template bool launch_ds<MMult>(DsKernel, const DsLaunch&);
+template bool OTSDB_LAUNCH<MMult>(DsKernel, const DsLaunch&);
 #elif OTSDB_DS_MONOID == 10
-template bool launch_ds<MDiff>(DsKernel, const DsLaunch&);
+template bool OTSDB_LAUNCH<MDiff>(DsKernel, const DsLaunch&);
 #elif OTSDB_DS_MONOID == 11
-template bool launch_ds<MNone>(DsKernel, const DsLaunch&);
+template bool OTSDB_LAUNCH<MNone>(DsKernel, const DsLaunch&);
 #endif
 
 }  // namespace otsdb

@@ -572,11 +572,11 @@ DsLaunch ds_args(otsdb_ctx* c, const Params& P, const BatchDev& B,
 }
 
 // Whether the ordered group fold (fold.hip) runs this query: every
-// downsampled, non-rate query with a monoid aggregator, fill or not.
-bool fold_path(const otsdb_query_spec* spec, const Params& P, bool cells,
-               int mode) {
-  return !cells && !P.ds_sel && !P.rate && !P.run_all &&
-         !is_selection(spec->agg_id) && mode != 2;
+// downsampled, non-rate query with a monoid aggregator, fill or not (from
+// compacted cells: when the grid fits one fold window, cellfold.hip).
+bool fold_path(const otsdb_query_spec* spec, const Params& P, int mode) {
+  return !P.ds_sel && !P.rate && !P.run_all && !is_selection(spec->agg_id) &&
+         mode != 2;
 }
 
 // Everything up to dense (group, bucket) results / partials.
@@ -597,7 +597,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   if (rc) return rc;
   const Tiles T = tiles_of(c, G);
   const int64_t nb = P.nb;
-  const bool fold = fold_path(spec, P, cells != nullptr, mode);
+  bool fold = fold_path(spec, P, mode);
 
   // grid trimming for very wide windows (NONE fill only): the rows span only
   // the buckets that hold data
@@ -625,10 +625,6 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   if (NB > (int64_t)INT32_MAX - 2)
     return fail(OTSDB_E_UNSUPPORTED, "bucket grid of %lld buckets per series",
                 (long long)NB);
-  // the bucket matrix (series rows) exists only off the fold path
-  if (!fold && (double)S * (double)NB > 2.0e10)
-    return fail(OTSDB_E_UNSUPPORTED, "bucket grid too large (%lld x %lld)",
-                (long long)S, (long long)NB);
   int64_t WB = 0, NW = 0;
   if (fold) {
     if (!with_monoid(spec->agg_id, [&](auto tag) {
@@ -637,6 +633,17 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       return fail(OTSDB_E_NO_SUCH_ELEMENT, "aggregator %d", spec->agg_id);
     NW = (NB + WB - 1) / WB;
   }
+  // the cells fold runs one window (no k_fold_prep over cells); wider grids
+  // from cells take k_bucketize_cells and the row pipeline
+  if (cells && fold && NW > 1) {
+    fold = false;
+    WB = NW = 0;
+  }
+  const bool cfold = cells && fold;
+  // the bucket matrix (series rows) exists only off the fold path
+  if (!fold && (double)S * (double)NB > 2.0e10)
+    return fail(OTSDB_E_UNSUPPORTED, "bucket grid too large (%lld x %lld)",
+                (long long)S, (long long)NB);
 
   // workspace
   const bool sel_large = is_selection(spec->agg_id) && (T.LG > 0 || mode == 2);
@@ -645,6 +652,11 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
                          (double)n_comb * kCombineSlices * NB * 33.0 < 2.0e9;
   const size_t rows = fold ? 0 : (size_t)S * NB;
   WinCtx* wc = nullptr;
+  CellsFold CF{};
+  if (cfold) {
+    CF.C = *cells;
+    CF.series_row = series_row;
+  }
   auto carve = [&](char* base) {
     Carve cv{base};
     W.SM.lo = cv.take<int64_t>(S);
@@ -664,6 +676,12 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     W.out_emit = cv.take<uint8_t>((size_t)G * NB);
     W.counts = cv.take<int64_t>(G + 1);
     if (NW > 1) wc = cv.take<WinCtx>((size_t)S * (NW - 1));
+    if (cfold) {
+      CF.rlo = cv.take<int64_t>(S);
+      CF.vlo = cv.take<int64_t>(S);
+      CF.qw = cv.take<uint8_t>(S);
+      CF.vl0 = cv.take<uint8_t>(S);
+    }
     if (two_level) {
       W.comb = cv.take<Packed>((size_t)n_comb * kCombineSlices * NB);
       W.comb_emit = cv.take<uint8_t>((size_t)n_comb * kCombineSlices * NB);
@@ -710,12 +728,17 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       using M = decltype(tag);
       {
         StageTimer tm(c, 3);
-        launch_ds<M>(DS_PREP, a);
-        if (NW > 1) {
-          a.wc = wc;
-          a.NW = NW;
-          a.WB = WB;
-          launch_ds<M>(DS_FOLD_PREP, a);
+        if (cfold) {
+          a.cf = CF;
+          launch_cells<M>(DS_CELLS_PREP, a);
+        } else {
+          launch_ds<M>(DS_PREP, a);
+          if (NW > 1) {
+            a.wc = wc;
+            a.NW = NW;
+            a.WB = WB;
+            launch_ds<M>(DS_FOLD_PREP, a);
+          }
         }
       }
       StageTimer tm(c, 0);
@@ -734,7 +757,10 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       a.out_emit = W.out_emit;
       a.always_partial = mode == 1;
       a.agg_id = spec->agg_id;
-      if (T.T > 0) launch_ds<M>(DS_FOLD, a);
+      if (T.T > 0) {
+        if (cfold) launch_cells<M>(DS_CELLS_FOLD, a);
+        else launch_ds<M>(DS_FOLD, a);
+      }
     });
     if (!ok) return fail(OTSDB_E_UNSUPPORTED, "downsampler %d", spec->ds_agg_id);
   } else if (cells && S > 0 && NB > 0) {

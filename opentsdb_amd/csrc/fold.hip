@@ -430,7 +430,22 @@ struct FoldKernel {
 // k_fold: see the file header.  Single-chunk groups finish here (out_val /
 // out_emit); chunks of larger groups (and every chunk with always_partial,
 // the multi-GPU partials) leave their window of partials for k_combine.
+// A cells member's stream context (CELLS = 1, cellfold.hip), kept in LDS
+struct CellsMember {
+  int64_t qb;     // qualifier byte offset of the series' point 0
+  int64_t vb0;    // value byte offset of its first row
+  int64_t vcur;   // value byte offset of point pa
+  int64_t rlo;    // row holding point pa
+  int64_t r1;     // one past the series' last row
+  int64_t qend, vend;  // readable bytes of the pools
+  int32_t qw, vl0;
+};
+
 template <class M, class A, int K>
+DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
+                           const FoldMember* mc, const CellsMember* cm);
+
+template <class M, class A, int K, int CELLS = 0>
 __global__ __launch_bounds__(256, OTSDB_FOLD_WAVES) void k_fold(
     Params P, BatchDev B, SeriesMeta SM, int64_t n_tiles,
     const int64_t* __restrict__ tile_g, const int64_t* __restrict__ tile_m0,
@@ -439,7 +454,7 @@ __global__ __launch_bounds__(256, OTSDB_FOLD_WAVES) void k_fold(
     const int64_t* __restrict__ members, const WinCtx* __restrict__ wc,
     int64_t NW, Packed* __restrict__ partial, uint8_t* __restrict__ tile_emit,
     double* __restrict__ out_val, uint8_t* __restrict__ out_emit,
-    int* err_word, int always_partial) {
+    int* err_word, int always_partial, CellsFold CF) {
   constexpr int WB = fold_wb<A>();
   __shared__ A st[WB];
   __shared__ uint8_t emit[WB];
@@ -448,6 +463,7 @@ __global__ __launch_bounds__(256, OTSDB_FOLD_WAVES) void k_fold(
   __shared__ int s_next;
   __shared__ FoldKernel kc;
   __shared__ FoldMember mc[4];
+  __shared__ CellsMember cm[CELLS ? 4 : 1];
   const int tid = threadIdx.x, lane = LANE, w = tid >> 6;
   const int64_t nb = P.nb;
   int32_t W0, W1;
@@ -531,8 +547,24 @@ __global__ __launch_bounds__(256, OTSDB_FOLD_WAVES) void k_fold(
       }
       m.sf = kc.series_float ? (int)kc.series_float[s] : 1;
       mc[w] = m;
+      if (CELLS) {
+        CellsMember c;
+        c.qb = CF.C.qual_off[CF.series_row[s]];
+        c.vb0 = CF.C.val_off[CF.series_row[s]];
+        c.r1 = CF.series_row[s + 1];
+        c.rlo = CF.rlo[s];
+        c.vcur = CF.vlo[s];
+        c.qw = CF.qw[s];
+        c.vl0 = CF.vl0[s];
+        c.qend = CF.C.qual_off[CF.C.R];
+        c.vend = CF.C.val_off[CF.C.R];
+        cm[CELLS ? w : 0] = c;
+      }
     }
-    fold_member<M, A, K>(P, B, F, &mc[w]);
+    if constexpr (CELLS != 0)
+      fold_member_cells<M, A, K>(P, CF.C, F, &mc[w], &cm[w]);
+    else
+      fold_member<M, A, K>(P, B, F, &mc[w]);
     fold_publish(F, kProgDone);
   }
   __syncthreads();

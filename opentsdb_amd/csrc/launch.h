@@ -33,6 +33,19 @@ struct WinCtx {
   double next_val;
 };
 
+// A cells fold (k_cells_prep -> k_fold<..., CELLS = 1>, cellfold.hip): the
+// compacted columns and what the prep derives per series.  A series' points
+// are numbered by qualifier: point p's qualifier sits at byte
+// qual_off[first row] + qw * p (rows are contiguous in the pools).
+struct CellsFold {
+  CellsDev C;
+  const int64_t* series_row;  // [S + 1] first row of each series
+  int64_t* rlo;               // row holding point lo
+  int64_t* vlo;               // byte offset in C.val of point lo's value
+  uint8_t* qw;                // qualifier width of the series (2 / 4)
+  uint8_t* vl0;               // value length of point lo (first guess)
+};
+
 // buckets per fold window: the aggregator states of a window live in LDS
 template <class A>
 constexpr int fold_wb() {
@@ -45,7 +58,9 @@ enum DsKernel {
   DS_RATE,       // k_bucketize_k with RateSpan fused into the ring flush
   DS_CELLS,      // k_bucketize_cells: decode fused into the downsample
   DS_FOLD_PREP,  // k_fold_prep: window boundaries of the ordered fold
-  DS_FOLD        // k_fold: downsample + contribution + ordered aggregator
+  DS_FOLD,       // k_fold: downsample + contribution + ordered aggregator
+  DS_CELLS_PREP, // k_cells_prep: bounds / cursors of a cells fold
+  DS_CELLS_FOLD  // k_fold fed straight from compacted columns
 };
 
 struct DsLaunch {
@@ -71,6 +86,8 @@ struct DsLaunch {
   uint8_t* out_emit;
   int always_partial;
   int agg_id;
+  // DS_CELLS_PREP / DS_CELLS_FOLD
+  CellsFold cf;
 };
 
 // Debug builds (-DOTSDB_DEBUG_SYNC): every launch reports itself and waits
@@ -95,5 +112,8 @@ struct DsLaunch {
 // monoid; false when the kernel does not exist for (M, agg).
 template <class M>
 bool launch_ds(DsKernel k, const DsLaunch& a);
+// the cells fold kernels (ds_tu.hip part 1, their own translation units)
+template <class M>
+bool launch_cells(DsKernel k, const DsLaunch& a);
 
 }  // namespace otsdb

@@ -12,6 +12,6 @@ for v in ${VARIANTS:-prod}; do
 import json, sys
 d = json.loads(open("gpurun_out/abc_%s.json" % sys.argv[1]).read().strip().splitlines()[-1])
 f = d["decode"]["fused_query"]
-print("%-10s cells kernel %8.2f ms  query %8.2f ms" % (sys.argv[1], f["k_bucketize_cells_ms"], f["ms_per_query"]), flush=True)
+print("%-10s cells kernel %8.2f ms  query %8.2f ms" % (sys.argv[1], f["kernel_ms"], f["ms_per_query"]), flush=True)
 PY
 done
