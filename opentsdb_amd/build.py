@@ -95,6 +95,7 @@ def build(force=False, verbose=False, jobs=None, defines=(), out=None):
         part1 = "-DOTSDB_DS_PART=1" in extra
         return any(os.path.getmtime(d) > t for d in DEPS
                    if part1 or not d.endswith("cellfold.hip"))
+
     todo = [u for u in units if stale(u)]
     with ThreadPoolExecutor(jobs) as ex:
         list(ex.map(compile_unit, todo))

@@ -338,10 +338,7 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
   static_assert(K == 8, "qualifier loads assume 8 points per lane");
   const int lane = LANE;
   const bool kept = uni(mc->kept) != 0;
-  F.flushed = F.W0;
-  F.pend = uni(mc->has_prev) ? F.W0 : -1;
-  F.x0 = uni(mc->px);
-  F.y0 = uni(mc->py);
+  fold_member_init(P, F, mc);
   if (!kept) return;
   const int32_t pe = (int32_t)uni(mc->pb);
   const int64_t r1 = uni(cm->r1);
@@ -463,6 +460,22 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
     int32_t a0 = act ? vcur + ((K * lane) << vsh) + mbefore : vcur;
     if (!vnear) cells_vload_vl(1 << vsh, vp, (uint32_t)a0, d);
     else cells_vload_bytes(vp, a0, vlim, d);
+#if defined(OTSDB_CELLS_ABL) && OTSDB_CELLS_ABL == 2  // timing: loads only
+    {
+      uint32_t x = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x ^= dq[i];
+#pragma unroll
+      for (int i = 0; i < 20; ++i) x ^= d[i];
+      if (x == 42) F.emit[0] = 1;
+      const int32_t hs = sb;
+      vcur += ((hs - p) << vsh) + (ps1 <= hs ? m0 : 0) + (ps2 <= hs ? m1 : 0) +
+              (ps3 <= hs ? m2 : 0);
+      ra += (ps1 <= hs ? 1 : 0) + (ps2 <= hs ? 1 : 0) + (ps3 <= hs ? 1 : 0);
+      p = hs;
+      continue;
+    }
+#endif
     // ---- buckets below the open one are final: drain them while the
     // loads are in flight (fold_member)
     const bool carry_ok = carry_key >= 0 && carry_key < P.nb;
@@ -613,8 +626,17 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
         hs == sb ? k_hi : fold_bucket(P, cells_pick<K>(t, hs - 1 - p));
     // a step cut at a row rule (not at a bucket edge) leaves the bucket of
     // its last point open: it carries into the next step (keep_open)
+#if defined(OTSDB_CELLS_ABL) && OTSDB_CELLS_ABL == 1  // timing: no reduction
+    {
+      int64_t x = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) x ^= t[j] + v[j];
+      if (x == 42) F.emit[0] = 1;
+    }
+#else
     reduce_step<M, K, 1>(P, Bd, 1, p, hs, p, p0, t, v, S, err, carry_key,
                          carry, hs < pe);
+#endif
     vcur += used + (ps1 <= hs ? m0 : 0) + (ps2 <= hs ? m1 : 0) +
             (ps3 <= hs ? m2 : 0);
     ra += (ps1 <= hs ? 1 : 0) + (ps2 <= hs ? 1 : 0) + (ps3 <= hs ? 1 : 0);
@@ -643,21 +665,7 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
   if (carry_key >= 0 && carry_key < P.nb && lane == 0)
     S.put(carry_key, carry.finish(&err));
   if (prev_hi >= 0) fold_flush(P, F, prev_hi + 1);
-  if (P.fill) {
-    if (F.flushed < F.W1) {
-      fold_wait(F, F.W1);
-      for (int32_t j0 = F.flushed; j0 < F.W1; j0 += 64) {
-        const int32_t b = j0 + lane;
-        if (b < F.W1) {
-          F.st[b - F.W0].push(P.fill_value);
-          F.emit[b - F.W0] = 1;
-        }
-      }
-    }
-  } else if (F.pend >= 0 && F.pend < F.W1 && uni(mc->has_next)) {
-    fold_wait(F, F.W1);
-    fold_fill_gap(P, F, F.pend, F.W1, uni(mc->nx), uni(mc->ny));
-  }
+  fold_member_tail(P, F, mc);
 }
 
 }  // namespace otsdb

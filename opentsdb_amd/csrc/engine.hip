@@ -91,6 +91,12 @@ inline int64_t jmod(int64_t a, int64_t b) { return a % b; }
 inline int64_t align_down(int64_t t, int64_t iv) { return t - jmod(t, iv); }
 
 constexpr int64_t kChunk = 256;  // series per cross-series chunk
+// members per tile of the ordered fold: one tile is one workgroup that
+// streams all its members' points, so big groups (C3's 62k-series
+// datacenters, C4's single 500k-series group) are cut finer than kChunk —
+// 256-member tiles of one day of points leave the last round of
+// workgroups half empty
+constexpr int64_t kFoldChunk = 64;
 
 struct Carve {
   char* base;
@@ -143,6 +149,7 @@ struct otsdb_ctx {
   int64_t n_tiles = 0, n_multi = 0, n_large = 0, n_large_chunks = 0;
   int64_t max_chunks = 0;  // most chunks in one group
   bool tiles_sel_all = false;
+  int64_t tiles_chunk = 0;
   std::mutex mu;  // one query at a time per context
   // stage timing (otsdb_prof_*)
   bool prof = false;
@@ -378,8 +385,9 @@ otsdb_status make_params(const otsdb_query_spec* s, Params* P,
 // sel_all: every group (even one without local members) joins the radix
 // select lists — the cross-rank selection protocol needs global segments
 otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff,
-                         bool sel_all = false) {
-  if (c->d_tiles && goff == c->goff_cache && sel_all == c->tiles_sel_all)
+                         bool sel_all = false, int64_t chunk = kChunk) {
+  if (c->d_tiles && goff == c->goff_cache && sel_all == c->tiles_sel_all &&
+      chunk == c->tiles_chunk)
     return OTSDB_OK;
   const int64_t G = (int64_t)goff.size() - 1;
   std::vector<int64_t> tg, tm0, tm1, mg, mt0, mt1, ag, at0, at1;
@@ -388,10 +396,10 @@ otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff,
   for (int64_t g = 0; g < G; ++g) {
     const int64_t a = goff[g], b = goff[g + 1];
     const int64_t t0 = (int64_t)tg.size();
-    for (int64_t m = a; m < b; m += kChunk) {
+    for (int64_t m = a; m < b; m += chunk) {
       tg.push_back(g);
       tm0.push_back(m);
-      tm1.push_back(std::min(b, m + kChunk));
+      tm1.push_back(std::min(b, m + chunk));
     }
     const int64_t t1 = (int64_t)tg.size();
     for (int64_t t = t0; t < t1; ++t) single.push_back(t1 - t0 == 1);
@@ -448,6 +456,7 @@ otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff,
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->goff_cache = goff;
   c->tiles_sel_all = sel_all;
+  c->tiles_chunk = chunk;
   c->n_tiles = T;
   c->n_multi = MG;
   c->n_large = LG;
@@ -573,7 +582,9 @@ DsLaunch ds_args(otsdb_ctx* c, const Params& P, const BatchDev& B,
 
 // Whether the ordered group fold (fold.hip) runs this query: every
 // downsampled, non-rate query with a monoid aggregator, fill or not (from
-// compacted cells: when the grid fits one fold window, cellfold.hip).
+// compacted cells, cellfold.hip: when the grid fits one fold window).
+// Rate queries keep RateSpan in k_bucketize_k's ring flush + k_group: a
+// RateSpan-in-the-fold build measured slower on C4.
 bool fold_path(const otsdb_query_spec* spec, const Params& P, int mode) {
   return !P.ds_sel && !P.rate && !P.run_all && !is_selection(spec->agg_id) &&
          mode != 2;
@@ -593,9 +604,6 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   hipStream_t st = c->stream;
   const int64_t S = B.S;
   const int64_t G = (int64_t)goff.size() - 1;
-  otsdb_status rc = build_tiles(c, goff, mode == 2);
-  if (rc) return rc;
-  const Tiles T = tiles_of(c, G);
   const int64_t nb = P.nb;
   bool fold = fold_path(spec, P, mode);
 
@@ -635,11 +643,14 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   }
   // the cells fold runs one window (no k_fold_prep over cells); wider grids
   // from cells take k_bucketize_cells and the row pipeline
-  if (cells && fold && NW > 1) {
+  if (cells && NW > 1) {
     fold = false;
     WB = NW = 0;
   }
   const bool cfold = cells && fold;
+  otsdb_status rc = build_tiles(c, goff, mode == 2, fold ? kFoldChunk : kChunk);
+  if (rc) return rc;
+  const Tiles T = tiles_of(c, G);
   // the bucket matrix (series rows) exists only off the fold path
   if (!fold && (double)S * (double)NB > 2.0e10)
     return fail(OTSDB_E_UNSUPPORTED, "bucket grid too large (%lld x %lld)",

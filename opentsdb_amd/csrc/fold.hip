@@ -287,6 +287,38 @@ struct FoldMember {
   int32_t kept, sf, has_prev, has_next;
 };
 
+template <class A>
+DEV void fold_member_init(const Params& P, FoldSink<A>& F,
+                          const FoldMember* mc) {
+  F.flushed = F.W0;
+  F.pend = uni(mc->has_prev) ? F.W0 : -1;
+  F.x0 = uni(mc->px);
+  F.y0 = uni(mc->py);
+}
+
+// A member's buckets after its last point: FillingDownsampler fill, or the
+// interpolation toward the point past the window.
+template <class A>
+DEV void fold_member_tail(const Params& P, FoldSink<A>& F,
+                          const FoldMember* mc) {
+  const int lane = LANE;
+  if (P.fill) {
+    if (F.flushed < F.W1) {
+      fold_wait(F, F.W1);
+      for (int32_t j0 = F.flushed; j0 < F.W1; j0 += 64) {
+        const int32_t b = j0 + lane;
+        if (b < F.W1) {
+          F.st[b - F.W0].push(P.fill_value);
+          F.emit[b - F.W0] = 1;
+        }
+      }
+    }
+  } else if (F.pend >= 0 && F.pend < F.W1 && uni(mc->has_next)) {
+    fold_wait(F, F.W1);
+    fold_fill_gap(P, F, F.pend, F.W1, uni(mc->nx), uni(mc->ny));
+  }
+}
+
 template <class M, class A, int K>
 DEV void fold_member(const Params& P, const BatchDev& B, FoldSink<A>& F,
                      const FoldMember* mc) {
@@ -295,10 +327,7 @@ DEV void fold_member(const Params& P, const BatchDev& B, FoldSink<A>& F,
   const bool kept = uni(mc->kept) != 0;
   const int sf = uni(mc->sf);
   const int64_t pa = uni(mc->pa), pb = uni(mc->pb);
-  F.flushed = F.W0;
-  F.pend = uni(mc->has_prev) ? F.W0 : -1;
-  F.x0 = uni(mc->px);
-  F.y0 = uni(mc->py);
+  fold_member_init(P, F, mc);
   if (!kept) return;  // contributes nowhere (SpanGroup.add dropped it)
   RowSink S{nullptr, nullptr, F.ring, FOLD_WIN - 1, 0, 0, 0, 0};
   int err = 0;
@@ -395,21 +424,7 @@ DEV void fold_member(const Params& P, const BatchDev& B, FoldSink<A>& F,
     S.put(carry_key, carry.finish(&err));
   if (prev_hi >= 0) fold_flush(P, F, prev_hi + 1);
   // the window's remaining buckets
-  if (P.fill) {
-    if (F.flushed < F.W1) {
-      fold_wait(F, F.W1);
-      for (int32_t j0 = F.flushed; j0 < F.W1; j0 += 64) {
-        const int32_t b = j0 + lane;
-        if (b < F.W1) {
-          F.st[b - F.W0].push(P.fill_value);
-          F.emit[b - F.W0] = 1;
-        }
-      }
-    }
-  } else if (F.pend >= 0 && F.pend < F.W1 && uni(mc->has_next)) {
-    fold_wait(F, F.W1);
-    fold_fill_gap(P, F, F.pend, F.W1, uni(mc->nx), uni(mc->ny));
-  }
+  fold_member_tail(P, F, mc);
 }
 
 // the kernel's own arguments the member loop and the finalisation read,
@@ -456,8 +471,12 @@ __global__ __launch_bounds__(256, OTSDB_FOLD_WAVES) void k_fold(
     double* __restrict__ out_val, uint8_t* __restrict__ out_emit,
     int* err_word, int always_partial, CellsFold CF) {
   constexpr int WB = fold_wb<A>();
-  __shared__ A st[WB];
-  __shared__ uint8_t emit[WB];
+  // the window's aggregator states and emit flags: dynamic LDS sized for
+  // min(WB, nb) buckets (fold_lds_bytes), so a short grid leaves room for
+  // more workgroups per CU
+  extern __shared__ __attribute__((aligned(16))) unsigned char fold_dyn[];
+  A* st = reinterpret_cast<A*>(fold_dyn);
+  uint8_t* emit = fold_dyn + fold_lds_states<A>(P.nb);
   __shared__ double ring[4][FOLD_WIN];
   __shared__ int32_t prog[256];
   __shared__ int s_next;

@@ -47,9 +47,25 @@ struct CellsFold {
 };
 
 // buckets per fold window: the aggregator states of a window live in LDS
+// (2,048 x 24-byte dev / diff states + ring + marks: 57 KB, within the
+// 64 KB a workgroup may hold; the states are dynamic LDS sized for the
+// grid, fold_lds_bytes)
 template <class A>
 constexpr int fold_wb() {
-  return sizeof(A) <= 16 ? 2048 : 1024;
+  return sizeof(A) <= 24 ? 2048 : 1024;
+}
+
+// dynamic LDS of k_fold: the states of min(WB, nb) buckets, then as many
+// emit flags (16-byte aligned pieces)
+template <class A>
+__host__ __device__ constexpr size_t fold_lds_states(int64_t nb) {
+  return (((size_t)(nb < fold_wb<A>() ? nb : fold_wb<A>()) * sizeof(A)) + 15) &
+         ~(size_t)15;
+}
+template <class A>
+constexpr size_t fold_lds_bytes(int64_t nb) {
+  return fold_lds_states<A>(nb) +
+         ((((size_t)(nb < fold_wb<A>() ? nb : fold_wb<A>())) + 15) & ~(size_t)15);
 }
 
 enum DsKernel {
