@@ -66,6 +66,9 @@ namespace otsdb {
 #ifndef OTSDB_FOLD_WAVES
 #define OTSDB_FOLD_WAVES 1
 #endif
+#ifndef OTSDB_CELLS_FOLD_WAVES  // the cells fold: at most 168 VGPRs
+#define OTSDB_CELLS_FOLD_WAVES 3
+#endif
 constexpr int FOLD_WIN = 128;  // per-wave ring of closed bucket values
 constexpr int FOLD_FL = OTSDB_FOLD_FL;  // flush once this many buckets are final
 constexpr int32_t kProgDone = INT32_MAX;
@@ -461,7 +464,8 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
                            const FoldMember* mc, const CellsMember* cm);
 
 template <class M, class A, int K, int CELLS = 0>
-__global__ __launch_bounds__(256, OTSDB_FOLD_WAVES) void k_fold(
+__global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
+                                        : OTSDB_FOLD_WAVES) void k_fold(
     Params P, BatchDev B, SeriesMeta SM, int64_t n_tiles,
     const int64_t* __restrict__ tile_g, const int64_t* __restrict__ tile_m0,
     const int64_t* __restrict__ tile_m1,
