@@ -506,3 +506,41 @@ def test_rate_long_gaps(engine, ri):
                      rate=True, ro=RATES[ri])
         check(engine, spec, hb, agg == "max",
               where="rategap%d/%s/%s" % (ri, agg, ds))
+
+
+# ------------------------------------------------ fold order / determinism
+def _cancel_batch(n_series, reps=180, cadence_ms=60000):
+    """n_series series on a one-point-per-minute grid (1m buckets hold one
+    point: the downsample is exact) whose values cancel: 1e17, 1, -1e17,
+    1, 1e17, ... — a sum's result depends on the order of the adds
+    (1e17 + 1 == 1e17)."""
+    from opentsdb_amd.batch import HostBatch, groups_from_ids
+    pattern = np.array([1e17, 1.0, -1e17, 1.0])
+    t = datasets.T0 + cadence_ms * np.arange(reps, dtype=np.int64)
+    ts = np.tile(t, n_series)
+    v = np.repeat(pattern[np.arange(n_series) % 4], reps)
+    offs = np.arange(n_series + 1, dtype=np.int64) * reps
+    g_off, members = groups_from_ids(np.zeros(n_series, np.int64), 1)
+    return HostBatch(offs, ts, v.view(np.int64), np.ones(len(ts), np.uint8),
+                     None, g_off, members)
+
+
+@pytest.mark.parametrize("agg", ["sum", "zimsum", "avg", "dev"])
+def test_fold_order_cancellation(engine, agg):
+    """The ordered group fold feeds the aggregator in SpanCmp order
+    (Aggregators.java:246-258 Sum.runDouble adds in span order): on values
+    whose sum depends on the order of the adds, a group inside one fold
+    tile is bit-exact with the reference's order, and every group —
+    several tiles merged in order included — gives bit-identical results
+    run after run."""
+    spec = _spec(agg, "avg")
+    one_tile = _cancel_batch(7)
+    check(engine, spec, one_tile, exact=True, where="cancel/%s/1tile" % agg)
+    many = _cancel_batch(203)  # four 64-member tiles + a partial one
+    first = engine.run(spec, many)
+    for _ in range(2):
+        again = engine.run(spec, many)
+        for a, b in zip(first, again):
+            assert np.array_equal(np.asarray(a.ts), np.asarray(b.ts))
+            assert np.array_equal(np.asarray(a.bits), np.asarray(b.bits)), (
+                "%s: run-to-run difference" % agg)
