@@ -13,7 +13,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from opentsdb_amd import build  # noqa: E402
 
-build.build()  # production objects up to date
+if not os.environ.get("OTSDB_NO_PROD_BUILD"):
+    build.build()  # production objects up to date
 
 
 UNITS = os.environ.get("OTSDB_UNITS", "1_1").split(",")

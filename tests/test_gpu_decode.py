@@ -327,3 +327,72 @@ def test_fused_cells_host_formats(engine, name, kind, rng_i, f4, ms, agg, ds):
     fl = cancel_floor(hb, 60) if kind == "int" else 0.0  # mixed signs
     compare(got, ref, agg == "max", floor=fl,
             where="fused-host/%s/%s/%s" % (name, agg, ds))
+
+
+def _ragged_rows_batch(seed, n_series, hours, kind):
+    """Series whose storage rows hold 1 (no meta byte), 2-7 (fewer than a
+    lane's 8 points: the cells fold cuts its step before such a row when it
+    sits inside one), ~30 or 360 points, in random order — the row shapes
+    sparse or irregular series give."""
+    from opentsdb_amd.batch import HostBatch, groups_from_ids
+    rng = np.random.default_rng(seed)
+    offs, tss, vals = [0], [], []
+    for s in range(n_series):
+        t = []
+        for h in range(hours):
+            n = int(rng.choice([0, 1, 2, 3, 5, 7, 8, 30, 360],
+                               p=[.05, .15, .1, .1, .1, .1, .1, .15, .15]))
+            if n:
+                sec = np.sort(rng.choice(3600, n, replace=False))
+                t.append(datasets.T0 + h * 3600000 + sec * 1000)
+        t = np.concatenate(t) if t else np.zeros(0, np.int64)
+        if kind == "float":
+            v = (rng.random(len(t)) * 100.0).view(np.int64)
+        else:  # 1/2/4/8-byte longs mixed inside rows
+            v = rng.integers(-(1 << 40), 1 << 40, len(t)) >> rng.integers(0, 40, len(t))
+        tss.append(t.astype(np.int64))
+        vals.append(v.astype(np.int64))
+        offs.append(offs[-1] + len(t))
+    gid = np.arange(n_series) % 3
+    g_off, members = groups_from_ids(gid, 3)
+    ts, val = np.concatenate(tss), np.concatenate(vals)
+    isf = np.full(len(ts), 1 if kind == "float" else 0, np.uint8)
+    return HostBatch(np.array(offs, np.int64), ts, val, isf, None, g_off,
+                     members)
+
+
+@pytest.mark.parametrize("kind", ["float", "int"])
+@pytest.mark.parametrize("agg,ds,window", [
+    ("sum", "5m-avg", "whole"), ("max", "1m-max", "whole"),
+    ("zimsum", "7m-count", "whole"), ("avg", "10m-sum", "mid-row"),
+    ("min", "1m-first", "mid-row")])
+def test_fused_cells_ragged_rows(engine, kind, agg, ds, window):
+    """The cells fold over rows of 1 to 360 points (steps cut before short
+    inner rows, single-point rows without a meta byte, lanes crossing row
+    boundaries), windows starting and ending inside rows, doubles and
+    mixed-width longs: against the oracle on the points RowSeq decodes."""
+    import torch
+    from opentsdb_amd import workload
+    from opentsdb_amd.engine import DeviceResult
+    from tests.test_gpu_parity import compare, cancel_floor
+    hb = _ragged_rows_batch(7 if kind == "float" else 8, 45, 24, kind)
+    enc = cells.encode_batch(hb)
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda()
+         for k, v in enc.items()}
+    dc = workload.DeviceCells(d, hb.n_series)
+    db = _device_batch(hb, kind)
+    if window == "whole":
+        t0, t1 = datasets.T0, datasets.T0 + 24 * 3600000 - 1000
+    else:
+        t0, t1 = datasets.T0 + 1234567, datasets.T0 + 20 * 3600000 + 777000
+    spec = core.make_spec(t0, t1, core.Aggregators.get(agg),
+                          core.DownsamplingSpecification(ds), t0, t1)
+    ref = pyoracle.group_by(spec, hb)
+    res = DeviceResult(torch, db.n_groups, 4 * len(hb.ts) + 64, "cuda")
+    workload.run_cells_device(engine, spec, dc, db, res)
+    got = _result_points(res, db.n_groups)
+    fn = ds.split("-")[1]
+    exact = fn in ("max", "count", "first") and agg in ("max", "min")
+    fl = cancel_floor(hb, 400) if kind == "int" else 0.0  # mixed signs
+    compare(got, ref, exact, where="ragged/%s/%s/%s" % (kind, agg, ds),
+            floor=fl)
