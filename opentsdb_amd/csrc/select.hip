@@ -591,7 +591,65 @@ __global__ __launch_bounds__(SS_THREADS) void k_seg_select(
       rank[t] = s0.rank[t];
       cnt[t] = s0.n;
     }
-    // (2) digit passes while some target has too many candidates
+    // (2a) the first pass bins by an OFFSET digit, (key >> s1) - (mn >> s1)
+    // with the smallest s1 whose range fits the 2,048 bins, instead of the
+    // top 11 bits below the common prefix: for doubles of one sign those are
+    // mostly exponent bits (cpu% values 1..100 use 7 of the 2,048 bins and
+    // a p99 target keeps ~1/3 of the keys), while the offset digit resolves
+    // the exponent and the leading mantissa bits in one pass — one pass over
+    // the keys less before the gather.  Monotone in the key, so the target's
+    // bin is again a bit prefix (bits >= s1) for the passes below.
+    if (shift > 0 && (cnt[0] > SS_CAP || (nt == 2 && cnt[1] > SS_CAP))) {
+      int s1 = 64 - __builtin_clzll(mx - mn) - SS_BITS;
+      if (s1 < 0) s1 = 0;
+      while (s1 < 64 && (mx >> s1) - (mn >> s1) >= (uint64_t)SS_BINS) ++s1;
+      const uint64_t b1 = mn >> s1;
+      for (int j = tid; j < SS_BINS; j += SS_THREADS) h[0][j] = 0;
+      __syncthreads();
+      for_keys([&](uint64_t key) {
+        if (key == KEY_NONE) return;
+        atomicAdd(&h[0][(uint32_t)((key >> s1) - b1)], 1u);
+      });
+      __syncthreads();
+      if (nt == 2)
+        for (int j = tid; j < SS_BINS; j += SS_THREADS) h[1][j] = h[0][j];
+      __syncthreads();
+      const int wv = tid >> 6, lane = LANE;
+      if (wv < nt) {
+        const int per = SS_BINS / 64;
+        uint32_t sum = 0;
+        for (int j = 0; j < per; ++j) sum += h[wv][lane * per + j];
+        uint32_t incl = sum;
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t y = __shfl_up(incl, d);
+          if (lane >= d) incl += y;
+        }
+        const int64_t excl = (int64_t)incl - sum;
+        const int64_t rr = rank[wv];
+        if (rr >= excl && rr < (int64_t)incl) {
+          int64_t cum = excl;
+          int j = 0;
+          for (; j < per - 1; ++j) {
+            const uint32_t c = h[wv][lane * per + j];
+            if (rr < cum + c) break;
+            cum += c;
+          }
+          s_digit[wv] = lane * per + j;
+          s_below[wv] = cum;
+          s_cnt[wv] = h[wv][lane * per + j];
+        }
+      }
+      __syncthreads();
+      for (int t = 0; t < nt; ++t) {
+        mask[t] = s1 >= 64 ? 0ULL : ~0ULL << s1;
+        prefix[t] = s1 >= 64 ? 0ULL : (b1 + (uint64_t)s_digit[t]) << s1;
+        rank[t] -= s_below[t];
+        cnt[t] = s_cnt[t];
+      }
+      shift = s1;
+      __syncthreads();
+    }
+    // (2b) digit passes while some target has too many candidates
     while (shift > 0 && (cnt[0] > SS_CAP || (nt == 2 && cnt[1] > SS_CAP))) {
       const int w = shift < SS_BITS ? shift : SS_BITS;
       shift -= w;
