@@ -45,7 +45,7 @@ bool launch_cells(DsKernel k, const DsLaunch& a) {
         using A = decltype(tag);
         hipLaunchKernelGGL((k_fold<M, A, 8, 1>),
                            dim3((unsigned)(a.n_tiles * a.NW)), dim3(256),
-                           (unsigned)fold_lds_bytes<A>(a.P.nb),
+                           (unsigned)fold_lds_bytes<A>(a.P),
                            a.st, a.P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
                            a.tm1, a.single, a.members, a.wc, a.NW, a.partial,
                            a.tile_emit, a.out_val, a.out_emit, a.err,
@@ -97,7 +97,7 @@ bool launch_ds(DsKernel k, const DsLaunch& a) {
         using A = decltype(tag);
         hipLaunchKernelGGL((k_fold<M, A, 8>),
                            dim3((unsigned)(a.n_tiles * a.NW)), dim3(256),
-                           (unsigned)fold_lds_bytes<A>(a.P.nb),
+                           (unsigned)fold_lds_bytes<A>(a.P),
                            a.st, a.P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
                            a.tm1, a.single, a.members, a.wc, a.NW, a.partial,
                            a.tile_emit, a.out_val, a.out_emit, a.err,

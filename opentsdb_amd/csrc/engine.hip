@@ -97,6 +97,10 @@ constexpr int64_t kChunk = 256;  // series per cross-series chunk
 // day of points leave the last round of workgroups half empty (C3 fold:
 // 256 -> 2.9 ms, 64 -> 2.57 ms, 32 -> 2.53 ms)
 constexpr int64_t kFoldChunk = 32;
+// below this many (tile, window) workgroups the fold narrows its windows,
+// down to kFoldMinWindow buckets
+constexpr int64_t kFoldMinBlocks = 2048;
+constexpr int64_t kFoldMinWindow = 128;
 
 struct Carve {
   char* base;
@@ -651,6 +655,22 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   otsdb_status rc = build_tiles(c, goff, mode == 2, fold ? kFoldChunk : kChunk);
   if (rc) return rc;
   const Tiles T = tiles_of(c, G);
+  P.fold_wb = 0;  // (P may come from an earlier pipeline run)
+  // few tiles (small queries, e.g. C1's 100 groups of 10 series): narrower
+  // fold windows give the grid more workgroups — each window's workgroup
+  // streams only that window's points (k_fold_prep hands it the context)
+  if (fold && !cfold && T.T > 0 && NB > kFoldMinWindow &&
+      T.T * NW < kFoldMinBlocks) {
+    const int64_t want = (kFoldMinBlocks + T.T - 1) / T.T;  // windows
+    int64_t wb = (NB + want - 1) / want;
+    wb = (wb + 63) / 64 * 64;
+    if (wb < kFoldMinWindow) wb = kFoldMinWindow;
+    if (wb < WB) {
+      WB = wb;
+      NW = (NB + WB - 1) / WB;
+      P.fold_wb = (int32_t)WB;
+    }
+  }
   // the bucket matrix (series rows) exists only off the fold path
   if (!fold && (double)S * (double)NB > 2.0e10)
     return fail(OTSDB_E_UNSUPPORTED, "bucket grid too large (%lld x %lld)",

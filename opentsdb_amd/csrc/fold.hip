@@ -480,7 +480,7 @@ __global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
   // more workgroups per CU
   extern __shared__ __attribute__((aligned(16))) unsigned char fold_dyn[];
   A* st = reinterpret_cast<A*>(fold_dyn);
-  uint8_t* emit = fold_dyn + fold_lds_states<A>(P.nb);
+  uint8_t* emit = fold_dyn + fold_lds_states<A>(P);
   __shared__ double ring[4][FOLD_WIN];
   __shared__ int32_t prog[256];
   __shared__ int s_next;
@@ -493,8 +493,9 @@ __global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
   {
     const int64_t t = (int64_t)blockIdx.x % n_tiles;
     const int64_t win = (int64_t)blockIdx.x / n_tiles;
-    W0 = (int32_t)(win * WB);
-    W1 = (int32_t)((W0 + WB < nb) ? W0 + WB : nb);
+    const int64_t wb = fold_window<A>(P);  // <= WB
+    W0 = (int32_t)(win * wb);
+    W1 = (int32_t)((W0 + wb < nb) ? W0 + wb : nb);
     if (tid == 0) {
       kc.SM = SM;
       kc.members = members;

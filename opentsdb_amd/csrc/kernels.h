@@ -82,7 +82,9 @@ struct Params {
   // only_redo, skip every other series
   uint8_t* redo;
   int32_t only_redo;
-  int32_t _pad3;
+  // buckets per window of the ordered fold (k_fold / k_fold_prep); 0: the
+  // largest the aggregator state allows (fold_wb)
+  int32_t fold_wb;
 };
 
 // value bits of an absent bucket in sentinel rows: a signalling NaN, which

@@ -55,17 +55,25 @@ constexpr int fold_wb() {
   return sizeof(A) <= 24 ? 2048 : 1024;
 }
 
-// dynamic LDS of k_fold: the states of min(WB, nb) buckets, then as many
-// emit flags (16-byte aligned pieces)
+// the fold's window: P.fold_wb buckets when the engine narrowed it (more
+// workgroups for queries with few tiles), else fold_wb<A>()
 template <class A>
-__host__ __device__ constexpr size_t fold_lds_states(int64_t nb) {
-  return (((size_t)(nb < fold_wb<A>() ? nb : fold_wb<A>()) * sizeof(A)) + 15) &
-         ~(size_t)15;
+__host__ __device__ constexpr int64_t fold_window(const Params& P) {
+  return P.fold_wb > 0 ? (int64_t)P.fold_wb : (int64_t)fold_wb<A>();
+}
+// dynamic LDS of k_fold: the states of min(window, nb) buckets, then as
+// many emit flags (16-byte aligned pieces)
+template <class A>
+__host__ __device__ constexpr int64_t fold_cap(const Params& P) {
+  return P.nb < fold_window<A>(P) ? P.nb : fold_window<A>(P);
 }
 template <class A>
-constexpr size_t fold_lds_bytes(int64_t nb) {
-  return fold_lds_states<A>(nb) +
-         ((((size_t)(nb < fold_wb<A>() ? nb : fold_wb<A>())) + 15) & ~(size_t)15);
+__host__ __device__ constexpr size_t fold_lds_states(const Params& P) {
+  return (((size_t)fold_cap<A>(P) * sizeof(A)) + 15) & ~(size_t)15;
+}
+template <class A>
+constexpr size_t fold_lds_bytes(const Params& P) {
+  return fold_lds_states<A>(P) + ((((size_t)fold_cap<A>(P)) + 15) & ~(size_t)15);
 }
 
 enum DsKernel {
