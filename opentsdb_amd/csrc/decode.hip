@@ -885,28 +885,61 @@ __global__ __launch_bounds__(256, WAVES) void k_bucketize_cells(
     if (!ok) {
       atomicOr(err_word, ERR_CAL_RANGE);
     } else {
-      M st = M::init();
       int64_t r = stop_r, i = stop_i;
-      while (r < r1) {
-        if (i >= w.n) {
-          if (++r >= r1) break;
-          w = cell_row(C, r);
-          if (!w.ok) break;
-          i = 0;
-          voff = 0;
-          continue;
+      // folds the points of [.., end) from (r, i) on, across rows; false
+      // when the span has no point left
+      auto fold_until = [&](int64_t end, double* out) -> bool {
+        M st = M::init();
+        bool any = false;
+        while (r < r1) {
+          if (i >= w.n) {
+            if (++r >= r1) break;
+            w = cell_row(C, r);
+            if (!w.ok) {
+              r = r1;
+              break;
+            }
+            i = 0;
+            voff = 0;
+            continue;
+          }
+          const uint32_t q = cell_qual(w, i);
+          if (qual_ts(w.base_ms, w.qw, q) >= end) break;
+          const int l = (int)(q & 0x7) + 1;
+          st.push(bits_to_double(dbits_of(
+              load_be(C.val, w.vbase + voff, l, vend), l, (q & 0x8) != 0)));
+          voff += l;
+          ++i;
+          any = true;
         }
-        const uint32_t q = cell_qual(w, i);
-        if (qual_ts(w.base_ms, w.qw, q) >= e) break;
-        const int l = (int)(q & 0x7) + 1;
-        st.push(bits_to_double(dbits_of(
-            load_be(C.val, w.vbase + voff, l, vend), l, (q & 0x8) != 0)));
-        voff += l;
-        ++i;
-      }
-      int e2 = 0;
-      of_val = st.finish(&e2);
+        int e2 = 0;
+        *out = st.finish(&e2);
+        return any;
+      };
+      fold_until(e, &of_val);
       of_has = 1;
+      if (P.rate) {  // kept rates past that bucket (k_prep's rates_beyond)
+        auto next = [&](int64_t* tn, double* vn) -> bool {
+          if (r >= r1 || i >= w.n) return false;
+          const int64_t tt = qual_ts(w.base_ms, w.qw, cell_qual(w, i));
+          int64_t bt, be;
+          if (P.cal) {
+            const int64_t k = cal_bucket(P, tt);
+            if (k < P.cal_lo || k + 1 >= P.cal_n) return false;
+            bt = P.cal[k];
+            be = P.cal[k + 1];
+          } else {
+            bt = align_ts(tt, P.interval);
+            be = bt + P.interval;
+          }
+          *tn = bt;
+          return fold_until(be, vn);
+        };
+        double r1v = 0.0;
+        const int kb = rates_beyond(P, of_ts, of_val, next, &r1v);
+        of_has |= (uint8_t)(kb << 1);
+        SM.of_rate[s] = r1v;
+      }
     }
   }
   if (__ballot(err) && lane == 0) atomicOr(err_word, err);

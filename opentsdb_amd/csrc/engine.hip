@@ -694,6 +694,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     W.SM.hi = cv.take<int64_t>(S);
     W.SM.of_ts = cv.take<int64_t>(S);
     W.SM.of_val = cv.take<double>(S);
+    W.SM.of_rate = cv.take<double>(S);
     W.SM.kf = cv.take<int32_t>(S);
     W.SM.kl = cv.take<int32_t>(S);
     W.SM.keep = cv.take<uint8_t>(S);

@@ -107,9 +107,12 @@ struct SeriesMeta {
   int32_t* kf;  // bucket of the first / last point in [lo, hi) (kf > kl:
   int32_t* kl;  // none) — the span sentinel rows are written over
   uint8_t* keep;
-  uint8_t* of_has;
+  uint8_t* of_has;  // bit 0: a bucket past the window (of_ts, of_val);
+                    // rate queries, bits 1-2: kept rates after that
+                    // bucket (0..2, capped), the first of them in of_rate
   int64_t* of_ts;
   double* of_val;
+  double* of_rate;
 };
 
 struct Rows {

@@ -106,6 +106,49 @@ DEV void k_prep_store(const Params& P, const BatchDev& B, SeriesMeta SM,
   SM.of_val[s] = of_val;
 }
 
+// RateSpan's rate between two bucket points (RateSpan.java:121-180); kept =
+// false for a counter reset RateSpan drops (dropResets)
+DEV double rate_between(const Params& P, int64_t t0, double v0, int64_t t1,
+                        double v1, bool* kept) {
+  const double dt = (double)(t1 - t0) / 1000.0;
+  double diff = v1 - v0;
+  *kept = true;
+  if (P.counter && diff < 0) {
+    if (P.drop_resets) {
+      *kept = false;
+      return 0.0;
+    }
+    diff = (double)P.counter_max - v0 + v1;
+    const double r = diff / dt;
+    return (P.reset_value > 0 && r > (double)P.reset_value) ? 0.0 : r;
+  }
+  return diff / dt;
+}
+
+// Rate queries: the kept rates AFTER the first bucket past the window.  The
+// reference's rate mode pre-consumes each span's first (junk) rate and keeps
+// the span contributing while it has a second one (AggregationIterator.java:
+// 448-459) — those rates may all lie past the window (a series whose
+// outage covers the whole window), so the bucket past it is not enough.
+// next(): fills (t, v) with the next bucket point after the previous one,
+// false when the span has no more.  Returns the count (capped at 2) and the
+// first rate in *r1.
+template <class Next>
+DEV int rates_beyond(const Params& P, int64_t t, double v, Next&& next,
+                     double* r1) {
+  int n = 0;
+  int64_t tn;
+  double vn;
+  for (int guard = 0; n < 2 && guard < (1 << 20) && next(&tn, &vn); ++guard) {
+    bool kept;
+    const double r = rate_between(P, t, v, tn, vn, &kept);
+    if (kept && n++ == 0) *r1 = r;
+    t = tn;
+    v = vn;  // RateSpan continues from a dropped reset's point too
+  }
+  return n;
+}
+
 template <class M>
 __global__ void k_prep(Params P, BatchDev B, SeriesMeta SM, int* err_word) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -138,11 +181,43 @@ __global__ void k_prep(Params P, BatchDev B, SeriesMeta SM, int* err_word) {
         e = of_ts + P.interval;
       }
       M st = M::init();
-      for (int64_t i = hi; i < p1 && B.ts[i] < e; ++i)
+      int64_t i = hi;
+      for (; i < p1 && B.ts[i] < e; ++i)
         st.push(point_value(B, i, B.val[i], sf));
       int err = 0;
       of_val = st.finish(&err);
       of_has = 1;
+      // (percentile downsampling: k_ds_select fills of_val later and the
+      // bucket values here are counts — its rate rows use the bucket past
+      // the window alone)
+      if (P.rate && !P.ds_sel) {
+        // the next bucket points: fixed-interval buckets (the row path takes
+        // rate queries; calendar grids step their table)
+        auto next = [&](int64_t* tn, double* vn) -> bool {
+          if (i >= p1) return false;
+          int64_t bt, be;
+          if (P.cal) {
+            const int64_t k = cal_bucket(P, B.ts[i]);
+            if (k < P.cal_lo || k + 1 >= P.cal_n) return false;
+            bt = P.cal[k];
+            be = P.cal[k + 1];
+          } else {
+            bt = align_ts(B.ts[i], P.interval);
+            be = bt + P.interval;
+          }
+          M b = M::init();
+          for (; i < p1 && B.ts[i] < be; ++i)
+            b.push(point_value(B, i, B.val[i], sf));
+          int e2 = 0;
+          *tn = bt;
+          *vn = b.finish(&e2);
+          return true;
+        };
+        double r1 = 0.0;
+        const int kb = rates_beyond(P, of_ts, of_val, next, &r1);
+        of_has |= (uint8_t)(kb << 1);
+        SM.of_rate[s] = r1;
+      }
     }
   }
   k_prep_store(P, B, SM, s, keep, lo, hi, of_has, of_ts, of_val);
@@ -674,25 +749,52 @@ DEV void ring_after(const Params& P, const BatchDev& B, RowSink& S,
 // the first kept rate -> the junk rate, held; past the last kept rate ->
 // absent, or the latest rate held toward a point past the window
 // (AggregationIterator.java:448-459, :744-753).  kl: the last flushed bucket.
+// The rates past the window (rates_beyond): is the rate at the bucket past
+// it kept, its value, and whether any kept rate lies past the window.
+struct PastRates {
+  bool of_kept, any;
+  int n;          // kept rates past the window, capped at 2
+  double first;   // the first of them
+};
+DEV PastRates past_rates(const Params& P, const SeriesMeta& SM, int64_t s,
+                         int64_t carry_pts, double carry_pv) {
+  PastRates q{false, false, 0, 0.0};
+  const int h = SM.of_has[s];
+  if (!(h & 1)) return q;
+  const double r = rate_between(P, carry_pts, carry_pv, SM.of_ts[s],
+                                SM.of_val[s], &q.of_kept);
+  const int kb = (h >> 1) & 3;
+  q.n = (q.of_kept ? 1 : 0) + kb;
+  if (q.n > 2) q.n = 2;
+  q.first = q.of_kept ? r : SM.of_rate[s];
+  q.any = q.n > 0;
+  return q;
+}
+
 DEV void rate_finish(const Params& P, const SeriesMeta& SM, int64_t s,
                      RowSink& S, const RateState& R, int64_t kl) {
   const int lane = LANE;
   const int64_t nb = P.nb;
-  bool of_kept = false;
-  if (SM.of_has[s]) {
-    const double diff = SM.of_val[s] - R.carry_pv;
-    of_kept = !(P.counter && diff < 0 && P.drop_resets);
-  }
-  const int total = R.kept_count + (of_kept ? 1 : 0);
+  const PastRates q = past_rates(P, SM, s, R.carry_pts, R.carry_pv);
+  const int total = R.kept_count + q.n;
   if (total < 2) {
     for (int64_t b = lane; b < nb; b += 64) S.rows[b] = ST_ABSENT;
+    return;
+  }
+  if (R.kept_count == 0) {
+    // every kept rate lies past the window: the first one (the junk rate)
+    // is held over the whole grid
+    for (int64_t b = lane; b < nb; b += 64) {
+      S.rowv[b] = q.first;
+      S.rows[b] = ST_INTERP;
+    }
     return;
   }
   for (int64_t b = lane; b < R.r0_idx; b += 64) {
     S.rowv[b] = R.r0_val;
     S.rows[b] = ST_INTERP;
   }
-  if (!of_kept) {
+  if (!q.any) {
     for (int64_t b = R.last_kept + 1 + lane; b < nb; b += 64)
       S.rows[b] = ST_ABSENT;
   } else {
@@ -719,15 +821,15 @@ DEV void bucketize_series(const Params& P, const BatchDev& B,
   const int lane = LANE;
   const int64_t lo = SM.keep[s] ? SM.lo[s] : 0;
   const int64_t hi = SM.keep[s] ? SM.hi[s] : 0;
+  RateState RS{P.rate_origin_ts, P.rate_origin_val, -1, 0.0, -1, -1, 0.0, 0, 0};
   if (lo >= hi) {
-    if (RATE) {  // contributes nowhere
-      for (int64_t b = lane; b < P.nb; b += 64) S.rows[b] = ST_ABSENT;
+    if (RATE) {  // absent, or its rates past the window held (rate_finish)
+      rate_finish(P, SM, s, S, RS, -1);
       if (lane == 0) P.redo[s] = 0;
     }
     return;
   }
   const int sf = B.series_float ? (int)B.series_float[s] : 1;
-  RateState RS{P.rate_origin_ts, P.rate_origin_val, -1, 0.0, -1, -1, 0.0, 0, 0};
   int64_t flushed = 0;
   if (WIN) {
     for (int i = lane; i < WIN; i += 64) ring[i] = absent_value();
@@ -1094,13 +1196,13 @@ DEV void transform_rate(const Params& P, const SeriesMeta& SM, int64_t s,
     }
   }
   if (__ballot(bad_ts) && lane == 0) atomicOr(err_word, ERR_RATE_TS);
-  // a rate point past the window keeps the series contributing to the end
-  bool of_kept = false;
-  if (!fill && SM.of_has[s]) {
-    const double diff = SM.of_val[s] - carry_pv;
-    of_kept = !(P.counter && diff < 0 && P.drop_resets);
-  }
-  const int total = kept_count + (of_kept ? 1 : 0);
+  // kept rates past the window keep the series contributing to the end (and
+  // when every kept rate lies past it, the first one is held everywhere)
+  PastRates q{false, false, 0, 0.0};
+  if (!fill) q = past_rates(P, SM, s, carry_pts, carry_pv);
+  const bool of_kept = q.any;
+  const int total = kept_count + q.n;
+  if (kept_count == 0) r0_val = q.first;
 
   int64_t carry_k = -1;
   double carry_kv = 0.0;

@@ -544,3 +544,43 @@ def test_fold_order_cancellation(engine, agg):
             assert np.array_equal(np.asarray(a.ts), np.asarray(b.ts))
             assert np.array_equal(np.asarray(a.bits), np.asarray(b.bits)), (
                 "%s: run-to-run difference" % agg)
+
+
+def _outage_batch(reset_after=False):
+    """Two counter series of one group: A reports every 10 s; B's outage
+    covers the whole query window, with points before it and after its end
+    (inside the scan range).  reset_after: B's counter resets right after
+    the window (dropResets then drops the first rate past it)."""
+    from opentsdb_amd.batch import HostBatch, groups_from_ids
+    t = datasets.T0 + 10000 * np.arange(6 * 360, dtype=np.int64)  # 6 h
+    a = 1000 + 37 * np.arange(len(t), dtype=np.int64)
+    keep = (t < datasets.T0 + 3600000) | (t >= datasets.T0 + 4 * 3600000)
+    tb = t[keep]
+    vb = 5_000_000 + 11 * np.arange(len(tb), dtype=np.int64)
+    if reset_after:
+        after = tb >= datasets.T0 + 4 * 3600000
+        vb[after] = 3 * np.arange(after.sum(), dtype=np.int64)
+    ts = np.concatenate([t, tb])
+    val = np.concatenate([a, vb])
+    offs = np.array([0, len(t), len(t) + len(tb)], np.int64)
+    g_off, members = groups_from_ids(np.zeros(2, np.int64), 1)
+    return HostBatch(offs, ts, val, np.zeros(len(ts), np.uint8), None, g_off,
+                     members)
+
+
+@pytest.mark.parametrize("drop", [False, True])
+@pytest.mark.parametrize("agg", ["min", "sum", "max"])
+def test_rate_series_whose_rates_all_lie_past_the_window(engine, agg, drop):
+    """Rate mode pre-consumes each span's first (junk) rate and keeps the
+    span contributing while it has a second (AggregationIterator.java:
+    448-459): a series whose outage covers the whole window still
+    contributes its junk rate, held over the window, when its rates lie
+    past the window's end (found by the random sweep, seed 48)."""
+    b = _outage_batch(reset_after=drop)
+    t0, t1 = datasets.T0 + 3600000 + 120000, datasets.T0 + 3 * 3600000
+    ro = core.RateOptions(True, core.LONG_MAX, 0, drop)
+    spec = core.make_spec(t0, t1, core.Aggregators.get(agg),
+                          core.DownsamplingSpecification("1m-sum"), t0, t1,
+                          True, ro)
+    check(engine, spec, b, exact=agg in ("min", "max"),
+          where="outage/%s/drop=%s" % (agg, drop))

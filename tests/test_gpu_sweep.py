@@ -1,0 +1,74 @@
+"""Seeded random-query sweep against the oracle: aggregator x downsampler x
+fill x interpolation override x rate x window x batch shape, drawn from the
+reference's surface (Aggregators, DownsamplingSpecification, FillPolicy,
+RateOptions).  Exercises the paths' interplay the parity matrix crosses only
+partly: multi-window and narrowed folds, 32-member tiles, the row path for
+rate and percentiles, fills, windows cut inside buckets."""
+import numpy as np
+import pytest
+
+from opentsdb_amd import core
+from tests import datasets
+from tests.test_gpu_parity import check, cancel_floor
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from opentsdb_amd.engine import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+AGGS = ["sum", "zimsum", "pfsum", "avg", "min", "max", "mimmin", "mimmax",
+        "dev", "count", "first", "last", "diff", "mult", "squareSum",
+        "median", "p50", "p95", "p99", "ep90r3", "ep99r7"]
+DSF = ["avg", "sum", "min", "max", "count", "first", "last", "dev",
+       "zimsum", "mimmax", "median", "p90"]
+FILLS = ["none", "none", "nan", "null", "zero"]
+INTERVALS = ["30s", "1m", "2m", "5m", "7m", "13m", "1h"]
+EXACT_DS = ("min", "max", "count", "first", "last", "mimmax", "median", "p90")
+EXACT_AGG = ("min", "max", "mimmin", "mimmax", "count", "first", "last",
+             "median", "p50", "p95", "p99", "ep90r3", "ep99r7")
+
+
+def _case(seed):
+    rng = np.random.default_rng(1000 + seed)
+    kind = ["float", "int", "mixed"][int(rng.integers(0, 3))]
+    rate = bool(rng.random() < 0.2)
+    n_series = int(rng.integers(1, 90))
+    b = datasets.random_batch(
+        5000 + seed, n_series=n_series,
+        n_groups=int(rng.integers(1, max(1, n_series // 3) + 1)),
+        span_ms=int(rng.integers(1, 7)) * 3600 * 1000,
+        cadence_ms=int(rng.choice([1000, 7000, 10000, 60000])),
+        value_kind="int" if rate else kind,
+        nan_frac=0.03 if kind == "float" and not rate else 0.0,
+        counter=rate, big_group=bool(rng.random() < 0.15))
+    agg = AGGS[int(rng.integers(0, len(AGGS)))]
+    ds = DSF[int(rng.integers(0, len(DSF)))]
+    fill = "none" if rate else FILLS[int(rng.integers(0, len(FILLS)))]
+    iv = INTERVALS[int(rng.integers(0, len(INTERVALS)))]
+    t0 = datasets.T0 + int(rng.integers(0, 3600)) * 1000
+    t1 = t0 + int(rng.integers(1800, 6 * 3600)) * 1000
+    interp = None
+    if rng.random() < 0.25:
+        interp = int(rng.integers(0, 5))  # LERP ZIM MAX MIN PREV
+    ro = core.RateOptions(True, core.LONG_MAX, 0) if rate else None
+    spec = core.make_spec(t0, t1, core.Aggregators.get(agg),
+                          core.DownsamplingSpecification("%s-%s-%s" % (iv, ds, fill)),
+                          t0, t1, rate, ro, interp)
+    exact = (ds in EXACT_DS and agg in EXACT_AGG and not rate
+             and kind != "mixed")
+    return b, spec, exact, "%d:%s:%s-%s-%s%s%s" % (
+        seed, agg, iv, ds, fill, ":rate" if rate else "",
+        "" if interp is None else ":i%d" % interp)
+
+
+@pytest.mark.parametrize("seed", range(120))
+def test_random_query_sweep(engine, seed):
+    b, spec, exact, where = _case(seed)
+    # sums of mixed-sign data cancel: the data's own 1e-12 floor
+    fl = cancel_floor(b, 2000)
+    check(engine, spec, b, exact, where=where, floor=fl)
