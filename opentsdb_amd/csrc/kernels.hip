@@ -187,9 +187,8 @@ __global__ void k_prep(Params P, BatchDev B, SeriesMeta SM, int* err_word) {
       int err = 0;
       of_val = st.finish(&err);
       of_has = 1;
-      // (percentile downsampling: k_ds_select fills of_val later and the
-      // bucket values here are counts — its rate rows use the bucket past
-      // the window alone)
+      // (percentile downsampling: the bucket values here are counts —
+      // k_ds_select fills of_val, of_rate and the rate bits later)
       if (P.rate && !P.ds_sel) {
         // the next bucket points: fixed-interval buckets (the row path takes
         // rate queries; calendar grids step their table)

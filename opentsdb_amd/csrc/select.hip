@@ -798,6 +798,61 @@ __global__ __launch_bounds__(64) void k_ds_select(Params P, BatchDev B,
     const int f = B.is_float ? (int)B.is_float[i] : sf;
     return f ? __longlong_as_double(b) : (double)b;
   };
+  // the percentile of the points [a, e) of each active lane's bucket (NaN
+  // when every value is NaN): buckets of up to DS_SMALL values by a per-lane
+  // insertion sort, larger ones by the whole wave, one bucket at a time
+  auto select_buckets = [&](bool act, int64_t a, int64_t e) -> double {
+    const int64_t cnt = act ? e - a : 0;
+    double res = qnan();
+    if (cnt > 0 && cnt <= DS_SMALL) {
+      int n = 0;
+      for (int64_t i = a; i < e; ++i) {
+        const double v = value(i);
+        if (is_nan(v)) continue;
+        const uint64_t k = dkey(v);
+        int q = n++;
+        while (q > 0 && sk[q - 1][lane] > k) {
+          sk[q][lane] = sk[q - 1][lane];
+          --q;
+        }
+        sk[q][lane] = k;
+      }
+      int64_t r0, r1;
+      double pos;
+      sel_ranks(median, p, n, &r0, &r1, &pos);
+      if (n)
+        res = sel_value(median, n, pos, key_value(sk[r0][lane]),
+                        key_value(sk[r1][lane]));
+    }
+    uint64_t big = __ballot(cnt > DS_SMALL);
+    while (big) {
+      const int l = __builtin_ctzll(big);
+      big &= big - 1;
+      const int64_t la = __shfl(a, l), le = __shfl(e, l);
+      // non-NaN count
+      int64_t nn = 0;
+      for (int64_t i = la + lane; i < le; i += 64) nn += !is_nan(value(i));
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) nn += __shfl_xor(nn, d);
+      // NaNs (either sign) take the largest key: ranks below nn never
+      // reach them
+      auto key_at = [&](int64_t i) {
+        const double v = value(la + i);
+        return is_nan(v) ? ~0ULL : dkey(v);
+      };
+      int64_t r0, r1;
+      double pos;
+      sel_ranks(median, p, nn, &r0, &r1, &pos);
+      double v = qnan();
+      if (nn > 0) {
+        const uint64_t k0 = wave_select(le - la, r0, hist, key_at);
+        const uint64_t k1 = (r1 == r0) ? k0 : wave_select(le - la, r1, hist, key_at);
+        v = sel_value(median, nn, pos, key_value(k0), key_value(k1));
+      }
+      if (lane == l) res = v;
+    }
+    return res;
+  };
   // buckets that can hold points: [b_first, b_last] (+ nb for of_val)
   int64_t b_first = 0, b_last = -1;
   if (lo < hi) {
@@ -806,6 +861,8 @@ __global__ __launch_bounds__(64) void k_ds_select(Params P, BatchDev B,
   }
   const bool of = SM.of_has[s] != 0;
   const int64_t n_b = (b_last - b_first + 1) + (of ? 1 : 0);
+  double of_v = 0.0;
+  int64_t of_e = hi;
   for (int64_t c0 = 0; c0 < n_b; c0 += 64) {
     const int64_t j = c0 + lane;
     const bool act = j < n_b;
@@ -827,28 +884,8 @@ __global__ __launch_bounds__(64) void k_ds_select(Params P, BatchDev B,
         e = lower_bound(B.ts, a, hi, bucket_ts(P, b + 1));
       }
     }
-    const int64_t cnt = e - a;
-    // small buckets: per-lane insertion sort of the non-NaN keys
-    int n = 0;
-    const bool small = cnt <= DS_SMALL;
-    if (act && cnt > 0 && small) {
-      for (int64_t i = a; i < e; ++i) {
-        const double v = value(i);
-        if (is_nan(v)) continue;
-        const uint64_t k = dkey(v);
-        int q = n++;
-        while (q > 0 && sk[q - 1][lane] > k) {
-          sk[q][lane] = sk[q - 1][lane];
-          --q;
-        }
-        sk[q][lane] = k;
-      }
-      int64_t r0, r1;
-      double pos;
-      sel_ranks(median, p, n, &r0, &r1, &pos);
-      const double v = n ? sel_value(median, n, pos, key_value(sk[r0][lane]),
-                                     key_value(sk[r1][lane]))
-                         : qnan();
+    const double v = select_buckets(act, a, e);
+    if (act && e > a) {
       if (is_of) {
         SM.of_val[s] = v;
       } else {
@@ -856,43 +893,59 @@ __global__ __launch_bounds__(64) void k_ds_select(Params P, BatchDev B,
         rows[b] = ST_REAL;
       }
     }
-    // large buckets: the whole wave selects, one bucket at a time
-    uint64_t big = __ballot(act && cnt > DS_SMALL);
-    while (big) {
-      const int l = __builtin_ctzll(big);
-      big &= big - 1;
-      const int64_t la = __shfl(a, l), le = __shfl(e, l);
-      const int64_t lb = __shfl(b, l);
-      const bool lof = __shfl((int)is_of, l) != 0;
-      // non-NaN count
-      int64_t nn = 0;
-      for (int64_t i = la + lane; i < le; i += 64) nn += !is_nan(value(i));
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) nn += __shfl_xor(nn, d);
-      // NaNs (either sign) take the largest key: ranks below nn never
-      // reach them
-      auto key_at = [&](int64_t i) {
-        const double v = value(la + i);
-        return is_nan(v) ? ~0ULL : dkey(v);
-      };
-      int64_t r0, r1;
-      double pos;
-      sel_ranks(median, p, nn, &r0, &r1, &pos);
-      double v = qnan();
-      if (nn > 0) {
-        const uint64_t k0 = wave_select(le - la, r0, hist, key_at);
-        const uint64_t k1 = (r1 == r0) ? k0 : wave_select(le - la, r1, hist, key_at);
-        v = sel_value(median, nn, pos, key_value(k0), key_value(k1));
-      }
-      if (lane == 0) {
-        if (lof) {
-          SM.of_val[s] = v;
-        } else {
-          rowv[lb] = v;
-          rows[lb] = ST_REAL;
-        }
-      }
+    const uint64_t om = __ballot(is_of);
+    if (om) {
+      const int l = __builtin_ctzll(om);
+      of_v = __shfl(v, l);
+      of_e = __shfl(e, l);
     }
+  }
+  if (!(P.rate && of)) return;
+  // rate queries: the kept rates past the bucket past the window (k_prep's
+  // rates_beyond, here over percentile buckets).  Lane j takes the j-th
+  // bucket from the one holding the next unread point; the rates then chain
+  // through the lanes in order until two are kept or the points run out.
+  int64_t t = SM.of_ts[s], pos = of_e;
+  double v = of_v, r1 = 0.0;
+  int nk = 0;
+  while (nk < 2 && pos < p1) {
+    const int64_t t_pos = B.ts[pos];
+    int64_t bt = 0, be = 0;
+    bool act = true;
+    if (P.cal) {
+      const int64_t k = cal_bucket(P, t_pos) + lane;
+      act = k >= P.cal_lo && k + 1 < P.cal_n;
+      if (act) {
+        bt = P.cal[k];
+        be = P.cal[k + 1];
+      }
+    } else {
+      bt = align_ts(t_pos, P.interval) + lane * P.interval;
+      be = bt + P.interval;
+    }
+    int64_t a = pos, e = pos;
+    if (act) {
+      a = lower_bound(B.ts, pos, p1, bt);
+      e = lower_bound(B.ts, a, p1, be);
+    }
+    const double bv = select_buckets(act, a, e);
+    const uint64_t hm = __ballot(act && e > a);
+    if (!hm) break;  // the calendar table ends here
+    for (uint64_t m = hm; m && nk < 2; m &= m - 1) {
+      const int l = __builtin_ctzll(m);
+      const int64_t tn = __shfl(bt, l);
+      const double vn = __shfl(bv, l);
+      bool kept;
+      const double r = rate_between(P, t, v, tn, vn, &kept);
+      if (kept && nk++ == 0) r1 = r;
+      t = tn;
+      v = vn;
+    }
+    pos = __shfl(e, 63 - __builtin_clzll(hm));
+  }
+  if (lane == 0) {
+    SM.of_has[s] = (uint8_t)(1 | (nk << 1));
+    SM.of_rate[s] = r1;
   }
 }
 

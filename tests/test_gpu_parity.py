@@ -568,9 +568,12 @@ def _outage_batch(reset_after=False):
                      members)
 
 
+@pytest.mark.parametrize("ds", ["1m-sum", "1m-p90", "1m-median", "2m-avg",
+                                "30s-p50"])
 @pytest.mark.parametrize("drop", [False, True])
 @pytest.mark.parametrize("agg", ["min", "sum", "max"])
-def test_rate_series_whose_rates_all_lie_past_the_window(engine, agg, drop):
+def test_rate_series_whose_rates_all_lie_past_the_window(engine, agg, drop,
+                                                         ds):
     """Rate mode pre-consumes each span's first (junk) rate and keeps the
     span contributing while it has a second (AggregationIterator.java:
     448-459): a series whose outage covers the whole window still
@@ -580,7 +583,6 @@ def test_rate_series_whose_rates_all_lie_past_the_window(engine, agg, drop):
     t0, t1 = datasets.T0 + 3600000 + 120000, datasets.T0 + 3 * 3600000
     ro = core.RateOptions(True, core.LONG_MAX, 0, drop)
     spec = core.make_spec(t0, t1, core.Aggregators.get(agg),
-                          core.DownsamplingSpecification("1m-sum"), t0, t1,
-                          True, ro)
+                          core.DownsamplingSpecification(ds), t0, t1, True, ro)
     check(engine, spec, b, exact=agg in ("min", "max"),
-          where="outage/%s/drop=%s" % (agg, drop))
+          where="outage/%s/%s/drop=%s" % (agg, ds, drop))

@@ -72,3 +72,38 @@ def test_random_query_sweep(engine, seed):
     # sums of mixed-sign data cancel: the data's own 1e-12 floor
     fl = cancel_floor(b, 2000)
     check(engine, spec, b, exact, where=where, floor=fl)
+
+
+def _rate_case(seed):
+    """Rate queries only: counter options (dropResets, counterMax,
+    resetValue — RateOptions.java:27-176) x downsampler (percentiles take the
+    k_ds_select path) x window; the generator's outages and counter resets
+    put kept rates past windows and resets next to bucket edges."""
+    rng = np.random.default_rng(7000 + seed)
+    n_series = int(rng.integers(1, 60))
+    b = datasets.random_batch(
+        9000 + seed, n_series=n_series,
+        n_groups=int(rng.integers(1, max(1, n_series // 3) + 1)),
+        span_ms=int(rng.integers(1, 7)) * 3600 * 1000,
+        cadence_ms=int(rng.choice([1000, 10000, 60000])),
+        value_kind="int", counter=True, big_group=bool(rng.random() < 0.15))
+    agg = AGGS[int(rng.integers(0, len(AGGS)))]
+    ds = DSF[int(rng.integers(0, len(DSF)))]
+    iv = INTERVALS[int(rng.integers(0, len(INTERVALS)))]
+    t0 = datasets.T0 + int(rng.integers(0, 3 * 3600)) * 1000
+    t1 = t0 + int(rng.integers(600, 4 * 3600)) * 1000
+    drop = bool(rng.random() < 0.5)
+    cmax = core.LONG_MAX if rng.random() < 0.7 else int(2**40)
+    reset = 0 if rng.random() < 0.6 else int(rng.integers(1, 10**6))
+    ro = core.RateOptions(True, cmax, reset, drop)
+    spec = core.make_spec(t0, t1, core.Aggregators.get(agg),
+                          core.DownsamplingSpecification("%s-%s" % (iv, ds)),
+                          t0, t1, True, ro)
+    return b, spec, "%d:%s:%s-%s:drop=%s:max=%d:reset=%d" % (
+        seed, agg, iv, ds, drop, cmax, reset)
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_random_rate_sweep(engine, seed):
+    b, spec, where = _rate_case(seed)
+    check(engine, spec, b, False, where=where, floor=cancel_floor(b, 2000))
