@@ -339,7 +339,9 @@ DEV void fold_member(const Params& P, const BatchDev& B, FoldSink<A>& F,
   int64_t lo_eff = pa;
   int32_t prev_hi = -1;  // bucket of the previous step's last point
   int dbg_n = 0;
-  for (int64_t base = pa & ~(int64_t)1; base < pb;) {
+  // (no points in the window: no step — an aligned base below an odd pa
+  // would stream the point before the window and read bucket bounds past it)
+  for (int64_t base = pa & ~(int64_t)1; pa < pb && base < pb;) {
     FOLD_GUARD(dbg_n, 1 << 30, F.err, "stream loop mi=%d base=%ld pa=%ld pb=%ld\n", F.mi, (long)base, (long)pa, (long)pb)
     const int64_t i0 = base + (int64_t)K * lane;
     int64_t t[K], v[K];

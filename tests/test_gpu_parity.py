@@ -586,3 +586,53 @@ def test_rate_series_whose_rates_all_lie_past_the_window(engine, agg, drop,
                           core.DownsamplingSpecification(ds), t0, t1, True, ro)
     check(engine, spec, b, exact=agg in ("min", "max"),
           where="outage/%s/%s/drop=%s" % (agg, ds, drop))
+
+
+def _empty_member_batch(after):
+    """A reports every 10 s over 6 h; B is kept (its points straddle the
+    window, or end inside the scan range when after=False) but has none
+    inside the window, and its first index past the window is odd (the fold
+    steps from an even base).  B is the batch's last series."""
+    from opentsdb_amd.batch import HostBatch, groups_from_ids
+    t = datasets.T0 + 10000 * np.arange(6 * 360, dtype=np.int64)
+    a = (t // 1000) % 97
+    # B's last point lies in [start, first bucket): kept, nothing in the grid
+    tb = (datasets.T0 + 3600000 + 127000
+          - 10000 * np.arange(100, -1, -1, dtype=np.int64))
+    if after:
+        tb = np.concatenate([tb, datasets.T0 + 4 * 3600000
+                             + 10000 * np.arange(40, dtype=np.int64)])
+    assert (len(t) + 101) % 2 == 1
+    vb = np.arange(len(tb), dtype=np.int64) % 13
+    ts = np.concatenate([t, tb])
+    val = np.concatenate([a, vb]).astype(np.int64)
+    offs = np.array([0, len(t), len(t) + len(tb)], np.int64)
+    g_off, members = groups_from_ids(np.zeros(2, np.int64), 1)
+    return HostBatch(offs, ts, val, np.zeros(len(ts), np.uint8), None, g_off,
+                     members)
+
+
+@pytest.mark.parametrize("after", [False, True])
+@pytest.mark.parametrize("fill", ["zero", "null", "nan", "none"])
+@pytest.mark.parametrize("ds", ["1m-sum", "30s-min", "2m-count"])
+def test_fold_member_without_window_points(engine, ds, fill, after):
+    """A kept member with no point inside the window (SpanGroup.add keeps
+    it; FillingDownsampler still fills its every bucket) must stream
+    nothing: found by the random sweep (seeds 850, 865, 1103), where such a
+    member at an odd point index pushed fills past the window's LDS states.
+    The 30s grid (236 buckets) runs as two narrowed fold windows."""
+    b = _empty_member_batch(after)
+    t0 = datasets.T0 + 3600000 + 125000
+    t1 = datasets.T0 + 3 * 3600000
+    spec = _spec("sum", ds.split("-")[1], fill, t0, t1,
+                 interval=ds.split("-")[0])
+    check(engine, spec, b, exact=False,
+          where="empty-member/%s/%s/after=%s" % (ds, fill, after))
+    # B alone: its group is fill values only (or absent)
+    from opentsdb_amd.batch import HostBatch
+    o = int(b.offsets[1])
+    bb = HostBatch(np.array([0, len(b.ts) - o], np.int64), b.ts[o:], b.val[o:],
+                   b.is_float[o:], None, np.array([0, 1], np.int64),
+                   np.array([0], np.int64))
+    check(engine, spec, bb, exact=True,
+          where="empty-member-alone/%s/%s/after=%s" % (ds, fill, after))
