@@ -110,6 +110,20 @@ def stage_reader(eng):
     return read
 
 
+def workload_label(config, n_series):
+    """The query as /api/query spells it (rate options included)."""
+    from opentsdb_amd import workload
+    cfg = workload.CONFIGS[config]
+    rate = ""
+    if cfg["rate"]:
+        counter, cmax, reset = cfg["rate"]
+        rate = "rate{%s,%d,%d}:" % ("counter" if counter else "", cmax, reset)
+    grp = (cfg["group"] + "=*") if cfg["group"] else ""
+    return "%s: %s:%s:%ssys.cpu.user{%s} over %d series x %d days @10s per " \
+           "GPU" % (config, cfg["agg"], cfg["ds"], rate, grp, n_series,
+                    cfg["days"])
+
+
 def named_spec(config):
     """BASELINE's metric shape, sum:1m-avg{host=*} (LERP), over config's
     window."""
@@ -469,12 +483,24 @@ def main():
     value = total_points / step_s
 
     # dominant kernel: the downsample stage streams every point once
-    # (16 B/point) — k_fold, or k_bucketize_k on the rate path
-    kb_s = stage_ms[0] / 1e3
+    # (16 B/point) — k_fold on the fold path.  Rate and selection queries
+    # run the row path: its roofline is priced over the whole on-device
+    # pipeline (every stage: prep, downsample, transform, group / selection,
+    # compact), with the downsample stage alone beside it
+    row_path = bool(cfg["rate"]) or cfg["agg"] in ("p99", "p999", "median")
+    kb_s = (sum(stage_ms[:5]) if row_path else stage_ms[0]) / 1e3
     achieved = BYTES_PER_POINT * n_points / kb_s / 1e9 if kb_s > 0 else None
-    kernel = "k_bucketize_k (rate-fused)" if cfg["rate"] else (
-        "k_bucketize_k + k_keys_transpose/k_seg_select"
-        if cfg["agg"] in ("p99", "p999", "median") else "k_fold")
+    kernel = ("k_fold" if not row_path else
+              "pipeline: k_prep + k_bucketize_k (rate-fused) + k_transform + "
+              "k_group<MDev> + k_compact"
+              if cfg["rate"] else
+              "pipeline: k_prep + k_bucketize_k + k_keys_transpose + "
+              "k_seg_select + k_compact")
+    ds_stage = None
+    if row_path and stage_ms[0] > 0:
+        ds_stage = {"kernel": "k_bucketize_k", "ms": stage_ms[0],
+                    "frac": BYTES_PER_POINT * n_points / (stage_ms[0] / 1e3)
+                    / 1e9 / HBM_PEAK_GBS}
     # PMC traffic of this exact workload (scripts/gpu_pmc.sh, default size,
     # one GPU, the shipped kernels), per launch of the dominant kernel
     traffic = None
@@ -517,11 +543,7 @@ def main():
                     "HBM; %d series x %d d @10s per GPU)" % (
                         n_series, cfg["days"]),
             "config": {
-                "workload": "%s: %s:%s:sys.cpu.user{%s} over %d series x %d "
-                            "days @10s per GPU" % (
-                                args.config, cfg["agg"], cfg["ds"],
-                                (cfg["group"] or "") + "=*" if cfg["group"]
-                                else "", n_series, cfg["days"]),
+                "workload": workload_label(args.config, n_series),
                 "points_per_gpu": n_points,
                 "groups_per_gpu": n_groups,
                 "buckets": n_buckets,
@@ -548,6 +570,8 @@ def main():
             },
             "cpu_baseline": extra.get("cpu_baseline"),
         }
+        if ds_stage:
+            line["roofline"]["downsample_stage"] = ds_stage
         for k in ("named_query", "p999", "pcie_inclusive", "decode"):
             if k in extra:
                 line[k] = extra[k]

@@ -59,13 +59,55 @@ public final class GpuAggregation {
     VALUES = v;
   }
 
-  /** One engine context per thread (a context serialises its queries). */
-  private static final ThreadLocal<Long> CTX = new ThreadLocal<Long>() {
-    @Override
-    protected Long initialValue() {
-      return nativeCtxCreate(Integer.getInteger("tsd.gpu.device", 0));
+  /**
+   * One engine context per thread (a context serialises its queries).  A
+   * failed creation (library present, no usable GPU) is remembered: every
+   * later query falls back to the Java iterators without retrying.
+   */
+  private static final ThreadLocal<Long> CTX = new ThreadLocal<Long>();
+  private static volatile boolean CTX_FAILED = false;
+  /** Contexts of every thread, destroyed at JVM exit. */
+  private static final List<Long> ALL_CTX = new ArrayList<Long>();
+  static {
+    Runtime.getRuntime().addShutdownHook(new Thread() {
+      @Override
+      public void run() {
+        synchronized (ALL_CTX) {
+          for (final Long c : ALL_CTX) {
+            nativeCtxDestroy(c);
+          }
+          ALL_CTX.clear();
+        }
+      }
+    });
+  }
+
+  /** This thread's context, or 0 when no GPU context can be had. */
+  private static long context() {
+    if (CTX_FAILED) {
+      return 0;
     }
-  };
+    final Long c = CTX.get();
+    if (c != null) {
+      return c;
+    }
+    final long created;
+    try {
+      created = nativeCtxCreate(Integer.getInteger("tsd.gpu.device", 0));
+    } catch (RuntimeException e) {
+      CTX_FAILED = true;
+      return 0;
+    }
+    if (created == 0) {
+      CTX_FAILED = true;
+      return 0;
+    }
+    CTX.set(created);
+    synchronized (ALL_CTX) {
+      ALL_CTX.add(created);
+    }
+    return created;
+  }
 
   private GpuAggregation() {}
 
@@ -100,8 +142,12 @@ public final class GpuAggregation {
       final long scan_start_s, final long scan_end_s,
       final Aggregator aggregator, final DownsamplingSpecification ds,
       final boolean rate, final RateOptions rate_options,
-      final long query_start, final long query_end) {
-    if (!LOADED || QUALIFIERS == null || groups.length == 0) {
+      final long query_start, final long query_end,
+      final boolean split_rollup_raw_leg) {
+    // the raw leg of a SplitRollupQuery must hand back SpanGroups
+    // (SplitRollupQuery.RunCB.makeSpanGroupMap, SplitRollupQuery.java:436-441)
+    if (!LOADED || QUALIFIERS == null || groups.length == 0
+        || split_rollup_raw_leg) {
       return null;
     }
     final long[] spec = new long[SPEC_LEN];
@@ -125,7 +171,11 @@ public final class GpuAggregation {
       spec[SPEC_DS_AGG] = ds_agg;
       spec[SPEC_FILL] = ds.getFillPolicy().ordinal();
       spec[SPEC_DS_INTERVAL] = ds.getInterval();
-      spec[SPEC_RUN_ALL] = ds.getStringInterval().contains("all") ? 1 : 0;
+      // Downsampler.java:131-133: the deprecated (interval, function, fill)
+      // constructor leaves the string interval null (not run-all)
+      final String si = ds.getStringInterval();
+      spec[SPEC_RUN_ALL] =
+          si != null && si.toLowerCase().contains("all") ? 1 : 0;
       if (ds.useCalendar() && spec[SPEC_RUN_ALL] == 0) {
         cal = calendarEdges(ds, spec[SPEC_START_MS], spec[SPEC_END_MS]);
         if (cal == null) {
@@ -204,7 +254,10 @@ public final class GpuAggregation {
     } else {
       cap = Math.max(cap, (long) vbytes + groups.length);
     }
-    final long ctx = CTX.get();
+    final long ctx = context();
+    if (ctx == 0) {
+      return null;  // no usable GPU: the Java iterators keep the query
+    }
     while (true) {
       if (cap > Integer.MAX_VALUE - 8) {
         return null;

@@ -4,13 +4,13 @@
  *
  * Built only where a JDK is installed (jni.h; see the Makefile next to this
  * file) — this repository's image has none.  The shim holds no state: every
- * native call maps Java arrays (GetPrimitiveArrayCritical: no copies, the
- * call is synchronous and makes no JNI calls while they are held) onto the
- * C-ABI structs, calls the engine and maps the status onto the exception
+ * native call copies the Java arrays into native buffers (nothing stays
+ * pinned while the GPU works) and maps them onto the C-ABI structs, calls the engine and maps the status onto the exception
  * the reference path throws (otsdb_status, include/otsdb_agg.h:39-61).
  */
 #include <jni.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "otsdb_agg.h"
@@ -71,23 +71,33 @@ JNIEXPORT jint JNICALL Java_net_opentsdb_core_GpuAggregation_nativeAggId(
   return id;
 }
 
-typedef struct {
-  jarray arr;
-  void* p;
-} pinned;
-
-static void* pin(JNIEnv* env, jarray a, pinned* slot) {
-  slot->arr = a;
-  slot->p = a ? (*env)->GetPrimitiveArrayCritical(env, a, NULL) : NULL;
-  return slot->p;
+/* Inputs are copied out of the Java heap (Get<Type>ArrayRegion) and outputs
+ * copied back (Set<Type>ArrayRegion): no array stays pinned while the GPU
+ * works, so the query never holds the GC locker.  The copies are host
+ * memcpys, small next to the H2D transfer the engine does anyway. */
+static void* copy_in(JNIEnv* env, jarray a, size_t elem, int is_byte,
+                     int* failed) {
+  if (!a || *failed) return NULL;
+  const jsize n = (*env)->GetArrayLength(env, a);
+  void* p = malloc(n > 0 ? (size_t)n * elem : 1);
+  if (!p) {
+    *failed = 1;
+    return NULL;
+  }
+  if (is_byte)
+    (*env)->GetByteArrayRegion(env, (jbyteArray)a, 0, n, (jbyte*)p);
+  else
+    (*env)->GetLongArrayRegion(env, (jlongArray)a, 0, n, (jlong*)p);
+  if ((*env)->ExceptionCheck(env)) *failed = 1;
+  return p;
 }
 
-static void unpin(JNIEnv* env, pinned* slot, int n, int commit_from) {
-  /* inputs: JNI_ABORT (nothing to copy back); outputs: 0 */
-  for (int i = n - 1; i >= 0; --i)
-    if (slot[i].p)
-      (*env)->ReleasePrimitiveArrayCritical(env, slot[i].arr, slot[i].p,
-                                            i >= commit_from ? 0 : JNI_ABORT);
+static void* alloc_out(JNIEnv* env, jarray a, size_t elem, int* failed) {
+  if (!a || *failed) return NULL;
+  const jsize n = (*env)->GetArrayLength(env, a);
+  void* p = calloc(n > 0 ? (size_t)n : 1, elem);
+  if (!p) *failed = 1;
+  return p;
 }
 
 JNIEXPORT jint JNICALL Java_net_opentsdb_core_GpuAggregation_nativeRunCells(
@@ -97,7 +107,8 @@ JNIEXPORT jint JNICALL Java_net_opentsdb_core_GpuAggregation_nativeRunCells(
     jbyteArray jval, jlongArray jgoff, jlongArray jgmem, jlongArray jooff,
     jlongArray jots, jlongArray joval, jbyteArray joisint) {
   (void)cls;
-  if ((*env)->GetArrayLength(env, jspec) < SPEC_LEN) {
+  if (!jspec || (*env)->GetArrayLength(env, jspec) < SPEC_LEN || !jgoff ||
+      !jooff || !jots || !joval || !joisint) {
     throw_status(env, OTSDB_E_ILLEGAL_ARGUMENT);
     return OTSDB_E_ILLEGAL_ARGUMENT;
   }
@@ -121,40 +132,79 @@ JNIEXPORT jint JNICALL Java_net_opentsdb_core_GpuAggregation_nativeRunCells(
   s.drop_resets = (int32_t)spec_v[SPEC_DROP_RESETS];
   s.counter_max = spec_v[SPEC_COUNTER_MAX];
   s.reset_value = spec_v[SPEC_RESET_VALUE];
-  const jsize n_rows = (*env)->GetArrayLength(env, jrow_series);
+  const jsize n_rows = jrow_series ? (*env)->GetArrayLength(env, jrow_series) : 0;
   const jsize n_groups = (*env)->GetArrayLength(env, jgoff) - 1;
+  const jsize n_out_off = (*env)->GetArrayLength(env, jooff);
   const jsize cap = (*env)->GetArrayLength(env, jots);
-  const jsize n_cal = jcal ? (*env)->GetArrayLength(env, jcal) : 0;
+  if (n_groups < 0 || n_out_off < n_groups + 1 ||
+      (*env)->GetArrayLength(env, joval) < cap ||
+      (*env)->GetArrayLength(env, joisint) < cap) {
+    throw_status(env, OTSDB_E_ILLEGAL_ARGUMENT);
+    return OTSDB_E_ILLEGAL_ARGUMENT;
+  }
 
-  /* inputs first (released with JNI_ABORT), outputs from index 9 on */
-  pinned pn[13];
-  memset(pn, 0, sizeof(pn));
-  s.cal_edges = (const int64_t*)pin(env, jcal, &pn[0]);
-  s.n_cal_edges = n_cal;
-  otsdb_cells c;
-  c.n_rows = n_rows;
-  c.row_series = (const int64_t*)pin(env, jrow_series, &pn[1]);
-  c.row_base_s = (const int64_t*)pin(env, jrow_base, &pn[2]);
-  c.qual_off = (const int64_t*)pin(env, jqual_off, &pn[3]);
-  c.qual = (const uint8_t*)pin(env, jqual, &pn[4]);
-  c.val_off = (const int64_t*)pin(env, jval_off, &pn[5]);
-  c.val = (const uint8_t*)pin(env, jval, &pn[6]);
-  otsdb_batch b;
-  memset(&b, 0, sizeof(b));
-  b.n_series = n_series;
-  b.n_groups = n_groups;
-  b.group_offsets = (const int64_t*)pin(env, jgoff, &pn[7]);
-  b.group_members = (const int64_t*)pin(env, jgmem, &pn[8]);
-  otsdb_result r;
-  r.capacity = cap;
-  r.offsets = (int64_t*)pin(env, jooff, &pn[9]);
-  r.ts = (int64_t*)pin(env, jots, &pn[10]);
-  r.val = (int64_t*)pin(env, joval, &pn[11]);
-  r.is_int = (uint8_t*)pin(env, joisint, &pn[12]);
+  int failed = 0;
+  void* in[9];
+  in[0] = copy_in(env, jcal, 8, 0, &failed);
+  in[1] = copy_in(env, jrow_series, 8, 0, &failed);
+  in[2] = copy_in(env, jrow_base, 8, 0, &failed);
+  in[3] = copy_in(env, jqual_off, 8, 0, &failed);
+  in[4] = copy_in(env, jqual, 1, 1, &failed);
+  in[5] = copy_in(env, jval_off, 8, 0, &failed);
+  in[6] = copy_in(env, jval, 1, 1, &failed);
+  in[7] = copy_in(env, jgoff, 8, 0, &failed);
+  in[8] = copy_in(env, jgmem, 8, 0, &failed);
+  void* out[4];
+  out[0] = alloc_out(env, jooff, 8, &failed);
+  out[1] = alloc_out(env, jots, 8, &failed);
+  out[2] = alloc_out(env, joval, 8, &failed);
+  out[3] = alloc_out(env, joisint, 1, &failed);
+
   otsdb_status st = OTSDB_E_DEVICE;
-  if (r.offsets && r.ts && r.val && r.is_int && b.group_offsets)
+  if (!failed) {
+    s.cal_edges = (const int64_t*)in[0];
+    s.n_cal_edges = jcal ? (*env)->GetArrayLength(env, jcal) : 0;
+    otsdb_cells c;
+    c.n_rows = n_rows;
+    c.row_series = (const int64_t*)in[1];
+    c.row_base_s = (const int64_t*)in[2];
+    c.qual_off = (const int64_t*)in[3];
+    c.qual = (const uint8_t*)in[4];
+    c.val_off = (const int64_t*)in[5];
+    c.val = (const uint8_t*)in[6];
+    otsdb_batch b;
+    memset(&b, 0, sizeof(b));
+    b.n_series = n_series;
+    b.n_groups = n_groups;
+    b.group_offsets = (const int64_t*)in[7];
+    b.group_members = (const int64_t*)in[8];
+    otsdb_result r;
+    r.capacity = cap;
+    r.offsets = (int64_t*)out[0];
+    r.ts = (int64_t*)out[1];
+    r.val = (int64_t*)out[2];
+    r.is_int = (uint8_t*)out[3];
     st = otsdb_agg_run_cells((otsdb_ctx*)(intptr_t)ctx, &s, &c, &b, &r);
-  unpin(env, pn, 13, 9);
+    if (st == OTSDB_OK || st == OTSDB_E_CAPACITY) {
+      /* offsets carry the needed size on CAPACITY too */
+      (*env)->SetLongArrayRegion(env, jooff, 0, n_groups + 1,
+                                 (const jlong*)out[0]);
+    }
+    if (st == OTSDB_OK) {
+      const jsize n = (jsize)((int64_t*)out[0])[n_groups];
+      (*env)->SetLongArrayRegion(env, jots, 0, n, (const jlong*)out[1]);
+      (*env)->SetLongArrayRegion(env, joval, 0, n, (const jlong*)out[2]);
+      (*env)->SetByteArrayRegion(env, joisint, 0, n, (const jbyte*)out[3]);
+    }
+  }
+  for (int i = 0; i < 9; ++i) free(in[i]);
+  for (int i = 0; i < 4; ++i) free(out[i]);
+  if ((*env)->ExceptionCheck(env)) return OTSDB_E_DEVICE; /* OOM pending */
+  if (failed) {
+    jclass oom = (*env)->FindClass(env, "java/lang/OutOfMemoryError");
+    if (oom) (*env)->ThrowNew(env, oom, "otsdb_agg_jni: native buffers");
+    return OTSDB_E_DEVICE;
+  }
   /* CAPACITY and UNSUPPORTED go back to Java (retry larger / keep the Java
    * iterators); the rest are the reference's exceptions */
   if (st != OTSDB_OK && st != OTSDB_E_CAPACITY && st != OTSDB_E_UNSUPPORTED)

@@ -2281,6 +2281,15 @@ otsdb_status otsdb_agg_run_cells(otsdb_ctx* c, const otsdb_query_spec* spec,
   for (int64_t m = 0; m < M; ++m)
     if (b->group_members[m] < 0 || b->group_members[m] >= S)
       return fail(OTSDB_E_ILLEGAL_ARGUMENT, "group member out of range");
+  // the pooled byte offsets set the H2D copy sizes: exclusive prefix sums
+  // from 0, never decreasing
+  if (R > 0 && (cells->qual_off[0] != 0 || cells->val_off[0] != 0))
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "qual_off / val_off must start at 0");
+  for (int64_t r = 0; r < R; ++r)
+    if (cells->qual_off[r + 1] < cells->qual_off[r] ||
+        cells->val_off[r + 1] < cells->val_off[r])
+      return fail(OTSDB_E_ILLEGAL_ARGUMENT,
+                  "qual_off / val_off must be nondecreasing");
   const int64_t QB = R ? cells->qual_off[R] : 0, VB = R ? cells->val_off[R] : 0;
   const int64_t cap = out->capacity;
   auto carve = [&](char* base) {

@@ -755,9 +755,16 @@ typedef struct {
   int64_t counter_max, reset_value;
   dp_t next_data, next_rate, prev_rate;
   int initialized;
+  int junk; /* the next rate populated is the junk first rate */
 } rate_view;
 
 #define INVALID_TS JLONG_MAX
+
+/* Test-only mutation hook: comparator tests scale the junk first rate
+ * (prev = the (0, 0) reset point) to prove the parity comparator catches a
+ * wrong junk rate.  1.0 = the reference's arithmetic. */
+static double g_junk_rate_scale = 1.0;
+void or_test_set_junk_rate_scale(double s) { g_junk_rate_scale = s; }
 
 static void rate_populate_next(rate_view* r) {
   for (;;) {
@@ -770,6 +777,8 @@ static void rate_populate_next(rate_view* r) {
     }
     prev_data = r->next_data;
     r->source->next(r->source, &r->next_data);
+    const double jscale = r->junk ? g_junk_rate_scale : 1.0;
+    r->junk = 0;
     const int64_t t0 = prev_data.ts, t1 = r->next_data.ts;
     if (t1 <= t0)
       jthrow(r->v.exc, OTSDB_E_ILLEGAL_STATE,
@@ -796,11 +805,11 @@ static void rate_populate_next(rate_view* r) {
           rate > (double)r->reset_value)
         r->next_rate.bits = d2bits(0.0);
       else
-        r->next_rate.bits = d2bits(rate);
+        r->next_rate.bits = d2bits(rate * jscale);
     } else {
       r->next_rate.ts = r->next_data.ts;
       r->next_rate.is_int = 0;
-      r->next_rate.bits = d2bits(difference / time_delta_secs);
+      r->next_rate.bits = d2bits(difference / time_delta_secs * jscale);
     }
     return;
   }
@@ -812,6 +821,7 @@ static void rate_init_if_not_done(rate_view* r) {
     r->next_data.ts = 0; /* next_data.reset(0, 0): a long point */
     r->next_data.is_int = 1;
     r->next_data.bits = 0;
+    r->junk = 1;
     rate_populate_next(r);
   }
 }

@@ -43,6 +43,9 @@ int or_group_by(const otsdb_query_spec* spec, const otsdb_batch* batch,
  * the way the reference's unit tests drive Downsampler / FillingDownsampler /
  * RateSpan directly.  chain: ds_interval_ms > 0 -> (Filling)Downsampler;
  * rate -> RateSpan on top.  If do_seek, seek(seek_ts) is called first.      */
+/* test-only: scales the junk first rate (comparator mutation tests) */
+void or_test_set_junk_rate_scale(double s);
+
 int or_view_stream(const otsdb_query_spec* spec, int do_seek, int64_t seek_ts,
                    int64_t n, const int64_t* ts, const int64_t* bits,
                    const uint8_t* is_float, or_point* out, int64_t cap,

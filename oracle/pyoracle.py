@@ -42,6 +42,8 @@ def lib():
         l.or_span_assemble.argtypes = [i64, vp, vp, vp, vp, vp,
                                        C.POINTER(i64), vp, vp, vp, vp, vp,
                                        cp, C.c_int]
+        l.or_test_set_junk_rate_scale.argtypes = [C.c_double]
+        l.or_test_set_junk_rate_scale.restype = None
         l.or_gen_count.argtypes = [vp, i64]
         l.or_gen_count.restype = i64
         l.or_gen_fill.argtypes = [vp, i64, vp, vp]
@@ -77,6 +79,21 @@ def group_by(spec, batch):
     if st != 0:
         raise OracleError(st, err.value.decode())
     return [out[offs[g]:offs[g + 1]].copy() for g in range(G)]
+
+
+class junk_rate_scaled:
+    """Context manager: the oracle's junk first rate (RateSpan.java:109-115)
+    scaled by `scale` — a mutation for comparator self-tests only."""
+
+    def __init__(self, scale):
+        self.scale = scale
+
+    def __enter__(self):
+        lib().or_test_set_junk_rate_scale(self.scale)
+        return self
+
+    def __exit__(self, *a):
+        lib().or_test_set_junk_rate_scale(1.0)
 
 
 def view_stream(spec, ts, bits, is_float, seek=None):

@@ -1,0 +1,101 @@
+"""Self-tests of the parity comparator (CPU only): the sweeps' comparator
+must reject results that differ from the reference's in exactly the rules
+the rate path implements.  A mutated oracle (its junk first rate scaled by
+1 + 1e-6, RateSpan.java:109-115, held by AggregationIterator.java:448-459
+until a span's first real rate) stands in for a wrong GPU result; the
+comparator run with the sweeps' own floor must flag it wherever the
+mutation reaches the output.  (The round-2 floor, 1e-12 x 2,000 x max|raw
+counter|, about 8.6 absolute, let 16 of these 18 mutated rate queries pass;
+the contribution floor catches all 18.)"""
+import numpy as np
+import pytest
+
+from oracle import pyoracle
+from tests.test_gpu_parity import compare, contribution_floor
+from tests.test_gpu_sweep import _case, _rate_case
+
+
+class _Res:
+    """An oracle group result in the engine's result shape."""
+
+    def __init__(self, pts):
+        self.ts, self.bits, self.is_int = pts["ts"], pts["bits"], pts["is_int"]
+
+
+def _mutated(spec, b, scale):
+    with pyoracle.junk_rate_scaled(scale):
+        return pyoracle.group_by(spec, b)
+
+
+def _visible(mut, ref):
+    """The mutation changes some output point by more than 1e-10 relative
+    (a 1e-6 change of one term among many can stay below the 1e-12 bar)."""
+    from tests.test_gpu_parity import _vals
+    for x, y in zip(mut, ref):
+        if len(x) != len(y):
+            return True
+        a, r = _vals(x["bits"], x["is_int"]), _vals(y["bits"], y["is_int"])
+        ok = np.isnan(a) == np.isnan(r)
+        if not ok.all():
+            return True
+        d = np.abs(a - r)[~np.isnan(r)]
+        if (d > 1e-10 * np.abs(r[~np.isnan(r)])).any():
+            return True
+    return False
+
+
+def test_comparator_catches_a_perturbed_junk_rate():
+    caught = reached = 0
+    for seed in range(60):
+        b, spec, exact, where = _rate_case(seed)
+        try:
+            ref = pyoracle.group_by(spec, b)
+        except pyoracle.OracleError:
+            continue
+        mut = _mutated(spec, b, 1.0 + 1e-6)
+        if not _visible(mut, ref):
+            continue  # the junk rate does not reach this query's output
+        reached += 1
+        fl = contribution_floor(spec, b, ref)
+        with pytest.raises(AssertionError):
+            compare([_Res(p) for p in mut], ref, exact, where, fl)
+        caught += 1
+    # the generator puts junk rates into most rate queries' output
+    assert reached >= 15, reached
+    assert caught == reached
+
+
+def test_contribution_floor_is_zero_for_same_signed_contributions():
+    """All-positive float data (U[0,100)): nothing can cancel, so the
+    comparator is the pure 1e-12 relative bound everywhere."""
+    from opentsdb_amd import core
+    from tests import datasets
+    b = datasets.random_batch(11, n_series=30, n_groups=3)
+    spec = core.make_spec(datasets.T0, datasets.T0 + 3 * 3600 * 1000,
+                          core.Aggregators.get("sum"),
+                          core.DownsamplingSpecification("1m-avg"),
+                          datasets.T0, datasets.T0 + 3 * 3600 * 1000)
+    ref = pyoracle.group_by(spec, b)
+    fl = contribution_floor(spec, b, ref)
+    assert sum(len(f) for f in fl) > 0
+    assert all((f == 0).all() for f in fl)
+
+
+def test_contribution_floor_is_set_where_signs_meet():
+    """Mixed-sign integer data (U[-50,100)): the floor is nonzero only where
+    both signs meet, finite, and far below the old raw-value floor
+    (1e-12 x 2,000 x max|raw|)."""
+    n_nonzero = n_points = 0
+    for seed in range(40):
+        b, spec, exact, where = _case(seed)
+        if spec.interp in (2, 3) or spec.rate:  # +-MAX_VALUE fill-ins
+            continue
+        try:
+            ref = pyoracle.group_by(spec, b)
+        except pyoracle.OracleError:
+            continue
+        for f in contribution_floor(spec, b, ref):
+            assert (f >= 0).all() and np.isfinite(f).all()
+            n_nonzero += int((f > 0).sum())
+            n_points += len(f)
+    assert 0 < n_nonzero < n_points

@@ -62,7 +62,91 @@ def cancel_floor(batch, terms):
     return 1e-12 * terms * float(mags.max())
 
 
+def _member_views(spec, batch):
+    """Per group, the oracle's view stream (Downsampler / RateSpan output,
+    seeked to the window start like AggregationIterator.java:421-437) of
+    every member SpanGroup.add keeps (SpanGroup.java:295-339)."""
+    offs = np.asarray(batch.offsets, np.int64)
+    ts = np.asarray(batch.ts, np.int64)
+    val = np.asarray(batch.val, np.int64)
+    isf = (np.ones(len(val), np.uint8) if batch.is_float is None
+           else np.asarray(batch.is_float, np.uint8))
+    g_off = np.asarray(batch.group_offsets, np.int64)
+    members = np.asarray(batch.group_members, np.int64)
+    out = []
+    for g in range(len(g_off) - 1):
+        views = []
+        for s in members[g_off[g]:g_off[g + 1]]:
+            p0, p1 = int(offs[s]), int(offs[s + 1])
+            if p1 <= p0 or not (ts[p0] <= spec.end_ms and
+                                ts[p1 - 1] >= spec.start_ms):
+                continue
+            v = pyoracle.view_stream(spec, ts[p0:p1], val[p0:p1],
+                                     isf[p0:p1], seek=spec.start_ms)
+            views.append((v["ts"], _vals(v["bits"], v["is_int"])))
+        out.append(views)
+    return out
+
+
+def contribution_floor(spec, batch, ref):
+    """Per emitted point, the absolute floor 1e-12 x sum|contributions|:
+    the values the cross-series aggregator is fed at that timestamp
+    (AggregationIterator.java:682-797) — each member's real value, or a bound
+    on its interpolated / held one — taken from the oracle's per-member view
+    streams.  Nonzero only where those contributions have both signs (a sum
+    of same-signed terms keeps its relative error); elsewhere the comparator
+    is the pure 1e-12 relative bound."""
+    interp = spec.interp
+    if interp < 0:
+        interp = core.Aggregators.by_id(spec.agg_id).interpolationMethod()
+    interp = int(interp)
+    big = np.finfo(np.float64).max
+    floors = []
+    for views, r in zip(_member_views(spec, batch), ref):
+        x = np.asarray(r["ts"], np.int64)
+        mag = np.zeros(len(x))
+        pos = np.zeros(len(x), bool)
+        neg = np.zeros(len(x), bool)
+        for vts, vv in views:
+            if len(vts) == 0:
+                continue
+            v = np.nan_to_num(vv, nan=0.0)
+            i = np.searchsorted(vts, x, "left")
+            exact_pt = (i < len(vts)) & (vts[np.minimum(i, len(vts) - 1)] == x)
+            y1 = v[np.minimum(i, len(vts) - 1)]
+            y0 = v[np.maximum(i - 1, 0)]
+            if spec.rate:
+                # every kept span contributes from the first emitted ts with
+                # its latest rate at or before x, the junk rate included
+                # (AggregationIterator.java:448-459, :744-753)
+                live = x <= vts[-1]
+                held = np.where(i > 0, y0, v[0])
+                lo = hi = np.where(exact_pt, y1, held)
+            else:
+                live = (x >= vts[0]) & (x <= vts[-1])
+                if interp == 0:    # LERP: between its neighbours
+                    lo, hi = y0, y1
+                elif interp == 1:  # ZIM
+                    lo = hi = np.zeros(len(x))
+                elif interp == 2:  # MAX
+                    lo = hi = np.full(len(x), big)
+                elif interp == 3:  # MIN
+                    lo = hi = np.full(len(x), -big)
+                else:              # PREV
+                    lo = hi = y0
+                lo = np.where(exact_pt, y1, lo)
+                hi = np.where(exact_pt, y1, hi)
+            m = np.maximum(np.abs(lo), np.abs(hi))
+            mag += np.where(live, m, 0.0)
+            pos |= live & ((lo > 0) | (hi > 0))
+            neg |= live & ((lo < 0) | (hi < 0))
+        floors.append(np.where(pos & neg, 1e-12 * mag, 0.0))
+    return floors
+
+
 def compare(got, ref, exact, where="", floor=0.0):
+    """floor: a scalar, or one per-point array per group
+    (contribution_floor)."""
     assert len(got) == len(ref), "%s: %d groups vs %d" % (where, len(got), len(ref))
     for g, (a, r) in enumerate(zip(got, ref)):
         w = "%s/g%d" % (where, g)
@@ -81,8 +165,9 @@ def compare(got, ref, exact, where="", floor=0.0):
             assert not bad.any(), "%s: not bit-exact at %s: %r vs %r" % (
                 w, np.nonzero(bad)[0][:5], va[bad][:5], vr[bad][:5])
         else:
+            fl = floor if np.isscalar(floor) else np.asarray(floor[g])[~na]
             d = np.abs(va - vr)[~na]
-            tol = 1e-12 * np.maximum(np.abs(va), np.abs(vr))[~na] + floor
+            tol = 1e-12 * np.maximum(np.abs(va), np.abs(vr))[~na] + fl
             inf = ~np.isfinite(va[~na]) | ~np.isfinite(vr[~na])
             assert np.array_equal(va[~na][inf], vr[~na][inf]), w + ": inf"
             ok = (d <= tol) | inf
@@ -107,9 +192,13 @@ def run_both(engine, spec, batch):
 
 
 def check(engine, spec, batch, exact, where="", floor=0.0):
-    """run_both + compare; a query both sides reject is parity too."""
+    """run_both + compare; a query both sides reject is parity too.
+    floor="contributions": contribution_floor of the oracle's result."""
     got, ref = run_both(engine, spec, batch)
     if ref is not None:
+        if isinstance(floor, str):
+            assert floor == "contributions"
+            floor = contribution_floor(spec, batch, ref)
         compare(got, ref, exact, where, floor)
     return got, ref
 

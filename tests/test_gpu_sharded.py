@@ -199,3 +199,79 @@ def test_two_processes_gloo():
         got = [DataPoints(*merged[g]) for g in range(hb.n_groups)]
         compare(got, ref, ds == "max" and agg not in ("sum", "dev"),
                 where="gloo/%s" % agg)
+
+
+def _rccl_main(port, q):
+    """World size 1 over RCCL: the device-tensor collectives of the sharded
+    path (classify_groups' MIN all-reduce, the partial all-gather, the
+    selection protocol's count / histogram all-reduces) run through
+    ProcessGroupNCCL = RCCL, exactly as bench.py's node launch calls them."""
+    import torch
+    import torch.distributed as tdist
+    torch.cuda.set_device(0)
+    tdist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port,
+                             rank=0, world_size=1,
+                             device_id=torch.device("cuda", 0))
+    assert tdist.get_backend() == "nccl"
+    e = Engine(0)
+    hb = datasets.random_batch(207, n_series=50, n_groups=3, nan_frac=0.02)
+    out = []
+    for agg, ds, fill in QUERIES:
+        spec = _spec(agg, ds, fill)
+        db = odist.to_device(hb)
+        # rank-local groups (classification all-reduce on device)
+        res = odist.run_sharded_any(e, spec, db, hb.n_groups)
+        torch.cuda.synchronize()
+        local = {g: tuple(a.copy() for a in v)
+                 for g, v in res.host_groups().items()}
+        # every group through the shared-group exchange: partials
+        # all-gathered over RCCL, merged by otsdb_agg_finalize_device
+        shared = None
+        if agg not in ("p99", "median"):
+            real = odist.classify_groups
+            odist.classify_groups = lambda goff, group=None, device=None: (
+                np.zeros(0, np.int64), np.nonzero(np.diff(goff) > 0)[0])
+            try:
+                db2 = odist.to_device(hb)
+                r2 = odist.run_sharded(e, spec, db2, hb.n_groups)
+            finally:
+                odist.classify_groups = real
+            torch.cuda.synchronize()
+            assert len(r2.shared_ids) == hb.n_groups
+            shared = {g: tuple(a.copy() for a in v)
+                      for g, v in r2.host_groups().items()}
+        out.append((local, shared))
+    tdist.barrier()
+    tdist.destroy_process_group()
+    e.close()
+    q.put(out)
+
+
+def test_rccl_world_size_one():
+    import queue
+    import time
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_main, args=(_free_port(), q))
+    p.start()
+    deadline = time.time() + 100
+    out = None
+    while out is None:
+        assert time.time() < deadline, "the RCCL rank did not report"
+        try:
+            out = q.get(timeout=5)
+        except queue.Empty:
+            assert p.is_alive() or p.exitcode == 0, p.exitcode
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    hb = datasets.random_batch(207, n_series=50, n_groups=3, nan_frac=0.02)
+    for (agg, ds, fill), (local, shared) in zip(QUERIES, out):
+        ref = pyoracle.group_by(_spec(agg, ds, fill), hb)
+        exact = ds == "max" and agg not in ("sum", "dev")
+        for name, res in (("local", local), ("shared", shared)):
+            if res is None:
+                continue
+            assert sorted(res) == list(range(hb.n_groups))
+            got = [DataPoints(*res[g]) for g in range(hb.n_groups)]
+            compare(got, ref, exact, where="rccl/%s/%s" % (name, agg))

@@ -9,7 +9,7 @@ import pytest
 
 from opentsdb_amd import core
 from tests import datasets
-from tests.test_gpu_parity import check, cancel_floor
+from tests.test_gpu_parity import check
 
 pytestmark = pytest.mark.gpu
 
@@ -59,8 +59,9 @@ def _case(seed):
     spec = core.make_spec(t0, t1, core.Aggregators.get(agg),
                           core.DownsamplingSpecification("%s-%s-%s" % (iv, ds, fill)),
                           t0, t1, rate, ro, interp)
-    exact = (ds in EXACT_DS and agg in EXACT_AGG and not rate
-             and kind != "mixed")
+    # order-free downsamplers feeding order-free aggregators: bit-exact,
+    # rate queries included (one RateSpan division of exact values)
+    exact = ds in EXACT_DS and agg in EXACT_AGG
     return b, spec, exact, "%d:%s:%s-%s-%s%s%s" % (
         seed, agg, iv, ds, fill, ":rate" if rate else "",
         "" if interp is None else ":i%d" % interp)
@@ -69,9 +70,9 @@ def _case(seed):
 @pytest.mark.parametrize("seed", range(120))
 def test_random_query_sweep(engine, seed):
     b, spec, exact, where = _case(seed)
-    # sums of mixed-sign data cancel: the data's own 1e-12 floor
-    fl = cancel_floor(b, 2000)
-    check(engine, spec, b, exact, where=where, floor=fl)
+    # 1e-12 relative; an absolute 1e-12 x sum|contributions| only at points
+    # whose contributions have both signs (contribution_floor)
+    check(engine, spec, b, exact, where=where, floor="contributions")
 
 
 def _rate_case(seed):
@@ -99,11 +100,12 @@ def _rate_case(seed):
     spec = core.make_spec(t0, t1, core.Aggregators.get(agg),
                           core.DownsamplingSpecification("%s-%s" % (iv, ds)),
                           t0, t1, True, ro)
-    return b, spec, "%d:%s:%s-%s:drop=%s:max=%d:reset=%d" % (
+    exact = ds in EXACT_DS and agg in EXACT_AGG
+    return b, spec, exact, "%d:%s:%s-%s:drop=%s:max=%d:reset=%d" % (
         seed, agg, iv, ds, drop, cmax, reset)
 
 
 @pytest.mark.parametrize("seed", range(60))
 def test_random_rate_sweep(engine, seed):
-    b, spec, where = _rate_case(seed)
-    check(engine, spec, b, False, where=where, floor=cancel_floor(b, 2000))
+    b, spec, exact, where = _rate_case(seed)
+    check(engine, spec, b, exact, where=where, floor="contributions")
