@@ -149,15 +149,34 @@ typedef struct {
    * (past the batch's last point if spans hold points beyond the window).
    * Bucket k is [cal_edges[k], cal_edges[k+1]) with timestamp cal_edges[k]
    * (ValuesInInterval.getIntervalTimestamp, :437-449).  The reference
-   * anchors each series at previousInterval(its first point); the caller
-   * passes a table only when every such anchor in [start_ms, end_ms] is an
-   * edge (the grid does not depend on the series) and otherwise keeps the
-   * Java iterators.  A point past the window whose bucket end is not in the
-   * table is OTSDB_E_UNSUPPORTED.  NULL with use_calendar = 1 ->
-   * OTSDB_E_UNSUPPORTED.  ds_interval_ms stays DownsamplingSpecification's
-   * nominal interval (parseDuration), which the scan bounds use.          */
+   * anchors each series at previousInterval(its first point): when every
+   * such anchor in the window is an edge of this one table (the grid does
+   * not depend on the series: 1dc, 1hc, 1nc, 30mc, ... in any zone) the
+   * caller passes it alone (n_cal_anchors = 0).  A point past the window
+   * whose bucket end is not in the table is OTSDB_E_UNSUPPORTED.  NULL with
+   * use_calendar = 1 -> OTSDB_E_UNSUPPORTED.  ds_interval_ms stays
+   * DownsamplingSpecification's nominal interval (parseDuration), which the
+   * scan bounds use.                                                       */
   const int64_t* cal_edges;
   int64_t n_cal_edges;
+  /* Per-series calendar anchors (n_cal_anchors > 0; 7mc, 2wc, 6hc across a
+   * DST change, ...): cal_edges then holds CHAINS, each the Downsampler's
+   * calendar stepped from one anchor (Downsampler.java:330-345, :383-397)
+   * until two edges lie past the window / the batch's last point, strictly
+   * ascending and ended by INT64_MAX.  cal_anchors[j] (ascending) are
+   * DateTime.previousInterval values and cal_anchor_edge[j] the index in
+   * cal_edges of the chain edge equal to cal_anchors[j]; for every series'
+   * first point f after the seek, previousInterval(f) must be the largest
+   * anchor <= f (true when the anchors hold every previousInterval value of
+   * the window, or just the ones the batch's series take), and so must
+   * previousInterval(start_ms) (the seek, Downsampler.java:419-429).  Series
+   * grids then differ, and the output timestamps are the union of the
+   * series' bucket starts (AggregationIterator.next).  FillingDownsampler
+   * fills over such grids (fill != NONE) -> OTSDB_E_UNSUPPORTED, as do the
+   * multi-GPU partial / selection entry points.  HOST memory.             */
+  const int64_t* cal_anchors;
+  const int64_t* cal_anchor_edge;
+  int64_t n_cal_anchors;
 } otsdb_query_spec;
 
 /* ------------------------------------------------------------------------ */

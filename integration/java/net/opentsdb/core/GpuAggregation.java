@@ -122,6 +122,7 @@ public final class GpuAggregation {
    * status is thrown as the reference's exception.
    */
   static native int nativeRunCells(long ctx, long[] spec, long[] calEdges,
+      long[] calAnchors, long[] calAnchorEdge,
       int nSeries, long[] rowSeries, long[] rowBase, long[] qualOff,
       byte[] qual, long[] valOff, byte[] val, long[] groupOffsets,
       long[] groupMembers, long[] outOffsets, long[] outTs, long[] outVal,
@@ -162,7 +163,7 @@ public final class GpuAggregation {
     }
     spec[SPEC_AGG] = agg;
     spec[SPEC_INTERP] = -1;  // the aggregator's own interpolation
-    long[] cal = null;
+    long[][] cal = null;
     if (ds != null && ds != DownsamplingSpecification.NO_DOWNSAMPLER) {
       final int ds_agg = nativeAggId(ds.getFunction().toString());
       if (ds_agg < 0 || ds.getFillPolicy() == FillPolicy.SCALAR) {
@@ -177,7 +178,8 @@ public final class GpuAggregation {
       spec[SPEC_RUN_ALL] =
           si != null && si.toLowerCase().contains("all") ? 1 : 0;
       if (ds.useCalendar() && spec[SPEC_RUN_ALL] == 0) {
-        cal = calendarEdges(ds, spec[SPEC_START_MS], spec[SPEC_END_MS]);
+        cal = calendarTables(ds, groups, spec[SPEC_START_MS],
+            spec[SPEC_END_MS]);
         if (cal == null) {
           return null;
         }
@@ -266,7 +268,9 @@ public final class GpuAggregation {
       final long[] out_ts = new long[(int) cap];
       final long[] out_val = new long[(int) cap];
       final byte[] out_is_int = new byte[(int) cap];
-      final int st = nativeRunCells(ctx, spec, cal, n_series, row_series,
+      final int st = nativeRunCells(ctx, spec, cal == null ? null : cal[0],
+          cal == null ? null : cal[1], cal == null ? null : cal[2], n_series,
+          row_series,
           row_base, qual_off, qual, val_off, val, group_offsets,
           group_members, out_offsets, out_ts, out_val, out_is_int);
       if (st == CAPACITY) {
@@ -301,48 +305,138 @@ public final class GpuAggregation {
     }
   }
 
+  /** Ends each chain of an anchored calendar table (otsdb_agg.h). */
+  static final long CHAIN_END = Long.MAX_VALUE;
+
+  /** The Downsampler's step of a calendar (Downsampler.java:387-394). */
+  private static void step(final Calendar c, final int n, final int unit) {
+    if (unit == Calendar.DAY_OF_WEEK) {
+      c.add(Calendar.DAY_OF_MONTH, 7 * n);
+    } else {
+      c.add(unit, n);
+    }
+  }
+
   /**
-   * The calendar bucket grid the reference's Downsampler walks
-   * (DateTime.previousInterval + Calendar.add, Downsampler.java:330-397),
-   * from previousInterval(start) until two edges lie past end, or null when
-   * a series could anchor its own grid off these edges (the engine then does
-   * not take the query).
+   * The calendar tables of otsdb_query_spec, built with the reference's own
+   * DateTime.previousInterval and Calendar.add.  {edges} alone when every
+   * series' grid is the one anchored at previousInterval(start)
+   * (previousInterval(first point) of every series in the window is one of
+   * its edges); otherwise {chains, anchors, anchor edges}: the series' own
+   * anchors previousInterval(first point after the seek) — each series'
+   * first point decoded through its Span iterator — and the window's, each
+   * with the chain the Downsampler steps from it (Downsampler.java:330-345,
+   * :383-397).  Null when a table would be unreasonably large.
    */
-  static long[] calendarEdges(final DownsamplingSpecification ds,
-      final long start_ms, final long end_ms) {
+  static long[][] calendarTables(final DownsamplingSpecification ds,
+      final SpanGroup[] groups, final long start_ms, final long end_ms) {
     final String si = ds.getStringInterval();
     final int n = DateTime.getDurationInterval(si);
     final String units = DateTime.getDurationUnits(si);
     final int unit = DateTime.unitsToCalendarType(units);
     final TimeZone tz = ds.getTimezone();
-    final Calendar c = DateTime.previousInterval(start_ms, n, unit, tz);
+    // the last point any span holds: chains run two edges past it
+    long last = end_ms;
+    for (final SpanGroup g : groups) {
+      for (final Span span : g.getSpans()) {
+        if (span.size() > 0) {
+          last = Math.max(last, span.timestamp(span.size() - 1));
+        }
+      }
+    }
+    // the window's own grid
+    final long[] global = chain(DateTime.previousInterval(start_ms, n, unit,
+        tz), n, unit, last);
+    if (global == null) {
+      return null;
+    }
+    // ValuesInInterval.seekInterval(start) (Downsampler.java:419-429)
+    long seek = global[0];
+    if (start_ms > seek) {
+      seek = global[1];
+    }
+    final java.util.TreeSet<Long> anchors = new java.util.TreeSet<Long>();
+    anchors.add(global[0]);
+    boolean shared = true;
+    final java.util.HashSet<Long> on_global = new java.util.HashSet<Long>();
+    for (final long e : global) {
+      on_global.add(e);
+    }
+    for (final SpanGroup g : groups) {
+      for (final Span span : g.getSpans()) {
+        final SeekableView it = span.iterator();
+        it.seek(seek);
+        if (!it.hasNext()) {
+          continue;
+        }
+        final long f = it.next().timestamp();
+        final long a = DateTime.previousInterval(f, n, unit, tz)
+            .getTimeInMillis();
+        anchors.add(a);
+        shared &= on_global.contains(a);
+      }
+    }
+    if (shared) {
+      return new long[][] {global, null, null};
+    }
+    // one chain per anchor not already on an earlier chain
+    final ArrayList<Long> edges = new ArrayList<Long>();
+    final java.util.HashMap<Long, Integer> pos =
+        new java.util.HashMap<Long, Integer>();
+    final long[] anchor_arr = new long[anchors.size()];
+    final long[] anchor_edge = new long[anchors.size()];
+    int j = 0;
+    for (final long a : anchors) {
+      Integer p = pos.get(a);
+      if (p == null) {
+        final Calendar c = Calendar.getInstance(tz);
+        c.setTimeInMillis(a);
+        final long[] ch = chain(c, n, unit, last);
+        if (ch == null) {
+          return null;
+        }
+        p = edges.size();
+        for (int k = 0; k < ch.length; k++) {
+          if (!pos.containsKey(ch[k])) {
+            pos.put(ch[k], p + k);
+          }
+          edges.add(ch[k]);
+        }
+        edges.add(CHAIN_END);
+        if (edges.size() > 4000000) {
+          return null;
+        }
+      }
+      anchor_arr[j] = a;
+      anchor_edge[j] = p;
+      j++;
+    }
+    final long[] out = new long[edges.size()];
+    for (int i = 0; i < out.length; i++) {
+      out[i] = edges.get(i);
+    }
+    return new long[][] {out, anchor_arr, anchor_edge};
+  }
+
+  /** A calendar's steps until two edges lie past `last`. */
+  private static long[] chain(final Calendar c, final int n, final int unit,
+      final long last) {
     final ArrayList<Long> edges = new ArrayList<Long>();
     edges.add(c.getTimeInMillis());
     int past = 0;
     while (past < 2) {
-      if (unit == Calendar.DAY_OF_WEEK) {
-        c.add(Calendar.DAY_OF_MONTH, 7 * n);
-      } else {
-        c.add(unit, n);
-      }
+      step(c, n, unit);
       edges.add(c.getTimeInMillis());
-      if (c.getTimeInMillis() > end_ms) {
+      if (c.getTimeInMillis() > last) {
         past++;
       }
-      if (edges.size() > 10000000) {
+      if (edges.size() > 4000000) {
         return null;
       }
     }
     final long[] out = new long[edges.size()];
     for (int i = 0; i < out.length; i++) {
       out[i] = edges.get(i);
-    }
-    // every anchor a series could start from must be an edge
-    for (int i = 0; i + 1 < out.length && out[i] <= end_ms; i++) {
-      final Calendar a = DateTime.previousInterval(out[i] + 1, n, unit, tz);
-      if (a.getTimeInMillis() != out[i]) {
-        return null;
-      }
     }
     return out;
   }

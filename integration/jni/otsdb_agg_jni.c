@@ -102,7 +102,7 @@ static void* alloc_out(JNIEnv* env, jarray a, size_t elem, int* failed) {
 
 JNIEXPORT jint JNICALL Java_net_opentsdb_core_GpuAggregation_nativeRunCells(
     JNIEnv* env, jclass cls, jlong ctx, jlongArray jspec, jlongArray jcal,
-    jint n_series, jlongArray jrow_series, jlongArray jrow_base,
+    jlongArray janch, jlongArray janch_edge, jint n_series, jlongArray jrow_series, jlongArray jrow_base,
     jlongArray jqual_off, jbyteArray jqual, jlongArray jval_off,
     jbyteArray jval, jlongArray jgoff, jlongArray jgmem, jlongArray jooff,
     jlongArray jots, jlongArray joval, jbyteArray joisint) {
@@ -143,8 +143,14 @@ JNIEXPORT jint JNICALL Java_net_opentsdb_core_GpuAggregation_nativeRunCells(
     return OTSDB_E_ILLEGAL_ARGUMENT;
   }
 
+  if ((janch == NULL) != (janch_edge == NULL) ||
+      (janch && (*env)->GetArrayLength(env, janch) !=
+                    (*env)->GetArrayLength(env, janch_edge))) {
+    throw_status(env, OTSDB_E_ILLEGAL_ARGUMENT);
+    return OTSDB_E_ILLEGAL_ARGUMENT;
+  }
   int failed = 0;
-  void* in[9];
+  void* in[11];
   in[0] = copy_in(env, jcal, 8, 0, &failed);
   in[1] = copy_in(env, jrow_series, 8, 0, &failed);
   in[2] = copy_in(env, jrow_base, 8, 0, &failed);
@@ -154,6 +160,8 @@ JNIEXPORT jint JNICALL Java_net_opentsdb_core_GpuAggregation_nativeRunCells(
   in[6] = copy_in(env, jval, 1, 1, &failed);
   in[7] = copy_in(env, jgoff, 8, 0, &failed);
   in[8] = copy_in(env, jgmem, 8, 0, &failed);
+  in[9] = copy_in(env, janch, 8, 0, &failed);
+  in[10] = copy_in(env, janch_edge, 8, 0, &failed);
   void* out[4];
   out[0] = alloc_out(env, jooff, 8, &failed);
   out[1] = alloc_out(env, jots, 8, &failed);
@@ -164,6 +172,9 @@ JNIEXPORT jint JNICALL Java_net_opentsdb_core_GpuAggregation_nativeRunCells(
   if (!failed) {
     s.cal_edges = (const int64_t*)in[0];
     s.n_cal_edges = jcal ? (*env)->GetArrayLength(env, jcal) : 0;
+    s.cal_anchors = (const int64_t*)in[9];
+    s.cal_anchor_edge = (const int64_t*)in[10];
+    s.n_cal_anchors = janch ? (*env)->GetArrayLength(env, janch) : 0;
     otsdb_cells c;
     c.n_rows = n_rows;
     c.row_series = (const int64_t*)in[1];
@@ -197,7 +208,7 @@ JNIEXPORT jint JNICALL Java_net_opentsdb_core_GpuAggregation_nativeRunCells(
       (*env)->SetByteArrayRegion(env, joisint, 0, n, (const jbyte*)out[3]);
     }
   }
-  for (int i = 0; i < 9; ++i) free(in[i]);
+  for (int i = 0; i < 11; ++i) free(in[i]);
   for (int i = 0; i < 4; ++i) free(out[i]);
   if ((*env)->ExceptionCheck(env)) return OTSDB_E_DEVICE; /* OOM pending */
   if (failed) {

@@ -44,6 +44,9 @@ class QuerySpec(C.Structure):
         ("reset_value", C.c_int64),
         ("cal_edges", C.c_void_p),
         ("n_cal_edges", C.c_int64),
+        ("cal_anchors", C.c_void_p),
+        ("cal_anchor_edge", C.c_void_p),
+        ("n_cal_anchors", C.c_int64),
     ]
 
 

@@ -420,15 +420,32 @@ def make_spec(start_time, end_time, aggregator, downsampler=None,
             # UnsupportedOperationException when it depends on the series
             import numpy as np
             from . import jcalendar
+            anchors = None
             if cal_edges is None:
                 n, unit = downsampler.calendar_interval()
-                cal_edges = jcalendar.calendar_edges(
-                    s.start_ms, s.end_ms, n, unit, downsampler.getTimezone(),
-                    cover_ms=cal_cover_ms)
+                tz = downsampler.getTimezone()
+                try:
+                    cal_edges = jcalendar.calendar_edges(
+                        s.start_ms, s.end_ms, n, unit, tz,
+                        cover_ms=cal_cover_ms)
+                except UnsupportedOperationException:
+                    # the grid depends on each series' first point: chains
+                    # per anchor (otsdb_query_spec.cal_anchors)
+                    cal_edges, anchors, anchor_edge = \
+                        jcalendar.calendar_anchor_tables(
+                            s.start_ms, s.end_ms, n, unit, tz,
+                            cover_ms=cal_cover_ms)
             edges = np.ascontiguousarray(cal_edges, np.int64)
             s._cal_edges_ref = edges  # keeps the table alive with the spec
             s.cal_edges = edges.ctypes.data
             s.n_cal_edges = len(edges)
+            if anchors is not None:
+                a = np.ascontiguousarray(anchors, np.int64)
+                ae = np.ascontiguousarray(anchor_edge, np.int64)
+                s._cal_anchor_refs = (a, ae)
+                s.cal_anchors = a.ctypes.data
+                s.cal_anchor_edge = ae.ctypes.data
+                s.n_cal_anchors = len(a)
     ro = rate_options or RateOptions()
     s.rate = int(bool(rate))
     s.counter = int(ro.counter)

@@ -26,6 +26,7 @@
 #include "decode.hip"
 #include "raw.hip"
 #include "rows.hip"
+#include "calendar.hip"
 #include "launch.h"
 
 using namespace otsdb;
@@ -168,6 +169,8 @@ struct otsdb_ctx {
   size_t cells_col_cap = 0;
   void* cal = nullptr;  // calendar bucket edges of the current query
   size_t cal_cap = 0;
+  void* acal = nullptr;  // per-series calendar: chains, anchors, series'
+  size_t acal_cap = 0;   // chain positions and bucket-start timestamps
   void* dec_ws = nullptr;  // decode workspace
   size_t dec_ws_cap = 0;
   void* ws2 = nullptr;     // raw group-by: candidates, sort, selection slab
@@ -240,7 +243,35 @@ otsdb_status check_spec(const otsdb_query_spec* s) {
   if (s->ds_agg_id == OTSDB_AGG_NONE)
     return fail(OTSDB_E_ILLEGAL_ARGUMENT,
                 "cannot use the NONE aggregator for downsampling");
-  if (s->use_calendar && !s->run_all) {
+  if (s->use_calendar && !s->run_all && s->n_cal_anchors > 0) {
+    // per-series anchors: chains ended by INT64_MAX, anchors ascending, each
+    // naming its chain edge
+    const int64_t n = s->n_cal_edges, na = s->n_cal_anchors;
+    if (!s->cal_edges || n < 3 || !s->cal_anchors || !s->cal_anchor_edge)
+      return fail(OTSDB_E_ILLEGAL_ARGUMENT, "anchored calendar without tables");
+    if (s->cal_edges[n - 1] != INT64_MAX)
+      return fail(OTSDB_E_ILLEGAL_ARGUMENT,
+                  "anchored cal_edges must end with INT64_MAX");
+    for (int64_t k = 1; k < n; ++k)
+      if (s->cal_edges[k - 1] != INT64_MAX && s->cal_edges[k] != INT64_MAX &&
+          s->cal_edges[k] <= s->cal_edges[k - 1])
+        return fail(OTSDB_E_ILLEGAL_ARGUMENT,
+                    "cal_edges chains must increase strictly (index %lld)",
+                    (long long)k);
+    for (int64_t j = 0; j < na; ++j) {
+      const int64_t e = s->cal_anchor_edge[j];
+      if ((j && s->cal_anchors[j] <= s->cal_anchors[j - 1]) || e < 0 ||
+          e >= n || s->cal_edges[e] != s->cal_anchors[j])
+        return fail(OTSDB_E_ILLEGAL_ARGUMENT, "bad calendar anchor %lld",
+                    (long long)j);
+    }
+    if (s->cal_anchors[0] > s->start_ms)
+      return fail(OTSDB_E_ILLEGAL_ARGUMENT,
+                  "no calendar anchor at or before start_ms");
+    if (s->fill != OTSDB_FILL_NONE)
+      return fail(OTSDB_E_UNSUPPORTED,
+                  "fill policies over per-series calendar grids");
+  } else if (s->use_calendar && !s->run_all) {
     if (!s->cal_edges || s->n_cal_edges < 2)
       return fail(OTSDB_E_UNSUPPORTED,
                   "calendar downsampling without a bucket-edge table");
@@ -361,6 +392,9 @@ otsdb_status make_params(const otsdb_query_spec* s, Params* P,
   const int64_t iv = s->ds_interval_ms;
   P->interval = iv;
   P->inv_interval = 1.0 / (double)iv;
+  if (s->use_calendar && s->n_cal_anchors > 0)  // callers derive stage B
+    return fail(OTSDB_E_UNSUPPORTED,
+                "per-series calendar grids on this entry point");
   if (s->use_calendar) return make_cal_params(s, P, c);
   const int64_t grid0 = align_down(s->start_ms + iv - 1, iv);
   P->gbase = grid0;
@@ -384,6 +418,52 @@ otsdb_status make_params(const otsdb_query_spec* s, Params* P,
   // points fed to the bucket fold lie in [gbase, stop_ts): 32-bit offsets
   P->narrow = iv < (int64_t(1) << 31) && P->nb < (int64_t(1) << 32) / iv;
   return OTSDB_OK;
+}
+
+// Per-series calendar grids (calendar.hip): the union grid U of stage B,
+// each anchor's chain terminator, the window's seek and the stage-B spec.
+struct AnchoredPlan {
+  std::vector<int64_t> U, chain_end;
+  int64_t seek_ts = 0;
+  otsdb_query_spec derived;
+};
+
+bool anchored(const otsdb_query_spec* s) {
+  return s->use_calendar && !s->run_all && s->n_cal_anchors > 0 &&
+         s->ds_interval_ms > 0;
+}
+
+otsdb_status plan_anchored(const otsdb_query_spec* s, AnchoredPlan* A) {
+  const int64_t n = s->n_cal_edges, na = s->n_cal_anchors;
+  const int64_t* e = s->cal_edges;
+  A->U.clear();
+  A->U.reserve(n);
+  for (int64_t k = 0; k < n; ++k)
+    if (e[k] != INT64_MAX) A->U.push_back(e[k]);
+  std::sort(A->U.begin(), A->U.end());
+  A->U.erase(std::unique(A->U.begin(), A->U.end()), A->U.end());
+  std::vector<int64_t> term(n + 1, n);
+  for (int64_t k = n - 1; k >= 0; --k) term[k] = e[k] == INT64_MAX ? k : term[k + 1];
+  A->chain_end.resize(na);
+  for (int64_t j = 0; j < na; ++j) A->chain_end[j] = term[s->cal_anchor_edge[j]];
+  // ValuesInInterval.seekInterval(start): previousInterval(start), stepped
+  // once when start lies past it (Downsampler.java:419-429)
+  const int64_t j = (int64_t)(std::upper_bound(s->cal_anchors,
+                                               s->cal_anchors + na,
+                                               s->start_ms) -
+                              s->cal_anchors) - 1;
+  int64_t k = s->cal_anchor_edge[j];
+  if (s->start_ms > e[k]) ++k;
+  if (e[k] == INT64_MAX)
+    return fail(OTSDB_E_UNSUPPORTED, "calendar chain ends before the seek");
+  A->seek_ts = e[k];
+  A->derived = *s;
+  A->derived.cal_edges = A->U.data();
+  A->derived.n_cal_edges = (int64_t)A->U.size();
+  A->derived.cal_anchors = nullptr;
+  A->derived.cal_anchor_edge = nullptr;
+  A->derived.n_cal_anchors = 0;
+  return check_spec(&A->derived);
 }
 
 // sel_all: every group (even one without local members) joins the radix
@@ -1185,9 +1265,80 @@ otsdb_status run_raw(otsdb_ctx* c, const otsdb_query_spec* spec,
 
 otsdb_status run_device_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
                              const otsdb_batch* b, otsdb_result* out,
+                             std::vector<int64_t>& goff);
+
+// Per-series calendar grids: stage A rewrites the timestamps to the series'
+// own bucket starts (calendar.hip), stage B runs the calendar pipeline over
+// the union grid.
+otsdb_status run_anchored(otsdb_ctx* c, const otsdb_query_spec* spec,
+                          const otsdb_batch* b, otsdb_result* out,
+                          std::vector<int64_t>& goff) {
+  AnchoredPlan A;
+  otsdb_status rc = plan_anchored(spec, &A);
+  if (rc) return rc;
+  hipStream_t st = c->stream;
+  const int64_t S = b->n_series, n = spec->n_cal_edges,
+                na = spec->n_cal_anchors;
+  int64_t N = 0;
+  if (S > 0) {
+    HIP_TRY(hipMemcpyAsync(&N, b->offsets + S, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  auto carve = [&](char* base) {
+    Carve cv{base};
+    void* p[8];
+    p[0] = cv.take<int64_t>(n);
+    p[1] = cv.take<int64_t>(na);
+    p[2] = cv.take<int64_t>(na);
+    p[3] = cv.take<int64_t>(na);
+    p[4] = cv.take<int64_t>(S + 1);
+    p[5] = cv.take<int64_t>(S + 1);
+    p[6] = cv.take<int64_t>(S + 1);
+    p[7] = cv.take<int64_t>(std::max<int64_t>(N, 2));
+    return std::make_pair(cv.off + 256, std::vector<void*>(p, p + 8));
+  };
+  rc = ensure(&c->acal, &c->acal_cap, carve(nullptr).first);
+  if (rc) return rc;
+  auto pp = carve((char*)c->acal).second;
+  HIP_TRY(hipMemcpyAsync(pp[0], spec->cal_edges, 8 * n, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(pp[1], spec->cal_anchors, 8 * na, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(pp[2], spec->cal_anchor_edge, 8 * na,
+                         hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(pp[3], A.chain_end.data(), 8 * na,
+                         hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), st));
+  AnchoredCal AC{(const int64_t*)pp[0], (const int64_t*)pp[1],
+                 (const int64_t*)pp[2], (const int64_t*)pp[3], na};
+  BatchDev B{S, b->offsets, b->ts_ms, b->val, b->is_float, b->series_float};
+  int64_t* vts = (int64_t*)pp[7];
+  if (S > 0) {
+    hipLaunchKernelGGL(k_cal_anchor, dim3(blocks_for(S, 256)), dim3(256), 0,
+                       st, spec->start_ms, spec->end_ms, A.seek_ts, B, AC,
+                       (int64_t*)pp[4], (int64_t*)pp[5], (int64_t*)pp[6],
+                       c->d_err);
+    hipLaunchKernelGGL(k_cal_vts, dim3(blocks_for(S, 4)), dim3(256), 0, st,
+                       spec->start_ms, B, AC, (const int64_t*)pp[4],
+                       (const int64_t*)pp[5], (const int64_t*)pp[6], vts,
+                       c->d_err);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (c->h_small[0] & ERR_CAL_RANGE)
+      return fail(OTSDB_E_UNSUPPORTED,
+                  "a point lies outside its series' calendar chain");
+  }
+  otsdb_batch vb = *b;
+  vb.ts_ms = vts;
+  return run_device_impl(c, &A.derived, &vb, out, goff);
+}
+
+otsdb_status run_device_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
+                             const otsdb_batch* b, otsdb_result* out,
                              std::vector<int64_t>& goff) {
   otsdb_status rc = check_spec(spec);
   if (rc) return rc;
+  if (anchored(spec)) return run_anchored(c, spec, b, out, goff);
   Params P;
   rc = make_params(spec, &P, c);
   if (rc) return rc;
@@ -1283,11 +1434,15 @@ otsdb_status run_cells_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
   if (S < 0 || R < 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
   const bool ds = spec->ds_interval_ms > 0 || spec->run_all;
   Params P;
-  rc = make_params(spec, &P, c);
-  if (rc) return rc;
+  // per-series calendar grids rewrite columnar timestamps: decode first
+  const bool fused = ds && !anchored(spec);
+  if (fused) {
+    rc = make_params(spec, &P, c);
+    if (rc) return rc;
+  }
   CellsDev C{R, cells->row_series, cells->row_base_s, cells->qual_off,
              cells->qual, cells->val_off, cells->val};
-  if (ds && !P.ds_sel && !P.run_all) {
+  if (fused && !P.ds_sel && !P.run_all) {
     rc = ensure(&c->cells_ws, &c->cells_ws_cap, (size_t)(S + 1) * 8);
     if (rc) return rc;
     int64_t* series_row = (int64_t*)c->cells_ws;
@@ -1679,6 +1834,7 @@ void otsdb_ctx_destroy(otsdb_ctx* c) {
   if (c->dec_ws) hipFree(c->dec_ws);
   if (c->ws2) hipFree(c->ws2);
   if (c->cal) hipFree(c->cal);
+  if (c->acal) hipFree(c->acal);
   if (c->cells_ws) hipFree(c->cells_ws);
   if (c->cells_col) hipFree(c->cells_col);
   if (c->rows_ws) hipFree(c->rows_ws);
@@ -1719,6 +1875,12 @@ otsdb_status otsdb_agg_plan(otsdb_ctx* c, const otsdb_query_spec* spec,
   if (!spec || !b || !out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
   otsdb_status rc = check_spec(spec);
   if (rc) return rc;
+  AnchoredPlan A;
+  if (anchored(spec)) {  // stage B's union grid
+    rc = plan_anchored(spec, &A);
+    if (rc) return rc;
+    spec = &A.derived;
+  }
   Params P;
   rc = make_params(spec, &P);
   if (rc) return rc;

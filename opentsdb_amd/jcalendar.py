@@ -307,6 +307,101 @@ def calendar_edges(start_ms, end_ms, interval, unit, tz=None, extra=2,
     return e
 
 
+SENTINEL = (1 << 63) - 1  # ends each chain of an anchored table
+MAX_ANCHORS = 1 << 20
+
+
+def _next_top(t, top, tz):
+    """The "top of <period>" instant after top t (previousInterval's snap
+    grid, DateTime.java:468-599)."""
+    if top == MILLISECOND:    # top of second
+        return _set_fields(t + 1000, tz, top)
+    if top == SECOND:         # top of minute
+        return _set_fields(t + 60000, tz, top)
+    u = {MINUTE: HOUR_OF_DAY, HOUR_OF_DAY: DAY_OF_MONTH,
+         DAY_OF_MONTH: MONTH, YEAR: YEAR, DAY_OF_WEEK: DAY_OF_MONTH}[top]
+    n = 7 if top == DAY_OF_WEEK else 1
+    t2 = _set_fields(cal_add(t, u, n, tz), tz, top)
+    if t2 <= t:
+        raise UnsupportedOperationException("calendar snap does not advance")
+    return t2
+
+
+def calendar_anchor_tables(start_ms, end_ms, interval, unit, tz=None,
+                           extra=2, cover_ms=None, max_edges=MAX_EDGES,
+                           max_anchors=MAX_ANCHORS):
+    """Per-series calendar grids (the reference anchors every series at
+    DateTime.previousInterval(its first point), Downsampler.java:330-345, and
+    steps that calendar, :383-397), as the tables otsdb_query_spec carries
+    when one edge table does not serve every series:
+
+      anchors  every value previousInterval(t) takes for t in
+               [start_ms, max(end_ms, cover_ms)], ascending — so
+               previousInterval(t) = the largest anchor <= t;
+      edges    chains, each the Downsampler's steps from an anchor until
+               `extra` edges lie past max(end_ms, cover_ms), each ended by
+               SENTINEL; anchors on one chain share it;
+      anchor_edge[j]  index in edges of anchor j.
+
+    Returns (edges, anchors, anchor_edge) as lists."""
+    tz = get_timezone(tz)
+    top, u, iv, _ = _anchor_rule(interval, unit)
+    last = end_ms if cover_ms is None else max(end_ms, cover_ms)
+    anchors = []
+    T = _set_fields(start_ms, tz, top)
+    while T <= last:
+        Tn = _next_top(T, top, tz)
+        # previousInterval(ts) for ts in [T, Tn): T stepped while <= ts and
+        # stepped back once (DateTime.java:600-608): the chain's elements
+        c = T
+        while c < Tn:
+            anchors.append(c)
+            if len(anchors) > max_anchors:
+                raise UnsupportedOperationException(
+                    "calendar grid has too many anchors (> %d)" % max_anchors)
+            c2 = cal_add(c, u, iv, tz)
+            if c2 <= c:
+                raise UnsupportedOperationException(
+                    "calendar step does not advance")
+            c = c2
+        T = Tn
+    anchors = sorted(set(anchors))
+    edges, pos_of = [], {}
+    anchor_edge = []
+    for a in anchors:
+        if a in pos_of:
+            anchor_edge.append(pos_of[a])
+            continue
+        chain = [a]
+        past = 0
+        while past < extra:
+            n = step(chain[-1], interval, unit, tz)
+            if n <= chain[-1]:
+                raise UnsupportedOperationException(
+                    "calendar step does not advance")
+            chain.append(n)
+            if n > last:
+                past += 1
+        base = len(edges)
+        for k, e in enumerate(chain):
+            pos_of.setdefault(e, base + k)
+        edges.extend(chain)
+        edges.append(SENTINEL)
+        if len(edges) > max_edges:
+            raise UnsupportedOperationException(
+                "calendar chains too long (> %d edges)" % max_edges)
+        anchor_edge.append(base)
+    return edges, anchors, anchor_edge
+
+
+def anchored_previous_interval(tables, ts):
+    """previousInterval(ts) on anchored tables: the edge index of the
+    largest anchor <= ts (None before the first)."""
+    edges, anchors, anchor_edge = tables
+    j = bisect.bisect_right(anchors, ts) - 1
+    return None if j < 0 else anchor_edge[j]
+
+
 def bucket_edges_for_series(first_ts, last_ts, interval, unit, tz=None):
     """The grid ONE series follows (anchored at its first point), covering
     its points — what a lone Downsampler over that series steps through."""

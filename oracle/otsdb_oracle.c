@@ -514,12 +514,34 @@ typedef struct {
   int cal;
   const int64_t* edges;
   int64_t n_edges;
+  /* per-series anchors (otsdb_query_spec.cal_anchors): edges holds chains,
+   * each ended by JLONG_MAX, and previousInterval(ts) is the chain edge of
+   * the largest anchor <= ts */
+  const int64_t* anchors;
+  const int64_t* anchor_edge;
+  int64_t n_anchors;
   int64_t prev_cal, next_cal;       /* ValuesInInterval                    */
   int64_t f_prev_cal, f_next_cal;   /* FillingDownsampler                  */
 } ds_view;
 
-/* DateTime.previousInterval(ts) on the table: the edge <= ts. */
+/* DateTime.previousInterval(ts) on the table: the edge <= ts (anchored
+ * tables: the edge of the largest anchor <= ts, whose chain the calendar
+ * then steps). */
 static int64_t cal_prev(ds_view* d, int64_t ts) {
+  if (d->n_anchors > 0) {
+    int64_t lo = 0, hi = d->n_anchors; /* first anchor > ts */
+    while (lo < hi) {
+      int64_t m = lo + (hi - lo) / 2;
+      if (d->anchors[m] <= ts) lo = m + 1; else hi = m;
+    }
+    if (lo == 0)
+      jthrow(d->v.exc, OTSDB_E_UNSUPPORTED,
+             "timestamp %lld before the calendar anchors", (long long)ts);
+    const int64_t k = d->anchor_edge[lo - 1];
+    if (k < 0 || k >= d->n_edges || d->edges[k] != d->anchors[lo - 1])
+      jthrow(d->v.exc, OTSDB_E_ILLEGAL_ARGUMENT, "bad calendar anchor table");
+    return k;
+  }
   int64_t lo = 0, hi = d->n_edges; /* first edge > ts */
   while (lo < hi) {
     int64_t m = lo + (hi - lo) / 2;
@@ -532,12 +554,12 @@ static int64_t cal_prev(ds_view* d, int64_t ts) {
 }
 /* Calendar.add(unit, interval) on an edge index. */
 static int64_t cal_step(ds_view* d, int64_t k) {
-  if (k + 1 >= d->n_edges)
+  if (k + 1 >= d->n_edges || d->edges[k + 1] == JLONG_MAX)
     jthrow(d->v.exc, OTSDB_E_UNSUPPORTED, "calendar table exhausted");
   return k + 1;
 }
 static int64_t cal_ts(ds_view* d, int64_t k) {
-  if (k < 0 || k >= d->n_edges)
+  if (k < 0 || k >= d->n_edges || d->edges[k] == JLONG_MAX)
     jthrow(d->v.exc, OTSDB_E_UNSUPPORTED, "calendar table exhausted");
   return d->edges[k];
 }
@@ -722,6 +744,9 @@ static void ds_init(ds_view* d, view_t* src, const otsdb_query_spec* s,
   d->cal = s->use_calendar && !s->run_all;
   d->edges = s->cal_edges;
   d->n_edges = s->n_cal_edges;
+  d->anchors = s->cal_anchors;
+  d->anchor_edge = s->cal_anchor_edge;
+  d->n_anchors = s->cal_anchors ? s->n_cal_anchors : 0;
   if (d->run_all) d->timestamp_end_interval = d->query_end;
   else if (d->cal) d->timestamp_end_interval = JLONG_MIN;
   else d->timestamp_end_interval = d->interval;

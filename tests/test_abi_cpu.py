@@ -41,7 +41,8 @@ def test_abi_version(lib):
 
 
 def test_struct_sizes_match_header():
-    assert C.sizeof(abi.QuerySpec) == 4 * 8 + 4 * 2 + 8 + 4 * 8 + 8 * 2 + 8 * 2
+    assert C.sizeof(abi.QuerySpec) == (4 * 8 + 4 * 2 + 8 + 4 * 8 + 8 * 2 + 8 * 2
+                                       + 8 * 3)  # calendar anchors
     assert C.sizeof(abi.Batch) == 10 * 8
     assert C.sizeof(abi.Result) == 5 * 8
     assert C.sizeof(abi.Partial) == 32

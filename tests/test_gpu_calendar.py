@@ -45,6 +45,14 @@ CASES = [
     ("1dc-sum-nan", "America/Denver", T_SPRING, 7, 600000),
     ("1dc-sum-zero", "America/Denver", T_FALL, 7, 600000),
     ("6hc-last", "America/Denver", T_SPRING, 4, 300000),
+    # grids anchored at each series' first point (otsdb_query_spec.
+    # cal_anchors): union of the series' own bucket starts
+    ("7mc-sum", None, T_SPRING, 3, 60000),
+    ("7mc-avg", "America/Denver", T_SPRING + 2 * DAY, 3, 45000),
+    ("2wc-max", None, T_SPRING, 45, 3600000),
+    ("6hc-avg", "America/Denver", T_SPRING, 5, 300000),
+    ("6hc-dev", "America/Denver", T_FALL, 5, 300000),
+    ("13mc-p90", "Asia/Kabul", T_SPRING, 2, 60000),
 ]
 
 
@@ -66,7 +74,9 @@ def test_calendar_group_by(engine, ds, tz, t0, days, cad, agg):  # noqa: F811
 
 
 @pytest.mark.parametrize("ds,tz", [("1hc-sum", "Asia/Kabul"),
-                                   ("1dc-sum-zero", "America/Denver")])
+                                   ("1dc-sum-zero", "America/Denver"),
+                                   ("7mc-sum", None),
+                                   ("6hc-max", "America/Denver")])
 def test_calendar_rate(engine, ds, tz):  # noqa: F811
     b = datasets.random_batch(5, n_series=20, n_groups=2, span_ms=5 * DAY,
                               cadence_ms=300000, counter=True, t0=T_SPRING)
@@ -74,3 +84,41 @@ def test_calendar_rate(engine, ds, tz):  # noqa: F811
     spec = _cal_spec("sum", ds, tz, T_SPRING, T_SPRING + 4 * DAY, True, ro,
                      batch=b)
     check(engine, spec, b, False, where=ds)
+
+
+def test_per_series_grids_with_fill_are_unsupported(engine):  # noqa: F811
+    """FillingDownsampler over per-series grids (its own grid is anchored at
+    start, FillingDownsampler.java:113-135, the series' values at their own
+    anchors) stays on the Java iterators: E_UNSUPPORTED, not a result."""
+    b = datasets.random_batch(7, n_series=10, n_groups=1, span_ms=3 * DAY,
+                              cadence_ms=60000, t0=T_SPRING)
+    spec = _cal_spec("sum", "7mc-sum-nan", None, T_SPRING, T_SPRING + 2 * DAY,
+                     batch=b)
+    assert spec.n_cal_anchors > 0
+    with pytest.raises(core.UnsupportedOperationException):
+        engine.run(spec, b)
+
+
+def test_per_series_grids_from_cells(engine):  # noqa: F811
+    """The same per-series grids from compacted cells
+    (otsdb_agg_run_cells_device: decoded, then the anchored pipeline)."""
+    import numpy as np
+    import torch
+    from opentsdb_amd import workload
+    from opentsdb_amd.engine import DeviceResult
+    from oracle import pyoracle
+    from tests.test_gpu_decode import _device_batch, _result_points
+    from tests.test_gpu_parity import compare
+    hb = datasets.random_batch(13, n_series=16, n_groups=2, span_ms=3 * DAY,
+                               cadence_ms=60000, t0=T_SPRING)
+    hb.ts[:] = hb.ts - hb.ts % 1000
+    hb.is_float = np.ones(len(hb.ts), np.uint8)
+    db = _device_batch(hb, "float")
+    cells_d = workload.encode_cells_device(engine, db)
+    spec = _cal_spec("sum", "7mc-avg", None, T_SPRING + 3600000,
+                     T_SPRING + 2 * DAY, batch=hb)
+    assert spec.n_cal_anchors > 0
+    ref = pyoracle.group_by(spec, hb)
+    res = DeviceResult(torch, db.n_groups, 4 * len(hb.ts) + 64, "cuda")
+    workload.run_cells_device(engine, spec, cells_d, db, res)
+    compare(_result_points(res, db.n_groups), ref, False, where="cells/7mc")
