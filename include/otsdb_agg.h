@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OTSDB_ABI_VERSION 2
+#define OTSDB_ABI_VERSION 3
 
 /* ------------------------------------------------------------------------ */
 /* Status codes — 1:1 with the exceptions of the reference path.             */

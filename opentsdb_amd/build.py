@@ -87,14 +87,21 @@ def build(force=False, verbose=False, jobs=None, defines=(), out=None):
     units = _units(out_dir, defines)
     # incremental: a unit is rebuilt when a source it may include is newer
     # than its object (only part-1 units include cellfold.hip)
+    # sources only engine.hip includes (ds_tu.hip's include graph:
+    # kernels.hip, decode.hip, fold.hip, cellfold.hip and the headers)
+    engine_only = ("engine.hip", "select.hip", "raw.hip", "rows.hip",
+                   "calendar.hip")
+
     def stale(u):
         src, extra, obj = u
         if force or not os.path.exists(obj):
             return True
         t = os.path.getmtime(obj)
         part1 = "-DOTSDB_DS_PART=1" in extra
+        ds = src.endswith("ds_tu.hip")
         return any(os.path.getmtime(d) > t for d in DEPS
-                   if part1 or not d.endswith("cellfold.hip"))
+                   if (part1 or not d.endswith("cellfold.hip")) and
+                   not (ds and os.path.basename(d) in engine_only))
 
     todo = [u for u in units if stale(u)]
     with ThreadPoolExecutor(jobs) as ex:

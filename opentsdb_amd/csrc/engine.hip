@@ -12,6 +12,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -179,6 +180,8 @@ struct otsdb_ctx {
   size_t rows_ws_cap = 0;   // and per-series plan arrays
   void* rows_scr = nullptr;  // GENERAL-row cell records + staging / replay arenas
   size_t rows_scr_cap = 0;
+  void* rows_large = nullptr;  // LARGE rows: ranked columns, keys, sort temp
+  size_t rows_large_cap = 0;
   void* raw_cells[2] = {nullptr, nullptr};  // raw-row query: compacted rows,
   size_t raw_cells_cap[2] = {0, 0};          // then the assembled spans
   void* raw_stage = nullptr;  // otsdb_agg_run_raw: host rows staged in HBM
@@ -1475,6 +1478,8 @@ otsdb_status run_cells_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
   rc = ensure(&c->cells_ws, &c->cells_ws_cap, (size_t)(S + 1) * 8 + 64);
   if (rc) return rc;
   int64_t* offs = (int64_t*)c->cells_ws;
+  // the generic decode (its own stage; released before the pipeline)
+  std::unique_ptr<StageTimer> dec_tm(new StageTimer(c, 7));
   rc = decode_impl(c, cells, S, offs, nullptr, nullptr, nullptr, 0, st);
   if (rc) return rc;
   int64_t N = 0;
@@ -1488,6 +1493,7 @@ otsdb_status run_cells_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
   int64_t* vv = (int64_t*)((char*)c->cells_col + col);
   uint8_t* isf = (uint8_t*)((char*)c->cells_col + 2 * col);
   rc = decode_impl(c, cells, S, offs, ts, vv, isf, N, st);
+  dec_tm.reset();
   if (rc) return rc;
   otsdb_batch cb = *b;
   cb.n_points = N;
@@ -1546,6 +1552,85 @@ otsdb_status cells_buffer(otsdb_ctx* c, int which, int64_t R, int64_t qb,
 
 // own >= 0: the output goes to the context's cells buffer `own`, returned in
 // *owned (o is ignored)
+// LARGE rows (rows.hip): rank the columns, record the cells, sort the keys,
+// merge — through global memory, one segment per row
+otsdb_status compact_large(otsdb_ctx* c, const RawDev& D, int fix,
+                           const LargeSlots& LS, int64_t n_large, int64_t NC,
+                           int64_t ncell, const int64_t* gen_base,
+                           const int64_t* gen_n, CellRec* rec, uint8_t* stq,
+                           uint8_t* stv, int64_t* out_q, int64_t* out_v,
+                           unsigned long long* first_err, hipStream_t st) {
+  if (NC >= (int64_t(1) << 32) || ncell >= (int64_t(1) << 32))
+    return fail(OTSDB_E_UNSUPPORTED, "compaction of %lld cells in large rows",
+                (long long)ncell);
+  size_t t_pairs = 0, t_keys = 0;
+  HIP_TRY(rocprim::segmented_radix_sort_pairs(
+      nullptr, t_pairs, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+      (const int64_t*)nullptr, (int64_t*)nullptr, (unsigned)NC,
+      (unsigned)n_large, (const int64_t*)nullptr, (const int64_t*)nullptr, 0,
+      64, st));
+  HIP_TRY(rocprim::segmented_radix_sort_keys(
+      nullptr, t_keys, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+      (unsigned)ncell, (unsigned)n_large, (const int64_t*)nullptr,
+      (const int64_t*)nullptr, 0, 54, st));
+  const size_t t_scan = scan_tmp_bytes(NC, st);
+  const size_t t_sort = std::max(std::max(t_pairs, t_keys), t_scan);
+  uint64_t *ckey, *ckey2, *rkey, *rkey2;
+  int64_t *cidx, *cidx2, *cslot, *ccount, *cbase, *segb, *sege;
+  int* bad;
+  void* tmp;
+  auto carve = [&](char* base) {
+    Carve cv{base};
+    ckey = cv.take<uint64_t>(NC);
+    ckey2 = cv.take<uint64_t>(NC);
+    cidx = cv.take<int64_t>(NC);
+    cidx2 = cv.take<int64_t>(NC);
+    cslot = cv.take<int64_t>(NC);
+    ccount = cv.take<int64_t>(NC + 1);
+    cbase = cv.take<int64_t>(NC + 1);
+    segb = cv.take<int64_t>(n_large);
+    sege = cv.take<int64_t>(n_large);
+    bad = cv.take<int>(n_large);
+    rkey = cv.take<uint64_t>(ncell);
+    rkey2 = cv.take<uint64_t>(ncell);
+    tmp = cv.take<char>(t_sort + 1);
+    return cv.off + 256;
+  };
+  otsdb_status rc = ensure(&c->rows_large, &c->rows_large_cap, carve(nullptr));
+  if (rc) return rc;
+  carve((char*)c->rows_large);
+  hipLaunchKernelGGL(k_large_cols, dim3(blocks_for(n_large, 4)), dim3(256), 0,
+                     st, D, LS, n_large, ckey, cidx, cslot, segb, sege);
+  size_t t = t_sort;
+  HIP_TRY(rocprim::segmented_radix_sort_pairs(
+      tmp, t, (const uint64_t*)ckey, ckey2, (const int64_t*)cidx, cidx2,
+      (unsigned)NC, (unsigned)n_large, (const int64_t*)segb,
+      (const int64_t*)sege, 0, 64, st));
+  HIP_TRY(hipMemsetAsync(ccount + NC, 0, 8, st));
+  const unsigned wblocks = blocks_for((NC + 63) / 64, 4);
+  hipLaunchKernelGGL(k_large_recs, dim3(wblocks), dim3(256), 0, st, D, LS, NC,
+                     (const int64_t*)cidx2, (const int64_t*)cslot, gen_base,
+                     ccount, (const int64_t*)nullptr, rec, rkey, bad, 0);
+  if ((rc = scan_excl(tmp, t_sort, ccount, cbase, NC, st))) return rc;
+  HIP_TRY(hipMemsetAsync(bad, 0, sizeof(int) * n_large, st));
+  hipLaunchKernelGGL(k_large_recs, dim3(wblocks), dim3(256), 0, st, D, LS, NC,
+                     (const int64_t*)cidx2, (const int64_t*)cslot, gen_base,
+                     ccount, (const int64_t*)cbase, rec, rkey, bad, 1);
+  hipLaunchKernelGGL(k_large_segs, dim3(blocks_for(n_large, 256)), dim3(256),
+                     0, st, LS, n_large, gen_base, gen_n, segb, sege);
+  t = t_sort;
+  HIP_TRY(rocprim::segmented_radix_sort_keys(
+      tmp, t, (const uint64_t*)rkey, rkey2, (unsigned)ncell,
+      (unsigned)n_large, (const int64_t*)segb, (const int64_t*)sege, 0, 54,
+      st));
+  hipLaunchKernelGGL(k_large_merge, dim3((unsigned)n_large), dim3(64), 0, st,
+                     D, fix, LS, gen_base, gen_n, (const CellRec*)rec,
+                     (const uint64_t*)rkey2, (const int*)bad, stq, stv, out_q,
+                     out_v, first_err);
+  HIP_TRY(hipGetLastError());
+  return OTSDB_OK;
+}
+
 otsdb_status compact_impl(otsdb_ctx* c, const otsdb_raw_rows* raw, int fix,
                           const otsdb_cells_out* o, int64_t qcap, int64_t vcap,
                           int64_t* n_out, int64_t* qbytes, int64_t* vbytes,
@@ -1561,8 +1646,9 @@ otsdb_status compact_impl(otsdb_ctx* c, const otsdb_raw_rows* raw, int fix,
   const size_t tmpb = scan_tmp_bytes(R, st);
   const size_t A = ((size_t)(R + 1) * 8 + 255) & ~(size_t)255;
   // kind, lone, gen_n, gen_base, out_q, out_v, kept, oq_off, ov_off, k_off,
-  // first_err, scan temp
-  const size_t need = 10 * A + 256 + tmpb;
+  // LARGE slots (row, columns, ranked-column base), first_err, counters,
+  // scan temp
+  const size_t need = 13 * A + 512 + tmpb;
   otsdb_status rc = ensure(&c->rows_ws, &c->rows_ws_cap, need);
   if (rc) return rc;
   char* w = (char*)c->rows_ws;
@@ -1576,19 +1662,25 @@ otsdb_status compact_impl(otsdb_ctx* c, const otsdb_raw_rows* raw, int fix,
   int64_t* oq_off = (int64_t*)(w + 7 * A);
   int64_t* ov_off = (int64_t*)(w + 8 * A);
   int64_t* k_off = (int64_t*)(w + 9 * A);
-  unsigned long long* first_err = (unsigned long long*)(w + 10 * A);
-  void* tmp = w + 10 * A + 256;
+  LargeSlots LS{(unsigned long long*)(w + 13 * A + 256), (int64_t*)(w + 10 * A),
+                (int64_t*)(w + 11 * A), (int64_t*)(w + 12 * A)};
+  unsigned long long* first_err = (unsigned long long*)(w + 13 * A);
+  void* tmp = w + 13 * A + 512;
   HIP_TRY(hipMemsetAsync(first_err, 0xFF, 8, st));
+  HIP_TRY(hipMemsetAsync(LS.ctr, 0, 16, st));
   for (int64_t* a : {gen_n, out_q, out_v, kept})
     HIP_TRY(hipMemsetAsync(a + R, 0, 8, st));
   if (R > 0)
     hipLaunchKernelGGL(k_rows_plan, dim3(blocks_for(R, 4)), dim3(256), 0, st,
-                       D, fix, kind, lone, gen_n, out_q, out_v, kept, first_err);
+                       D, fix, kind, lone, gen_n, out_q, out_v, kept, first_err,
+                       LS);
   HIP_TRY(hipGetLastError());
   if ((rc = scan_excl(tmp, tmpb, gen_n, gen_base, R, st))) return rc;
   HIP_TRY(hipMemcpyAsync(&c->h_small[0], gen_base + R, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_small[5], LS.ctr, 16, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
   const int64_t ncell = c->h_small[0];
+  const int64_t n_large = c->h_small[5], NC = c->h_small[6];
   if (ncell > 0) {
     const size_t recb = ((size_t)ncell * sizeof(CellRec) + 255) & ~(size_t)255;
     const size_t qb = ((size_t)ncell * 4 + 255) & ~(size_t)255;
@@ -1601,6 +1693,10 @@ otsdb_status compact_impl(otsdb_ctx* c, const otsdb_raw_rows* raw, int fix,
                        (const uint8_t*)kind, (const int64_t*)gen_base, rec, stq,
                        stv, out_q, out_v, first_err);
     HIP_TRY(hipGetLastError());
+    if (n_large > 0 &&
+        (rc = compact_large(c, D, fix, LS, n_large, NC, ncell, gen_base, gen_n,
+                            rec, stq, stv, out_q, out_v, first_err, st)))
+      return rc;
   }
   HIP_TRY(hipMemcpyAsync(&c->h_small[1], first_err, 8, hipMemcpyDeviceToHost, st));
   if ((rc = scan_excl(tmp, tmpb, out_q, oq_off, R, st))) return rc;
@@ -1777,16 +1873,22 @@ otsdb_status run_raw_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
   if (!raw->row_series) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null row_series");
   int64_t nk = 0, tq = 0, tv = 0;
   otsdb_cells_out co;
-  otsdb_status rc =
-      compact_impl(c, raw, fix, nullptr, 0, 0, &nk, &tq, &tv, st, 0, &co);
+  otsdb_status rc;
+  {
+    StageTimer tm(c, 5);  // query-time compaction
+    rc = compact_impl(c, raw, fix, nullptr, 0, 0, &nk, &tq, &tv, st, 0, &co);
+  }
   if (rc) return rc;
   otsdb_cells cc{nk, co.row_series, co.row_base_s, co.qual_off, co.qual,
                  co.val_off, co.val};
   int64_t ns = 0, sq = 0, sv = 0;
   bool identity = true;
   otsdb_cells_out so;
-  rc = span_impl(c, &cc, b->n_series, nullptr, 0, 0, &ns, &sq, &sv, &identity,
-                 st, 1, &so);
+  {
+    StageTimer tm(c, 6);  // span assembly
+    rc = span_impl(c, &cc, b->n_series, nullptr, 0, 0, &ns, &sq, &sv,
+                   &identity, st, 1, &so);
+  }
   if (rc) return rc;
   if (!identity)
     cc = otsdb_cells{ns, so.row_series, so.row_base_s, so.qual_off, so.qual,
@@ -1839,6 +1941,7 @@ void otsdb_ctx_destroy(otsdb_ctx* c) {
   if (c->cells_col) hipFree(c->cells_col);
   if (c->rows_ws) hipFree(c->rows_ws);
   if (c->rows_scr) hipFree(c->rows_scr);
+  if (c->rows_large) hipFree(c->rows_large);
   for (void* p : c->raw_cells)
     if (p) hipFree(p);
   if (c->raw_stage) hipFree(c->raw_stage);

@@ -80,7 +80,9 @@ struct RawDev {
 
 // row status codes (otsdb_status values)
 enum : int { RS_ILLEGAL_DATA = 1, RS_ILLEGAL_ARGUMENT = 3, RS_UNSUPPORTED = 5 };
-enum : uint8_t { RK_EMPTY = 0, RK_VERBATIM = 1, RK_LONE = 2, RK_GENERAL = 3 };
+enum : uint8_t {
+  RK_EMPTY = 0, RK_VERBATIM = 1, RK_LONE = 2, RK_GENERAL = 3, RK_LARGE = 4
+};
 // column types
 enum : int { CT_SKIP = 0, CT_APPEND = 1, CT_ONE = 2, CT_MULTI = 3 };
 
@@ -101,6 +103,15 @@ struct CellRec {
 };
 enum : uint8_t {
   RF_QFIX = 1, RF_QINVAL = 2, RF_MS = 4, RF_APPEND = 8, RF_OVERRUN = 16
+};
+
+// LARGE rows (past kRowCellCap cells or kRowColCap data columns): one slot
+// each, claimed by k_rows_plan
+struct LargeSlots {
+  unsigned long long* ctr;  // [0] slots, [1] ranked columns
+  int64_t* row;             // slot -> row
+  int64_t* ncol;            // its data columns
+  int64_t* cbase;           // its first ranked-column position
 };
 
 DEV void row_error(unsigned long long* first_err, int64_t r, int code) {
@@ -416,7 +427,7 @@ __global__ __launch_bounds__(256) void k_rows_plan(
     RawDev D, int fix, uint8_t* __restrict__ kind, int64_t* __restrict__ lone,
     int64_t* __restrict__ gen_n, int64_t* __restrict__ out_q,
     int64_t* __restrict__ out_v, int64_t* __restrict__ kept,
-    unsigned long long* first_err) {
+    unsigned long long* first_err, LargeSlots LS) {
   const int lane = LANE;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= D.R) return;
@@ -500,8 +511,16 @@ __global__ __launch_bounds__(256) void k_rows_plan(
     return;
   }
   if (cells > kRowCellCap || n_data > kRowColCap) {
-    if (lane == 0) row_error(first_err, r, RS_UNSUPPORTED);
-    put(RK_EMPTY, 0, 0, 0);
+    // past the LDS caps: the global-memory merge (k_large_*); a slot, its
+    // ranked-column range (slots and ranges in claim order: the layout may
+    // vary, the merged rows do not)
+    if (lane == 0) {
+      const unsigned long long sl = atomicAdd(&LS.ctr[0], 1ULL);
+      LS.row[sl] = r;
+      LS.ncol[sl] = n_data;
+      LS.cbase[sl] = (int64_t)atomicAdd(&LS.ctr[1], (unsigned long long)n_data);
+    }
+    put(RK_LARGE, 0, 0, cells);
     return;
   }
   put(RK_GENERAL, 0, 0, cells);
@@ -528,6 +547,91 @@ DEV void write_cell(const RawDev& D, const CellRec& x, uint8_t* dq,
   for (int i = 0; i < x.ql; ++i)
     dq[i] = (i == 1 && (x.flags & RF_QFIX)) ? x.qfix : qs[x.qpos + i];
   for (int i = 0; i < x.vl; ++i) dv[i] = D.val[x.vpos + i];
+}
+
+// The heap order over keys sorted by (offset, rank-order record index)
+// (defaultMergeDataPoints, CompactionQueue.java:549-584): the first cell of
+// each offset is kept and written to the staging area, later ones are
+// duplicates compared with it (IllegalDataException unless fix_duplicates);
+// an append column's TreeMap-replaced pair is never popped.  keys: LDS
+// (GENERAL rows) or global memory (LARGE rows).
+DEV void merge_sorted(const RawDev& D, int fix, const CellRec* R, int64_t n,
+                      const uint64_t* keys, uint8_t* sq, uint8_t* sv,
+                      int64_t& nq, int64_t& nv, int64_t& nk, int& ms_in,
+                      int& s_in, int& bad) {
+  const int lane = LANE;
+  int64_t lvpos = 0;
+  int lvl = 0, lvav = 0;
+  for (int64_t p0 = 0; p0 < n; p0 += 64) {
+    const int64_t p = p0 + lane;
+    const bool in = p < n;
+    CellRec x{};
+    bool lead = false, dup = false;
+    if (in) {
+      const uint64_t key = keys[p];
+      x = R[(uint32_t)key];
+      if (p == 0 || (keys[p - 1] >> 32) != (key >> 32)) {
+        lead = true;
+      } else {
+        const CellRec& y = R[(uint32_t)keys[p - 1]];
+        // a pair an append column's TreeMap replaced: never popped
+        dup = !((x.flags & RF_APPEND) && y.col == x.col);
+      }
+    }
+    const uint64_t lm = __ballot(lead);
+    const int ll = lane_last_le(lm, lane);
+    int64_t rvpos = __shfl(x.vpos, ll < 0 ? 0 : ll);
+    int rvl = __shfl((int)x.vl, ll < 0 ? 0 : ll);
+    int rvav = __shfl((int)x.vav, ll < 0 ? 0 : ll);
+    if (ll < 0) {
+      rvpos = lvpos;
+      rvl = lvl;
+      rvav = lvav;
+    }
+    if (dup && !fix &&
+        !bytes_equal_padded(D.val, x.vpos, x.vl, x.vav, rvpos, rvl, rvav))
+      bad = 1;
+    if (lead && (x.flags & RF_OVERRUN)) bad = 1;
+    const int64_t kq = lead ? x.ql : 0, kv = lead ? x.vl : 0;
+    const int64_t iq = wave_incl_scan(kq), iv = wave_incl_scan(kv);
+    if (lead && !bad) write_cell(D, x, sq + nq + iq - kq, sv + nv + iv - kv);
+    ms_in |= __ballot(lead && (x.flags & RF_MS)) != 0;
+    s_in |= __ballot(lead && !(x.flags & RF_MS)) != 0;
+    nq += __shfl(iq, 63);
+    nv += __shfl(iv, 63);
+    nk += __popcll(lm);
+    if (lm) {
+      const int last = 63 - __builtin_clzll(lm);
+      lvpos = __shfl(x.vpos, last);
+      lvl = __shfl((int)x.vl, last);
+      lvav = __shfl((int)x.vav, last);
+    }
+    if (__ballot(bad)) break;
+  }
+}
+
+// buildCompactedColumn (CompactionQueue.java:594-616): the meta byte of a
+// multi-value column, the row's output sizes (or its error)
+DEV void finish_row(int64_t r, int bad, int64_t nq, int64_t nv, int64_t nk,
+                    int ms_in, int s_in, uint8_t* sv, int64_t* out_q,
+                    int64_t* out_v, unsigned long long* first_err) {
+  const int lane = LANE;
+  if (__ballot(bad)) {
+    if (lane == 0) {
+      row_error(first_err, r, RS_ILLEGAL_DATA);
+      out_q[r] = 0;
+      out_v[r] = 0;
+    }
+    return;
+  }
+  if (nk > 1) {
+    if (lane == 0) sv[nv] = (ms_in && s_in) ? 1 : 0;
+    nv += 1;
+  }
+  if (lane == 0) {
+    out_q[r] = nq;
+    out_v[r] = nv;
+  }
 }
 
 __global__ __launch_bounds__(64) void k_rows_general(
@@ -764,54 +868,7 @@ __global__ __launch_bounds__(64) void k_rows_general(
         }
         wave_sync();
       }
-    int64_t lvpos = 0;
-    int lvl = 0, lvav = 0;
-    for (int p0 = 0; p0 < n; p0 += 64) {
-      const int p = p0 + lane;
-      const bool in = p < n;
-      CellRec x{};
-      bool lead = false, dup = false;
-      if (in) {
-        const uint64_t key = sm.keys[p];
-        x = R[(uint32_t)key];
-        if (p == 0 || (sm.keys[p - 1] >> 32) != (key >> 32)) {
-          lead = true;
-        } else {
-          const CellRec& y = R[(uint32_t)sm.keys[p - 1]];
-          // a pair an append column's TreeMap replaced: never popped
-          dup = !((x.flags & RF_APPEND) && y.col == x.col);
-        }
-      }
-      const uint64_t lm = __ballot(lead);
-      const int ll = lane_last_le(lm, lane);
-      int64_t rvpos = __shfl(x.vpos, ll < 0 ? 0 : ll);
-      int rvl = __shfl((int)x.vl, ll < 0 ? 0 : ll);
-      int rvav = __shfl((int)x.vav, ll < 0 ? 0 : ll);
-      if (ll < 0) {
-        rvpos = lvpos;
-        rvl = lvl;
-        rvav = lvav;
-      }
-      if (dup && !fix &&
-          !bytes_equal_padded(D.val, x.vpos, x.vl, x.vav, rvpos, rvl, rvav))
-        bad = 1;
-      if (lead && (x.flags & RF_OVERRUN)) bad = 1;
-      const int64_t kq = lead ? x.ql : 0, kv = lead ? x.vl : 0;
-      const int64_t iq = wave_incl_scan(kq), iv = wave_incl_scan(kv);
-      if (lead && !bad) write_cell(D, x, sq + nq + iq - kq, sv + nv + iv - kv);
-      ms_in |= __ballot(lead && (x.flags & RF_MS)) != 0;
-      s_in |= __ballot(lead && !(x.flags & RF_MS)) != 0;
-      nq += __shfl(iq, 63);
-      nv += __shfl(iv, 63);
-      nk += __popcll(lm);
-      if (lm) {
-        const int last = 63 - __builtin_clzll(lm);
-        lvpos = __shfl(x.vpos, last);
-        lvl = __shfl((int)x.vl, last);
-        lvav = __shfl((int)x.vav, last);
-      }
-      if (__ballot(bad)) break;
-    }
+    merge_sorted(D, fix, R, n, sm.keys, sq, sv, nq, nv, nk, ms_in, s_in, bad);
   } else if (has_append) {
     // not reached by the write path or compaction: appended pairs next to a
     // compacted column whose offsets go back in time
@@ -888,22 +945,245 @@ __global__ __launch_bounds__(64) void k_rows_general(
     s_in = __builtin_amdgcn_readfirstlane(s_in);
     bad = __builtin_amdgcn_readfirstlane(bad);
   }
-  if (__ballot(bad)) {
+  finish_row(r, bad, nq, nv, nk, ms_in, s_in, sv, out_q, out_v, first_err);
+}
+
+// ------------------------------------------------------------- LARGE rows
+// A row past the LDS caps (an hour of millisecond points written as single
+// cells is up to 3.6 M columns) runs the same merge through global memory:
+//   k_large_cols    its data columns, index order reversed, keyed by the
+//                   HBase timestamp (descending) -> a stable segmented radix
+//                   sort gives the rank order (newer cell first, then the
+//                   later column: ColumnDatapointIterator.compareTo);
+//   k_large_count   cells per ranked column (multi-point columns walked);
+//                   an exclusive scan gives each column's record base;
+//   k_large_recs    the cell records in rank order and their keys
+//                   (offset << 32 | record index);
+//   segmented radix sort of the keys = the heap order;
+//   k_large_merge   merge_sorted + finish_row, one wavefront per row.
+// A LARGE row holding a column whose cells go back in time (never written by
+// the write path or compaction) is OTSDB_E_UNSUPPORTED.
+struct LargeWs {
+  LargeSlots LS;
+  uint64_t* ckey;     // [NC] rank keys
+  int64_t* cidx;      // [NC] column index (sorted alongside)
+  int64_t* cslot;     // [NC] slot of each ranked position
+  int64_t* ccount;    // [NC + 1] cells per ranked column
+  int64_t* cbase;     // [NC + 1] exclusive scan of ccount
+  int* bad;           // [slots] unsorted columns seen
+};
+
+__global__ __launch_bounds__(256) void k_large_cols(
+    RawDev D, LargeSlots LS, int64_t n_slots, uint64_t* __restrict__ ckey,
+    int64_t* __restrict__ cidx, int64_t* __restrict__ cslot,
+    int64_t* __restrict__ segb, int64_t* __restrict__ sege) {
+  const int lane = LANE;
+  const int64_t sl = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (sl >= n_slots) return;
+  const int64_t r = LS.row[sl], nc = LS.ncol[sl], cb = LS.cbase[sl];
+  const int64_t c0 = D.row_col_off[r], c1 = D.row_col_off[r + 1];
+  if (lane == 0) {
+    segb[sl] = cb;
+    sege[sl] = cb + nc;
+  }
+  int64_t k = 0;
+  for (int64_t cc = c0; cc < c1; cc += 64) {
+    const int64_t c = cc + lane;
+    ColInfo ci{CT_SKIP, 0, 0, 0};
+    if (c < c1) ci = col_info(D, c);
+    const uint64_t dm = __ballot(ci.type != CT_SKIP);
+    if (ci.type != CT_SKIP) {
+      const int64_t kk = k + __popcll(dm & ((1ULL << lane) - 1));
+      const int64_t pos = cb + (nc - 1 - kk);  // index order reversed
+      const int64_t ts = D.col_ts ? D.col_ts[c] : c;
+      // ascending key = descending timestamp (signed order)
+      ckey[pos] = ~((uint64_t)ts ^ 0x8000000000000000ULL);
+      cidx[pos] = c;
+      cslot[pos] = sl;
+    }
+    k += __popcll(dm);
+  }
+}
+
+// Cells of ranked columns [w*64, w*64+64) (mode 0: count; mode 1: write
+// the records and keys at the scanned bases)
+__global__ __launch_bounds__(256) void k_large_recs(
+    RawDev D, LargeSlots LS, int64_t NC, const int64_t* __restrict__ cidx,
+    const int64_t* __restrict__ cslot, const int64_t* __restrict__ gen_base,
+    int64_t* __restrict__ ccount, const int64_t* __restrict__ cbase,
+    CellRec* __restrict__ rec, uint64_t* __restrict__ rkey,
+    int* __restrict__ bad, int mode) {
+  const int lane = LANE;
+  const int64_t p0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+  if (p0 >= NC) return;
+  const int64_t pos = p0 + lane;
+  const bool in = pos < NC;
+  int64_t c = 0, sl = 0, rbase = 0, rank = 0, base_in_row = 0;
+  int type = CT_SKIP;
+  ColInfo ci{CT_SKIP, 0, 0, 0};
+  if (in) {
+    c = cidx[pos];
+    sl = cslot[pos];
+    ci = col_info(D, c);
+    type = ci.type;
+    rank = pos - LS.cbase[sl];
+    if (mode) {
+      rbase = gen_base[LS.row[sl]];
+      base_in_row = cbase[pos] - cbase[LS.cbase[sl]];
+    }
+  }
+  auto key_of = [](int32_t off, int64_t i) {
+    return ((uint64_t)(uint32_t)off << 32) | (uint64_t)(uint32_t)i;
+  };
+  if (type == CT_ONE || type == CT_APPEND) {
+    if (!mode) ccount[pos] = ci.cells;
+  }
+  if (mode && type == CT_ONE) {
+    const int64_t qb = D.col_qoff[c], ql = D.col_qoff[c + 1] - qb;
+    const int64_t vb = D.col_voff[c], vl = D.col_voff[c + 1] - vb;
+    CellRec x;
+    x.col = (int32_t)rank;
+    x.qpos = qb;
+    x.ql = (uint8_t)ql;
+    if (ql == 2) {
+      int vskip, bd;
+      const uint8_t nf = fixup2(D.qual[qb + 1], D.val + vb, vl, vskip, bd);
+      const int cur = (nf & 0x7) + 1;
+      x.flags = RF_QFIX;
+      x.qfix = nf;
+      x.vpos = vb + vskip;
+      x.vl = (uint8_t)cur;
+      x.vav = (uint8_t)(cur <= vl - vskip ? cur : vl - vskip);
+      if (cur > vl - vskip) x.flags |= RF_OVERRUN;
+      x.off = (int32_t)((((uint32_t)D.qual[qb] << 8) | nf) >> 4) * 1000;
+    } else {
+      const uint32_t qv = ((uint32_t)D.qual[qb] << 24) |
+                          ((uint32_t)D.qual[qb + 1] << 16) |
+                          ((uint32_t)D.qual[qb + 2] << 8) | D.qual[qb + 3];
+      const int cur = (int)(qv & 0x7) + 1;
+      x.flags = RF_MS;
+      x.qfix = 0;
+      x.vpos = vb;
+      x.vl = (uint8_t)cur;
+      x.vav = (uint8_t)(cur <= vl ? cur : vl);
+      if (cur > vl) x.flags |= RF_OVERRUN;
+      x.off = qual_off_ms(qv, 1);
+    }
+    rec[rbase + base_in_row] = x;
+    rkey[rbase + base_in_row] = key_of(x.off, base_in_row);
+  }
+  uint64_t om = __ballot(type == CT_MULTI || (mode && type == CT_APPEND));
+  while (om) {
+    const int b = __builtin_ctzll(om);
+    om &= om - 1;
+    const int64_t cb = __shfl(c, b);
+    const int64_t rb = __shfl(rbase, b), bir = __shfl(base_in_row, b);
+    const int64_t rk = __shfl(rank, b), bsl = __shfl(sl, b);
+    const int btype = __shfl(type, b);
+    const int64_t qb = D.col_qoff[cb], vb = D.col_voff[cb];
+    const int64_t ql = D.col_qoff[cb + 1] - qb, vl = D.col_voff[cb + 1] - vb;
+    if (btype == CT_APPEND) {  // lane 0 walks the pairs (reverse arrival)
+      if (lane == 0) {
+        const int64_t np = cbase[p0 + b + 1] - cbase[p0 + b];
+        int64_t p = 0;
+        for (int64_t j = 0; j < np; ++j) {
+          const uint8_t* e = D.val + vb + p;
+          const int eql = (e[0] & 0xF0) == 0xF0 ? 4 : 2;
+          uint32_t qv = 0;
+          for (int t = 0; t < eql; ++t) qv = (qv << 8) | e[t];
+          const int cur = (int)(qv & 0x7) + 1;
+          CellRec x;
+          x.qpos = vb + p;
+          x.vpos = vb + p + eql;
+          x.off = qual_off_ms(qv, eql == 4);
+          x.col = (int32_t)rk;
+          x.ql = (uint8_t)eql;
+          x.vl = x.vav = (uint8_t)cur;
+          x.flags = RF_QINVAL | RF_APPEND | (eql == 4 ? RF_MS : 0);
+          x.qfix = 0;
+          const int64_t i = bir + np - 1 - j;
+          rec[rb + i] = x;
+          rkey[rb + i] = key_of(x.off, i);
+          p += eql + cur;
+        }
+      }
+      continue;
+    }
+    ColWalk w(D.qual + qb, ql, vl);
+    int64_t n = 0;
+    bool hp = false;
+    int32_t prev = 0;
+    int unsorted = 0;
+    while (w.step()) {
+      if (mode) {
+        const int pl = lane_prev(w.mask, lane);
+        int32_t po = __shfl(w.off, pl < 0 ? 0 : pl);
+        const bool have = pl >= 0 || hp;
+        if (pl < 0) po = prev;
+        if (__ballot(w.cell && have && w.off < po)) unsorted = 1;
+        if (w.cell) {
+          CellRec x;
+          x.qpos = qb + w.qo;
+          x.vpos = vb + w.vo;
+          x.off = w.off;
+          x.col = (int32_t)rk;
+          x.ql = (uint8_t)w.ql;
+          x.vl = (uint8_t)w.vl;
+          x.vav = (uint8_t)(w.vo + w.vl <= vl ? w.vl : vl - w.vo);
+          x.flags = (w.ms ? RF_MS : 0) | (w.vo + w.vl > vl ? RF_OVERRUN : 0);
+          x.qfix = 0;
+          rec[rb + bir + w.k] = x;
+          rkey[rb + bir + w.k] = key_of(x.off, bir + w.k);
+        }
+        if (w.mask) {
+          prev = __shfl(w.off, 63 - __builtin_clzll(w.mask));
+          hp = true;
+        }
+      }
+      n += __popcll(w.mask);
+    }
+    if (!mode && lane == 0) ccount[p0 + b] = n;
+    if (mode && unsorted && lane == 0) atomicOr(&bad[bsl], 1);
+  }
+}
+
+__global__ void k_large_segs(LargeSlots LS, int64_t n_slots,
+                             const int64_t* __restrict__ gen_base,
+                             const int64_t* __restrict__ gen_n,
+                             int64_t* __restrict__ segb,
+                             int64_t* __restrict__ sege) {
+  const int64_t sl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (sl >= n_slots) return;
+  const int64_t r = LS.row[sl];
+  segb[sl] = gen_base[r];
+  sege[sl] = gen_base[r] + gen_n[r];
+}
+
+__global__ __launch_bounds__(64) void k_large_merge(
+    RawDev D, int fix, LargeSlots LS, const int64_t* __restrict__ gen_base,
+    const int64_t* __restrict__ gen_n, const CellRec* __restrict__ rec,
+    const uint64_t* __restrict__ rkey, const int* __restrict__ bad_in,
+    uint8_t* __restrict__ stq, uint8_t* __restrict__ stv,
+    int64_t* __restrict__ out_q, int64_t* __restrict__ out_v,
+    unsigned long long* first_err) {
+  const int lane = LANE;
+  const int64_t sl = blockIdx.x;
+  const int64_t r = LS.row[sl];
+  const int64_t gb = gen_base[r], n = gen_n[r];
+  if (bad_in[sl]) {
     if (lane == 0) {
-      row_error(first_err, r, RS_ILLEGAL_DATA);
+      row_error(first_err, r, RS_UNSUPPORTED);
       out_q[r] = 0;
       out_v[r] = 0;
     }
     return;
   }
-  if (nk > 1) {
-    if (lane == 0) sv[nv] = (ms_in && s_in) ? 1 : 0;
-    nv += 1;
-  }
-  if (lane == 0) {
-    out_q[r] = nq;
-    out_v[r] = nv;
-  }
+  int64_t nq = 0, nv = 0, nk = 0;
+  int ms_in = 0, s_in = 0, bad = 0;
+  merge_sorted(D, fix, rec + gb, n, rkey + gb, stq + 4 * gb, stv + 9 * gb, nq,
+               nv, nk, ms_in, s_in, bad);
+  finish_row(r, bad, nq, nv, nk, ms_in, s_in, stv + 9 * gb, out_q, out_v,
+             first_err);
 }
 
 // ------------------------------------------------------------------ pack

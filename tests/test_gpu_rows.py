@@ -153,12 +153,82 @@ def test_compaction_uncompacted_hour(engine):
     assert got == [(0, rows_fuzz.BASE, q, v)]
 
 
-def test_compaction_unsupported_beyond_caps(engine):
-    """More than 8192 points to merge in one row: UnsupportedOperation (the
-    caller keeps the reference's compaction for that row)."""
+def test_compaction_large_ms_row(engine):
+    """An hour of millisecond points written as single cells (100,000
+    columns, past the LDS caps: the global-memory merge of rows.hip), with
+    repeats under newer and older HBase timestamps, next to ordinary rows in
+    the same call: bit-exact with or_compact_row."""
+    rng = np.random.default_rng(61)
+    offs = np.sort(rng.choice(3600 * 1000, size=100000, replace=False))
+    pts = [rows_fuzz.cell(rng, int(o), True) for o in offs]
+    cols = [(q, v, int(t)) for (q, v), t in
+            zip(pts, rng.integers(0, 1 << 40, size=len(pts)))]
+    for k in rng.integers(0, len(pts), size=300):  # equal-byte repeats
+        cols.append((pts[k][0], pts[k][1], int(rng.integers(0, 1 << 40))))
+    order = rng.permutation(len(cols))
+    big = [cols[i] for i in order]
+    small = rows_fuzz.random_row(np.random.default_rng(62))
+    while rows_fuzz.heap_with_append(small):
+        small = rows_fuzz.random_row(np.random.default_rng(63))
+    # a 12,000-column row the oracle merges in seconds
+    mid = [c for c in big if (int.from_bytes(c[0], "big") >> 6) % 9 == 0][:12000]
+    rows = [(0, rows_fuzz.BASE, small), (1, rows_fuzz.BASE, big),
+            (2, rows_fuzz.BASE + 3600, small), (3, rows_fuzz.BASE, mid)]
+    got = _gpu_compact(engine, rows)
+    ref = _oracle_rows([rows[0], rows[2], rows[3]], True)
+    assert len(got) == 4
+    assert [got[0], got[2], got[3]] == ref
+    # the 100,000-point row: every offset once, in time order, the repeats
+    # (equal bytes) dropped (CompactionQueue.java:549-584); the oracle's heap
+    # takes ~40 s on it, so the expectation is the column it must build
+    q, v = rows_fuzz.compacted(pts)
+    assert got[1] == (1, rows_fuzz.BASE, q, v)
+
+
+def test_compaction_large_merged_columns(engine):
+    """Two compacted columns of 5,000 ms points each (10,000 cells to
+    merge) plus an append column and second-resolution cells: the large-row
+    merge keeps the heap order (newer column first on equal offsets) and the
+    mixed-resolution meta byte, bit-exact with the oracle; fix_duplicates
+    off raises IllegalDataException on a differing duplicate."""
     rng = np.random.default_rng(6)
-    a = rows_fuzz.compacted([rows_fuzz.cell(rng, k, True) for k in range(5000)])
-    b = rows_fuzz.compacted([rows_fuzz.cell(rng, k, True) for k in range(5000)])
+    a = rows_fuzz.compacted([rows_fuzz.cell(rng, 2 * k, True)
+                             for k in range(5000)])
+    b = rows_fuzz.compacted([rows_fuzz.cell(rng, 2 * k + 1, True)
+                             for k in range(5000)])
+    app = b"".join(q + v for q, v in [rows_fuzz.cell(rng, 20000 + 7 * k, True)
+                                      for k in range(40)])
+    sec = [rows_fuzz.cell(rng, 1000 * k, False) for k in range(30, 60)]
+    cols = [a + (3,), b + (1,), (bytes([5, 0, 0]), app, 2)]
+    cols += [(q, v, 9) for q, v in sec]
+    rows = [(0, rows_fuzz.BASE, cols)]
+    got = _gpu_compact(engine, rows)
+    assert got == _oracle_rows(rows, True)
+    # a repeated offset with different bytes
+    dup = rows_fuzz.cell(rng, 4, True, value=(0x7, b"\0" * 7 + b"\x05"))
+    cols2 = cols + [(dup[0], dup[1], 99)]
+    try:
+        ref = _oracle_rows([(0, rows_fuzz.BASE, cols2)], False)
+        err = None
+    except pyoracle.OracleError as e:
+        err = e.status
+    if err is None:
+        assert _gpu_compact(engine, [(0, rows_fuzz.BASE, cols2)], fix=False) == ref
+    else:
+        with pytest.raises(STATUS_EXC[err]):
+            _gpu_compact(engine, [(0, rows_fuzz.BASE, cols2)], fix=False)
+
+
+def test_compaction_large_row_out_of_order_is_unsupported(engine):
+    """A large row holding a compacted column whose offsets go back in time
+    (never written by the write path or compaction): UnsupportedOperation,
+    the caller keeps the reference's compaction for that row."""
+    rng = np.random.default_rng(7)
+    offs = list(range(0, 20000, 2))
+    offs[10], offs[11] = offs[11], offs[10]
+    a = rows_fuzz.compacted([rows_fuzz.cell(rng, o, True) for o in offs])
+    b = rows_fuzz.compacted([rows_fuzz.cell(rng, o + 1, True)
+                             for o in range(0, 20000, 2)])
     with pytest.raises(core.UnsupportedOperationException):
         _gpu_compact(engine, [(0, rows_fuzz.BASE, [a + (0,), b + (1,)])])
 
