@@ -99,14 +99,21 @@ def timed_reps(fn, warm, reps):
     return statistics.median(ts), sum(ts) / len(ts)
 
 
-def stage_reader(eng):
+# otsdb_prof_* stages: 0 downsample / fold, 1 transform, 2 group /
+# selection, 3 prep, 4 compact, 5 query-time row compaction, 6 span
+# assembly, 7 the generic cells decode
+STAGES = ("downsample", "transform", "group", "prep", "compact",
+          "row_compaction", "span_assembly", "cells_decode")
+
+
+def stage_reader(eng, all_stages=False):
     import ctypes as C
 
     def read(reset=True):
         ms = (C.c_double * 8)()
         n = (C.c_int64 * 8)()
         eng.lib.otsdb_prof_read(eng.ctx, ms, n, 8, 1 if reset else 0)
-        return [ms[i] / max(n[i], 1) for i in range(5)]
+        return [ms[i] / max(n[i], 1) for i in range(8 if all_stages else 5)]
     return read
 
 
@@ -273,8 +280,31 @@ def decode_figure(eng, config, n_series, reps=5):
     dq, _ = timed_reps(
         lambda: workload.run_cells_device(eng, spec, cells, db, res), 1, reps)
     kb = read()[0] / 1e3
+    # the same query from storage rows (otsdb_agg_run_raw_device): every
+    # compacted row as the scanner returns it, through query-time compaction
+    # (verbatim rows: copied), span assembly and the cells fold
+    from opentsdb_amd import storage
+    raw = storage.raw_rows_from_cells(cells)
+    read_all = stage_reader(eng, all_stages=True)
+    read_all()
+    dr, _ = timed_reps(
+        lambda: storage.run_raw_device(eng, spec, raw, db, res), 1, reps)
+    st_raw = read_all()
     eng.lib.otsdb_prof_enable(eng.ctx, 0)
-    del cells, res, db
+    del raw, cells
+    torch.cuda.empty_cache()
+    storage_fig = {
+        "what": "the same C2 query from storage rows (otsdb_agg_run_raw_device"
+                "): query-time compaction, span assembly, the cells fold",
+        "value": n / dr, "unit": "data points/s", "ms_per_query": dr * 1e3,
+        "stage_ms": {k: v for k, v in zip(STAGES, st_raw) if v},
+        "kernels": "k_rows_plan + k_rows_write (compaction), k_span_plan "
+                   "(assembly), k_cells_prep + k_fold<cells>"}
+    fold_ms = st_raw[0]
+    if fold_ms:
+        storage_fig["fold_frac_of_8TBs"] = cb / (fold_ms / 1e3) / 8e12
+    mixed = mixed_cells_figure(eng, config, n_series, db, res, reps)
+    del res, db
     torch.cuda.empty_cache()
     return {"kernel": "k_decode (count + scan + write)",
             "points": n, "ms": dt * 1e3, "value": n / dt,
@@ -291,7 +321,52 @@ def decode_figure(eng, config, n_series, reps=5):
                 "ms_per_query": dq * 1e3,
                 "kernel_ms": kb * 1e3,
                 "achieved_GBs_compacted": cb / kb / 1e9 if kb else None,
-                "frac_of_8TBs": cb / kb / 8e12 if kb else None}}
+                "frac_of_8TBs": cb / kb / 8e12 if kb else None},
+            "storage_rows": storage_fig,
+            "mixed_resolution_cells": mixed}
+
+
+def mixed_cells_figure(eng, config, n_series, db_groups, res, reps):
+    """The same query over points half on whole seconds, half on
+    milliseconds: the encoder writes 2-byte and 4-byte qualifiers, so every
+    storage row mixes both (MS_MIXED_COMPACT, RowSeq.java:338-356): the
+    fused cells fold does not take such columns, the generic decode does
+    (k_decode into columns, then the columnar fold)."""
+    import torch
+    from opentsdb_amd import workload
+    g = workload.gen_spec(config)
+    g.flags = 0
+    db = workload.generate_device(eng, g, 0, n_series, config=config)
+    n = db.n_points_total
+    # every other point on a whole second (10 s cadence: order kept): the
+    # encoder gives those 2-byte qualifiers, the rest 4-byte ms ones
+    even = db.ts[0::2]
+    even -= torch.remainder(even, 1000)
+    cells = workload.encode_cells_device(eng, db)
+    del db, even
+    torch.cuda.empty_cache()
+    spec = workload.query_spec(config)
+    read = stage_reader(eng, all_stages=True)
+    eng.lib.otsdb_prof_enable(eng.ctx, 1)
+    read()
+    dq, _ = timed_reps(
+        lambda: workload.run_cells_device(eng, spec, cells, db_groups, res), 1,
+        reps)
+    st = read()
+    eng.lib.otsdb_prof_enable(eng.ctx, 0)
+    cb = cells.n_bytes
+    del cells
+    torch.cuda.empty_cache()
+    out = {"what": "the C2 query over ms-stamped points from compacted cells "
+                   "whose rows mix 2- and 4-byte qualifiers (generic decode "
+                   "+ columnar fold)",
+           "points": n, "compacted_bytes": cb, "value": n / dq,
+           "unit": "data points/s", "ms_per_query": dq * 1e3,
+           "stage_ms": {k: v for k, v in zip(STAGES, st) if v},
+           "kernels": "k_decode (count + scan + write), k_prep, k_fold"}
+    if st[7]:
+        out["decode_frac_of_8TBs"] = (cb + 17 * n) / (st[7] / 1e3) / 8e12
+    return out
 
 
 def cpu_baseline(config, target_s):

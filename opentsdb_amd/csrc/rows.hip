@@ -323,6 +323,7 @@ DEV bool bytes_equal_padded(const uint8_t* val, int64_t a, int la, int aav,
 struct LoneOut {
   int64_t nq, nv, kept;
   int err;
+  int meta;  // the meta byte written when kept > 1
 };
 
 // A row with one data column: the one-iterator heap.  Points in column
@@ -334,7 +335,7 @@ template <bool WRITE>
 DEV LoneOut lone_walk(const RawDev& D, int64_t c, int fix, uint8_t* oq,
                       uint8_t* ov) {
   const int lane = LANE;
-  LoneOut o{0, 0, 0, 0};
+  LoneOut o{0, 0, 0, 0, 0};
   const int64_t qb = D.col_qoff[c], ql = D.col_qoff[c + 1] - qb;
   const int64_t vb = D.col_voff[c], vl = D.col_voff[c + 1] - vb;
   const uint8_t* q = D.qual + qb;
@@ -416,7 +417,8 @@ DEV LoneOut lone_walk(const RawDev& D, int64_t c, int fix, uint8_t* oq,
     }
   }
   if (o.kept > 1) {
-    if (WRITE && lane == 0) ov[o.nv] = (ms_in && s_in) ? 1 : 0;
+    o.meta = (ms_in && s_in) ? 1 : 0;
+    if (WRITE && lane == 0) ov[o.nv] = (uint8_t)o.meta;
     o.nv += 1;
   }
   return o;
@@ -500,6 +502,14 @@ __global__ __launch_bounds__(256) void k_rows_plan(
     if (o.err) {
       if (lane == 0) row_error(first_err, r, o.err);
       put(RK_EMPTY, 0, 0, 0);
+      return;
+    }
+    // a column the one-iterator merge rebuilds byte for byte (no repeated
+    // offset, every value byte used, the same meta byte: what a TSD
+    // compaction wrote) is copied as stored
+    if (o.kept > 1 && o.nq == ql && o.nv == vl &&
+        D.val[D.col_voff[first_c] + vl - 1] == (uint8_t)o.meta) {
+      put(RK_VERBATIM, ql, vl, 0);
       return;
     }
     put(o.kept ? RK_LONE : RK_EMPTY, o.nq, o.nv, 0);
@@ -1187,8 +1197,14 @@ __global__ __launch_bounds__(64) void k_large_merge(
 }
 
 // ------------------------------------------------------------------ pack
+// 16 bytes per lane (gfx950 global accesses at any byte address), the last
+// partial 16 bytes one per lane
 DEV void wave_copy(uint8_t* dst, const uint8_t* src, int64_t n) {
-  for (int64_t i = LANE; i < n; i += 64) dst[i] = src[i];
+  const int lane = LANE;
+  for (int64_t i = (int64_t)lane * 16; i + 16 <= n; i += 64 * 16)
+    *reinterpret_cast<uint4*>(dst + i) =
+        *reinterpret_cast<const uint4*>(src + i);
+  for (int64_t j = (n & ~(int64_t)15) + lane; j < n; j += 64) dst[j] = src[j];
 }
 
 __global__ __launch_bounds__(256) void k_rows_write(

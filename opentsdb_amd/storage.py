@@ -79,6 +79,23 @@ class DeviceRawRows:
                            else t["col_ts"].data_ptr())
 
 
+def raw_rows_from_cells(cells):
+    """DeviceCells -> DeviceRawRows holding each compacted row as a storage
+    row with that one column (what the scanner returns for hours already
+    compacted by the TSD); the tensors are shared, not copied."""
+    import torch
+    t = cells.t
+    R = cells.n_rows
+    dev = t["qual"].device
+    rt = dict(row_series=t["row_series"], row_base_s=t["row_base_s"],
+              row_col_off=torch.arange(R + 1, dtype=torch.int64, device=dev),
+              col_qual_off=t["qual_off"], qual=t["qual"],
+              col_val_off=t["val_off"], val=t["val"], col_ts=None)
+    return DeviceRawRows(rt, R, cells.n_series,
+                         int(t["qual_off"][-1].item()),
+                         int(t["val_off"][-1].item()))
+
+
 def _cells_out(R, Q, V, device):
     import torch
     t = dict(row_series=torch.zeros(max(R, 1), dtype=torch.int64, device=device),

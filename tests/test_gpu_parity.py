@@ -62,10 +62,30 @@ def cancel_floor(batch, terms):
     return 1e-12 * terms * float(mags.max())
 
 
-def _member_views(spec, batch):
-    """Per group, the oracle's view stream (Downsampler / RateSpan output,
-    seeked to the window start like AggregationIterator.java:421-437) of
-    every member SpanGroup.add keeps (SpanGroup.java:295-339)."""
+ORDER_FREE_DS = {"min", "max", "mimmin", "mimmax", "first", "last", "count",
+                 "median", "p50", "p75", "p90", "p95", "p99", "p999"}
+
+
+def _spec_variant(spec, **kw):
+    """A copy of a query spec with some fields changed (the calendar tables
+    stay the original spec's: keep it alive)."""
+    s2 = type(spec).from_buffer_copy(spec)
+    for k, v in kw.items():
+        setattr(s2, k, v)
+    return s2
+
+
+def _member_scales(spec, batch):
+    """Per group, per member SpanGroup.add keeps (SpanGroup.java:295-339):
+    (ts, value, scale) of its view stream (Downsampler / RateSpan output,
+    seeked to the window start like AggregationIterator.java:421-437) — the
+    value the aggregator is fed and the magnitude its rounding is relative
+    to.  A downsampled value's scale is |value|, or n x max|raw value| of
+    its bucket when the downsampling function subtracts internally (dev,
+    diff, or a sum over raw values of both signs); a rate's is
+    (scale(v0) + scale(v1)) / dt of the two bucket values it differences
+    (counterMax added at a counter wrap, RateSpan.java:121-180)."""
+    from opentsdb_amd import core as _core
     offs = np.asarray(batch.offsets, np.int64)
     ts = np.asarray(batch.ts, np.int64)
     val = np.asarray(batch.val, np.int64)
@@ -73,74 +93,134 @@ def _member_views(spec, batch):
            else np.asarray(batch.is_float, np.uint8))
     g_off = np.asarray(batch.group_offsets, np.int64)
     members = np.asarray(batch.group_members, np.int64)
+    ds = spec.ds_interval_ms > 0 or spec.run_all
+    ds_name = _core.Aggregators.by_id(spec.ds_agg_id).registry_name if ds \
+        else None
+    plain = _spec_variant(spec, rate=0)
+    if ds:
+        # bucket min / max / count of the raw values (same grid)
+        v_min = _spec_variant(spec, rate=0, ds_agg_id=_core.Aggregators.MIN.id)
+        v_max = _spec_variant(spec, rate=0, ds_agg_id=_core.Aggregators.MAX.id)
+        v_cnt = _spec_variant(spec, rate=0,
+                              ds_agg_id=_core.Aggregators.COUNT.id)
     out = []
     for g in range(len(g_off) - 1):
         views = []
-        for s in members[g_off[g]:g_off[g + 1]]:
-            p0, p1 = int(offs[s]), int(offs[s + 1])
+        for sid in members[g_off[g]:g_off[g + 1]]:
+            p0, p1 = int(offs[sid]), int(offs[sid + 1])
             if p1 <= p0 or not (ts[p0] <= spec.end_ms and
                                 ts[p1 - 1] >= spec.start_ms):
                 continue
-            v = pyoracle.view_stream(spec, ts[p0:p1], val[p0:p1],
-                                     isf[p0:p1], seek=spec.start_ms)
-            views.append((v["ts"], _vals(v["bits"], v["is_int"])))
+            sl = (ts[p0:p1], val[p0:p1], isf[p0:p1])
+
+            def view(sp):
+                v = pyoracle.view_stream(sp, *sl, seek=spec.start_ms)
+                return v["ts"], _vals(v["bits"], v["is_int"])
+            dts, dv = view(plain)
+            scale = np.abs(np.nan_to_num(dv, nan=0.0))
+            # a bucket value computed exactly rounds nowhere: order-free
+            # functions, and sums / averages of longs below 2^53
+            exact = np.full(len(dv), ds_name in ORDER_FREE_DS)
+            if ds_name in ("sum", "zimsum", "pfsum", "avg") and \
+                    not sl[2].any() and (np.abs(dv) < 2.0 ** 52).all():
+                exact[:] = True
+            if ds and ds_name not in ORDER_FREE_DS:
+                _, mn = view(v_min)
+                _, mx = view(v_max)
+                _, n = view(v_cnt)
+                mn, mx, n = np.nan_to_num(mn), np.nan_to_num(mx), np.nan_to_num(n)
+                raw = np.maximum(np.abs(mn), np.abs(mx)) * np.maximum(n, 1)
+                cancels = (ds_name in ("dev", "diff")) | ((mn < 0) & (mx > 0))
+                scale = np.where(cancels, np.maximum(scale, raw), scale)
+            if not spec.rate:
+                views.append((dts, dv, scale))
+                continue
+            rts, rv = view(spec)
+            # each rate's bucket pair: the ds point at its ts and the one
+            # before it (the (0, 0) reset point for the junk rate); only an
+            # inexact bucket value carries rounding into the difference
+            err = np.where(exact, 0.0, scale)
+            k = np.searchsorted(dts, rts)
+            s1 = err[k]
+            s0 = np.where(k > 0, err[np.maximum(k - 1, 0)], 0.0)
+            t0 = np.where(k > 0, dts[np.maximum(k - 1, 0)], 0)
+            v0 = np.where(k > 0, dv[np.maximum(k - 1, 0)], 0.0)
+            wrap = bool(spec.counter) & (dv[k] < v0)
+            s0 = s0 + np.where(wrap & ~exact[k], float(spec.counter_max), 0.0)
+            dt = np.maximum((rts - t0) / 1000.0, 1e-3)
+            rscale = (s0 + s1) / dt
+            views.append((rts, rv, rscale + np.abs(np.nan_to_num(rv))))
         out.append(views)
     return out
 
 
 def contribution_floor(spec, batch, ref):
-    """Per emitted point, the absolute floor 1e-12 x sum|contributions|:
+    """Per emitted point, the absolute floor 1e-12 x sum of the scales of
     the values the cross-series aggregator is fed at that timestamp
-    (AggregationIterator.java:682-797) — each member's real value, or a bound
-    on its interpolated / held one — taken from the oracle's per-member view
-    streams.  Nonzero only where those contributions have both signs (a sum
-    of same-signed terms keeps its relative error); elsewhere the comparator
-    is the pure 1e-12 relative bound."""
+    (AggregationIterator.java:682-797) — each member's real value, or its
+    interpolated / held one bounded by its neighbours — from the oracle's
+    per-member view streams (_member_scales: |value|, or the raw magnitude
+    a downsampled value or a rate was computed from when that computation
+    subtracts).  Nonzero only where rounding can be amplified: the
+    contributions have both signs, the aggregator subtracts (dev, diff), or
+    a contribution's own computation does (rates; dev / diff downsampling;
+    sums over raw values of both signs).  Elsewhere the comparator is the
+    pure 1e-12 relative bound (a sum of same-signed terms keeps its relative
+    error)."""
     interp = spec.interp
     if interp < 0:
         interp = core.Aggregators.by_id(spec.agg_id).interpolationMethod()
     interp = int(interp)
+    agg = core.Aggregators.by_id(spec.agg_id).registry_name
     big = np.finfo(np.float64).max
     floors = []
-    for views, r in zip(_member_views(spec, batch), ref):
+    for views, r in zip(_member_scales(spec, batch), ref):
         x = np.asarray(r["ts"], np.int64)
         mag = np.zeros(len(x))
         pos = np.zeros(len(x), bool)
         neg = np.zeros(len(x), bool)
-        for vts, vv in views:
+        amp = np.zeros(len(x), bool)  # a contribution's own subtraction
+        for vts, vv, sc in views:
             if len(vts) == 0:
                 continue
             v = np.nan_to_num(vv, nan=0.0)
             i = np.searchsorted(vts, x, "left")
-            exact_pt = (i < len(vts)) & (vts[np.minimum(i, len(vts) - 1)] == x)
-            y1 = v[np.minimum(i, len(vts) - 1)]
-            y0 = v[np.maximum(i - 1, 0)]
+            last = len(vts) - 1
+            exact_pt = (i <= last) & (vts[np.minimum(i, last)] == x)
+            y1, s1 = v[np.minimum(i, last)], sc[np.minimum(i, last)]
+            y0, s0 = v[np.maximum(i - 1, 0)], sc[np.maximum(i - 1, 0)]
             if spec.rate:
                 # every kept span contributes from the first emitted ts with
                 # its latest rate at or before x, the junk rate included
                 # (AggregationIterator.java:448-459, :744-753)
                 live = x <= vts[-1]
                 held = np.where(i > 0, y0, v[0])
+                hs = np.where(i > 0, s0, sc[0])
                 lo = hi = np.where(exact_pt, y1, held)
+                m = np.where(exact_pt, s1, hs)
             else:
                 live = (x >= vts[0]) & (x <= vts[-1])
                 if interp == 0:    # LERP: between its neighbours
-                    lo, hi = y0, y1
+                    lo, hi, m = y0, y1, np.maximum(s0, s1)
                 elif interp == 1:  # ZIM
-                    lo = hi = np.zeros(len(x))
+                    lo = hi = m = np.zeros(len(x))
                 elif interp == 2:  # MAX
-                    lo = hi = np.full(len(x), big)
+                    lo = hi = m = np.full(len(x), big)
                 elif interp == 3:  # MIN
                     lo = hi = np.full(len(x), -big)
+                    m = np.full(len(x), big)
                 else:              # PREV
                     lo = hi = y0
+                    m = s0
                 lo = np.where(exact_pt, y1, lo)
                 hi = np.where(exact_pt, y1, hi)
-            m = np.maximum(np.abs(lo), np.abs(hi))
+                m = np.where(exact_pt, s1, m)
             mag += np.where(live, m, 0.0)
             pos |= live & ((lo > 0) | (hi > 0))
             neg |= live & ((lo < 0) | (hi < 0))
-        floors.append(np.where(pos & neg, 1e-12 * mag, 0.0))
+            amp |= live & (m > np.maximum(np.abs(lo), np.abs(hi)))
+        need = (pos & neg) | amp | (agg in ("dev", "diff"))
+        floors.append(np.where(need, 1e-12 * mag, 0.0))
     return floors
 
 
