@@ -388,6 +388,7 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
     }
   };
   int32_t p = (int32_t)uni(mc->pa);
+  L2Touch pq_, pv_;
   const int32_t n_guard = pe - p + 64;  // every step consumes >= 1 point
   int dbg_n = 0;
   while (p < pe) {
@@ -460,6 +461,18 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
     int32_t a0 = act ? vcur + ((K * lane) << vsh) + mbefore : vcur;
     if (!vnear) cells_vload_vl(1 << vsh, vp, (uint32_t)a0, d);
     else cells_vload_bytes(vp, a0, vlim, d);
+    if (OTSDB_PF_CELLS) {
+      // the lines OTSDB_PF_CELLS steps ahead (at this step's value length)
+      pq_.retire();
+      pv_.retire();
+      const int32_t pq = (p + OTSDB_PF_CELLS * PTS) << qsh;
+      if (((p + (OTSDB_PF_CELLS + 1) * PTS) << qsh) + 16 <= qlim)
+        pq_.touch(qp + pq + (lane << (qsh + 3)));
+      const int32_t pvo = vcur + ((OTSDB_PF_CELLS * PTS) << vsh) +
+                          (lane << (vsh + 3));
+      if (vcur + (((OTSDB_PF_CELLS + 1) * PTS) << vsh) + 128 <= vlim)
+        pv_.touch(vp + pvo);
+    }
 #if defined(OTSDB_CELLS_ABL) && OTSDB_CELLS_ABL == 2  // timing: loads only
     {
       uint32_t x = 0;

@@ -339,6 +339,7 @@ DEV void fold_member(const Params& P, const BatchDev& B, FoldSink<A>& F,
   int64_t lo_eff = pa;
   int32_t prev_hi = -1;  // bucket of the previous step's last point
   int dbg_n = 0;
+  L2Touch pt_, pv_;
   // (no points in the window: no step — an aligned base below an odd pa
   // would stream the point before the window and read bucket bounds past it)
   for (int64_t base = pa & ~(int64_t)1; pa < pb && base < pb;) {
@@ -358,6 +359,14 @@ DEV void fold_member(const Params& P, const BatchDev& B, FoldSink<A>& F,
       for (int j = 0; j < K; ++j) {
         t[j] = (i0 + j < pb) ? B.ts[i0 + j] : 0;
         v[j] = (i0 + j < pb) ? B.val[i0 + j] : 0;
+      }
+    }
+    if (OTSDB_PF_FOLD) {
+      pt_.retire();
+      pv_.retire();
+      if (base + (OTSDB_PF_FOLD + 1) * PTS <= pb) {
+        pt_.touch(B.ts + i0 + OTSDB_PF_FOLD * PTS);
+        pv_.touch(B.val + i0 + OTSDB_PF_FOLD * PTS);
       }
     }
 #ifdef OTSDB_FOLD_ABL_STREAM  // timing ablation: the loads alone

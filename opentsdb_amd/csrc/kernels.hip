@@ -260,6 +260,30 @@ DEV void wait_vmcnt(int n) {
   }
 }
 
+// L2 prefetch of a stream's bytes some steps ahead: each lane loads one
+// dword of every 64-byte stretch (a step's lines, one load per lane) into a
+// register the stream only retires at its next step, after that step's own
+// loads are issued.  The point streams are bound by the bytes a wavefront
+// keeps in flight at their occupancy; this adds the lines of a later step
+// for one VGPR and one load per array.  Distances are build knobs
+// (OTSDB_PF_FOLD / _CELLS / _BUCK, steps ahead, 0 = off).
+#ifndef OTSDB_PF_FOLD
+#define OTSDB_PF_FOLD 0
+#endif
+#ifndef OTSDB_PF_CELLS
+#define OTSDB_PF_CELLS 0
+#endif
+#ifndef OTSDB_PF_BUCK
+#define OTSDB_PF_BUCK 0
+#endif
+struct L2Touch {
+  uint32_t v = 0;
+  DEV void touch(const void* p) { v = *reinterpret_cast<const uint32_t*>(p); }
+  // the data is never used: an empty asm only makes the register live, so
+  // the wait for it lands here (a step later), not at the touch
+  DEV void retire() { asm volatile("" ::"v"(v)); }
+};
+
 DEV double readlane_d(double x, int l) {
   const int64_t b = __builtin_bit_cast(int64_t, x);
   const int32_t lo = __builtin_amdgcn_readlane((int32_t)(uint32_t)b, l);
@@ -868,6 +892,7 @@ DEV void bucketize_series(const Params& P, const BatchDev& B,
   int64_t tn[K], vn[K];
   const int64_t base0 = lo & ~(int64_t)1;
   if (PF) load_step(base0 + (int64_t)K * lane, tn, vn);
+  L2Touch pt_, pv_;
   for (int64_t base = base0; base < hi; base += PTS) {
     const int64_t i0 = base + (int64_t)K * lane;
     int64_t t[K], v[K];
@@ -877,6 +902,14 @@ DEV void bucketize_series(const Params& P, const BatchDev& B,
       if (base + PTS < hi) load_step(i0 + PTS, tn, vn);
     } else {
       load_step(i0, t, v);
+    }
+    if (OTSDB_PF_BUCK) {
+      pt_.retire();
+      pv_.retire();
+      if (base + (OTSDB_PF_BUCK + 1) * PTS <= hi) {
+        pt_.touch(B.ts + i0 + OTSDB_PF_BUCK * PTS);
+        pv_.touch(B.val + i0 + OTSDB_PF_BUCK * PTS);
+      }
     }
     if (ABL == 1) {  // tuning ablation: stream only
       int64_t x = 0;
