@@ -8,7 +8,10 @@ all-gathered over RCCL (torch.distributed, backend "nccl"; "gloo" in CPU
 tests) and merged in rank order, which is series order, by
 otsdb_agg_finalize_device.  Median / percentiles across ranks run the
 otsdb_sel_* protocol instead: all-reduced contribution counts, then eight
-radix-select passes whose 256-bin histograms are all-reduced (exact).
+radix-select passes whose 256-bin histograms are all-reduced (exact).  Raw
+(non-downsampled) queries, whose union-timestamp merge needs every member's
+points, run the groups spanning ranks as replicas over all-gathered member
+series (gather_shared_series).
 """
 import numpy as np
 
@@ -371,10 +374,125 @@ class _SelResult:
         return _host_slices(range(len(self.res.offsets) - 1), self.res)
 
 
+def _all_gather_var(t, group=None):
+    """All-gather of a 1-D tensor whose length differs per rank: lengths
+    first, then the tensors padded to the longest.  Returns the per-rank
+    tensors in rank order (on t's device)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dev = t.device
+    staged = _staged(group)
+    n = torch.tensor([t.numel()], dtype=torch.int64,
+                     device="cpu" if staged else dev)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    ns = [int(x.item()) for x in ns]
+    L = max(max(ns), 1)
+    src = t.cpu() if staged else t
+    pad = torch.zeros(L, dtype=t.dtype, device=src.device)
+    pad[:t.numel()] = src
+    outs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad, group=group)
+    return [o[:k].to(dev) for o, k in zip(outs, ns)]
+
+
+def gather_shared_series(dbatch, shared_ids, group=None):
+    """Raw (non-downsampled) group-by over groups that span ranks: the
+    union-timestamp merge (AggregationIterator.next, AggregationIterator.java:
+    514-567) needs every member's points, so those groups run as replicas
+    (SURVEY §8e): each rank contributes its members of the shared groups
+    (points in SpanCmp order) and every rank gathers all of them, rank order
+    being series order.  Returns a DeviceBatch over the shared groups only
+    (group i = shared_ids[i]) on dbatch's device."""
+    import torch
+    from .engine import DeviceBatch
+    dev = dbatch.ts.device
+    goff = dbatch.group_offsets.cpu().numpy()
+    mem = dbatch.group_members.cpu().numpy()
+    offs = dbatch.offsets.cpu().numpy()
+    series, gids = [], []
+    for k, g in enumerate(shared_ids):
+        for s in mem[goff[g]:goff[g + 1]]:
+            series.append(int(s))
+            gids.append(k)
+    sidx = torch.tensor(series or [0], dtype=torch.int64, device=dev)[:len(series)]
+    lens = torch.tensor([offs[s + 1] - offs[s] for s in series] or [0],
+                        dtype=torch.int64, device=dev)[:len(series)]
+    pts = (torch.cat([torch.arange(int(offs[s]), int(offs[s + 1]),
+                                   dtype=torch.int64, device=dev)
+                      for s in series])
+           if series else torch.zeros(0, dtype=torch.int64, device=dev))
+    ts = dbatch.ts[pts]
+    val = dbatch.val[pts]
+    if dbatch.is_float is not None:
+        isf = dbatch.is_float[pts]
+    elif dbatch.series_float is not None:
+        isf = torch.repeat_interleave(dbatch.series_float[sidx].to(torch.uint8),
+                                      lens)
+    else:
+        isf = torch.ones(len(pts), dtype=torch.uint8, device=dev)
+    gl = torch.tensor(gids or [0], dtype=torch.int64, device=dev)[:len(gids)]
+    parts = [_all_gather_var(x, group) for x in (lens, gl, ts, val, isf)]
+    lens_all = torch.cat(parts[0])
+    g_all = torch.cat(parts[1])
+    # members of each shared group: rank-major = series order
+    order = torch.argsort(g_all, stable=True)
+    n_sh = len(shared_ids)
+    counts = torch.bincount(g_all, minlength=n_sh) if g_all.numel() else \
+        torch.zeros(n_sh, dtype=torch.int64, device=dev)
+    g_off = torch.zeros(n_sh + 1, dtype=torch.int64, device=dev)
+    g_off[1:] = torch.cumsum(counts, 0)
+    offsets = torch.zeros(lens_all.numel() + 1, dtype=torch.int64, device=dev)
+    offsets[1:] = torch.cumsum(lens_all, 0)
+    cat = lambda xs: torch.cat(xs) if xs else xs  # noqa: E731
+    ts_all, val_all, isf_all = cat(parts[2]), cat(parts[3]), cat(parts[4])
+    # 16-byte aligned columns for the engine's streaming loads
+    n = ts_all.numel()
+    tsb = torch.zeros(max(n, 2), dtype=torch.int64, device=dev)
+    vb = torch.zeros_like(tsb)
+    tsb[:n] = ts_all
+    vb[:n] = val_all
+    db = DeviceBatch(offsets, tsb[:n], vb[:n], g_off, order.contiguous(),
+                     isf_all.contiguous(), None)
+    db.n_points_total = n
+    return db
+
+
+def run_sharded_raw(engine, spec, dbatch, n_groups_global, group=None):
+    """Raw group-by over series-sharded ranks: groups a rank holds alone run
+    locally; groups spanning ranks run as replicas over their gathered
+    members (gather_shared_series), identical on every rank."""
+    import torch
+    from .engine import DeviceResult, run_device
+    plans = getattr(dbatch, "_shard_plans", None)
+    if plans is None:
+        plans = dbatch._shard_plans = {}
+    key = (id(engine), bytes(memoryview(spec).cast("B")), n_groups_global,
+           "raw")
+    plan = plans.get(key)
+    if plan is None:
+        plan = plans[key] = ShardPlan(engine, spec, dbatch, n_groups_global,
+                                      group)
+    if len(plan.local):
+        run_device(engine, spec, plan.local_batch, plan.local_res)
+    shared_res = None
+    if len(plan.shared):
+        sb = gather_shared_series(dbatch, plan.shared, group)
+        cap = int(engine.plan(spec, sb).max_out_points)
+        shared_res = DeviceResult(torch, len(plan.shared), max(cap, 1),
+                                  dbatch.ts.device)
+        run_device(engine, spec, sb, shared_res)
+    return ShardedResult(plan.local, plan.local_res, plan.shared, shared_res)
+
+
 def run_sharded_any(engine, spec, dbatch, n_groups_global, group=None):
-    """Dispatch: selection aggregators take the histogram protocol, every
-    other aggregator the shared-group partial exchange.  The result has
-    n_points()."""
+    """Dispatch: selection aggregators take the histogram protocol, raw
+    (non-downsampled) queries the replica exchange, every other aggregator
+    the shared-group partial exchange.  The result has n_points()."""
+    raw = not (spec.ds_interval_ms > 0 or spec.run_all)
+    if raw:
+        return run_sharded_raw(engine, spec, dbatch, n_groups_global, group)
     if spec.agg_id == 5 or spec.agg_id >= 17:  # median, p*, ep*
         return _SelResult(run_sharded_select(engine, spec, dbatch,
                                              n_groups_global, group))

@@ -189,3 +189,50 @@ def test_bench_spawns_ranks_dry_run():
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["steps"] == 3
+
+
+def _gather_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from tests import datasets
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    hb = datasets.random_batch(31, n_series=29, n_groups=4, value_kind="mixed")
+    db = odist.to_device(odist.shard_host_batch(hb, world, rank), "cpu")
+    sb = odist.gather_shared_series(db, np.array([0, 2, 3]))
+    q.put((rank, sb.offsets.numpy().copy(), sb.ts.numpy().copy(),
+           sb.val.numpy().copy(), sb.is_float.numpy().copy(),
+           sb.group_offsets.numpy().copy(), sb.group_members.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_raw_replica_gather_gloo_world2():
+    """Raw group-by across ranks runs the shared groups as replicas: every
+    rank gathers the same batch of those groups' members, in series
+    (SpanCmp) order, points and value types intact."""
+    from tests import datasets
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict((x[0], x[1:]) for x in (q.get(timeout=120) for _ in range(world)))
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for a, b in zip(got[0], got[1]):
+        assert np.array_equal(a, b)  # identical on every rank
+    offs, ts, val, isf, goff, mem = got[0]
+    hb = datasets.random_batch(31, n_series=29, n_groups=4, value_kind="mixed")
+    for k, g in enumerate([0, 2, 3]):
+        exp = hb.group_members[hb.group_offsets[g]:hb.group_offsets[g + 1]]
+        got_m = mem[goff[k]:goff[k + 1]]
+        assert len(got_m) == len(exp)
+        for sg, s in zip(got_m, exp):
+            a, b = hb.offsets[s], hb.offsets[s + 1]
+            assert np.array_equal(ts[offs[sg]:offs[sg + 1]], hb.ts[a:b])
+            assert np.array_equal(val[offs[sg]:offs[sg + 1]], hb.val[a:b])
+            assert np.array_equal(isf[offs[sg]:offs[sg + 1]], hb.is_float[a:b])

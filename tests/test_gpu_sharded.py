@@ -138,7 +138,16 @@ def _free_port():
 
 
 QUERIES = [("sum", "avg", "none"), ("dev", "max", "nan"), ("p99", "avg", "nan"),
-           ("median", "max", "none")]
+           ("median", "max", "none"),
+           # raw (non-downsampled) group-by: shared groups run as replicas
+           ("sum", None, None), ("max", None, None)]
+
+
+def _qspec(agg, ds, fill):
+    if ds is None:
+        t0, t1 = datasets.T0, datasets.T0 + 3 * 3600 * 1000
+        return core.make_spec(t0, t1, core.Aggregators.get(agg), None, t0, t1)
+    return _spec(agg, ds, fill)
 
 
 def _rank_main(rank, world, port, q):
@@ -152,7 +161,7 @@ def _rank_main(rank, world, port, q):
     hb = datasets.random_batch(205, n_series=50, n_groups=3, nan_frac=0.02)
     out = []
     for agg, ds, fill in QUERIES:
-        spec = _spec(agg, ds, fill)
+        spec = _qspec(agg, ds, fill)
         db = odist.to_device(odist.shard_host_batch(hb, world, rank))
         res = odist.run_sharded_any(e, spec, db, hb.n_groups)
         torch.cuda.synchronize()
@@ -191,14 +200,15 @@ def test_two_processes_gloo():
         assert p.exitcode == 0
     hb = datasets.random_batch(205, n_series=50, n_groups=3, nan_frac=0.02)
     for k, (agg, ds, fill) in enumerate(QUERIES):
-        ref = pyoracle.group_by(_spec(agg, ds, fill), hb)
+        ref = pyoracle.group_by(_qspec(agg, ds, fill), hb)
         merged = {}
         for _, out in outs:
             merged.update(out[k])
         assert sorted(merged) == list(range(hb.n_groups))
         got = [DataPoints(*merged[g]) for g in range(hb.n_groups)]
-        compare(got, ref, ds == "max" and agg not in ("sum", "dev"),
-                where="gloo/%s" % agg)
+        # raw: the replica runs the whole group in span order (exact)
+        compare(got, ref, (ds == "max" and agg not in ("sum", "dev")) or
+                ds is None, where="gloo/%s/%s" % (agg, ds))
 
 
 def _rccl_main(port, q):
@@ -217,7 +227,7 @@ def _rccl_main(port, q):
     hb = datasets.random_batch(207, n_series=50, n_groups=3, nan_frac=0.02)
     out = []
     for agg, ds, fill in QUERIES:
-        spec = _spec(agg, ds, fill)
+        spec = _qspec(agg, ds, fill)
         db = odist.to_device(hb)
         # rank-local groups (classification all-reduce on device)
         res = odist.run_sharded_any(e, spec, db, hb.n_groups)
@@ -233,7 +243,8 @@ def _rccl_main(port, q):
                 np.zeros(0, np.int64), np.nonzero(np.diff(goff) > 0)[0])
             try:
                 db2 = odist.to_device(hb)
-                r2 = odist.run_sharded(e, spec, db2, hb.n_groups)
+                # partial exchange, or (raw) the replica gather
+                r2 = odist.run_sharded_any(e, spec, db2, hb.n_groups)
             finally:
                 odist.classify_groups = real
             torch.cuda.synchronize()
@@ -267,8 +278,8 @@ def test_rccl_world_size_one():
     assert p.exitcode == 0
     hb = datasets.random_batch(207, n_series=50, n_groups=3, nan_frac=0.02)
     for (agg, ds, fill), (local, shared) in zip(QUERIES, out):
-        ref = pyoracle.group_by(_spec(agg, ds, fill), hb)
-        exact = ds == "max" and agg not in ("sum", "dev")
+        ref = pyoracle.group_by(_qspec(agg, ds, fill), hb)
+        exact = (ds == "max" and agg not in ("sum", "dev")) or ds is None
         for name, res in (("local", local), ("shared", shared)):
             if res is None:
                 continue
