@@ -298,18 +298,19 @@ DEV void cells_vextract_vl(int vl, int fl, const uint32_t* d, int jb,
   }
 }
 
-// timestamp of in-step point `rel` (wave-uniform; lane rel / K, element
-// rel % K — a uniform select, then a readlane: no dynamic register index)
+// grid-relative time of in-step point `rel` (wave-uniform; lane rel / K,
+// element rel % K — a uniform select, then a readlane: no dynamic register
+// index)
 template <int K>
-DEV int64_t cells_pick(const int64_t* t, int32_t rel) {
+DEV uint32_t cells_pick(const uint32_t* t, int32_t rel) {
   // the element index is per lane (-1 off lane L): with a wave-uniform one
   // the compiler turns the select chain into t[e] and puts t[] in scratch
   const int L = (int)(rel / K);
   const int e = LANE == L ? (int)(rel % K) : -1;
-  int64_t x = 0;
+  uint32_t x = 0;
 #pragma unroll
   for (int j = 0; j < K; ++j) x = j == e ? t[j] : x;
-  return readlane_l(x, L);
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, L);
 }
 
 DEV int wave_excl_scan(int x, int& total) {
@@ -324,7 +325,9 @@ DEV int wave_excl_scan(int x, int& total) {
 }
 
 // One member's points [pa, pb) straight from its compacted columns (the
-// cells counterpart of fold_member; NW == 1, so no window context).
+// cells counterpart of fold_member; NW == 1, so no window context).  The
+// grid is narrow (run_pipeline sends other grids to k_bucketize_cells):
+// point times are 32-bit ms since the grid base, row bases too.
 // Indexing is 32-bit and relative to the series (its point numbers, and
 // value bytes from its first row's val_off; k_cells_prep sends series whose
 // pools exceed 2^30 bytes to the generic decode): loads address a uniform
@@ -366,16 +369,17 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
   int32_t prev_hi = -1;
   int fault = 0;  // ERR_CELLS_GENERIC / ERR_CORRUPT_CELL / ERR_INTERNAL
   // row metadata, row mb + lane: first point, first value byte, points |
-  // bad shape << 30, base time
-  int64_t mb = -(int64_t)BIG, w_bms = 0;
-  int32_t w_ps = 0, w_vo = 0, w_nb = 0;
+  // bad shape << 30, base time (ms since the grid base, mod 2^32)
+  int64_t mb = -(int64_t)BIG;
+  int32_t w_ps = 0, w_vo = 0, w_nb = 0, w_br = 0;
+  const int64_t gbase = P.gbase;
   auto load_window = [&](int64_t m) {
     mb = m;
     const int64_t x = m + lane;
     w_ps = BIG;
     w_vo = 0;
     w_nb = 0;
-    w_bms = 0;
+    w_br = 0;
     if (x <= r1) {
       const int64_t qo = C.qual_off[x];
       w_ps = (int32_t)((qo - qb) >> qsh);
@@ -383,7 +387,7 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
       if (x < r1) {
         const int32_t ql = (int32_t)(C.qual_off[x + 1] - qo);
         w_nb = (ql >> qsh) | ((ql <= 0 || (ql & (qw - 1))) ? (1 << 30) : 0);
-        w_bms = C.row_base_s[x] * 1000;
+        w_br = (int32_t)(uint32_t)(C.row_base_s[x] * 1000 - gbase);
       }
     }
   };
@@ -500,13 +504,13 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
     const int jb = nbnd - p0 < K ? nbnd - p0 : K;
     const bool cross = act && jb < nv;  // (jb < 0 on lanes past the step)
     const int32_t mnext = rl == 0 ? m0 : (rl == 1 ? m1 : m2);
-    // row base times relative to row ra's (32-bit per point)
-    const int64_t bm0 = readlane_l(w_bms, j0);
-    const int32_t rb1 = (int32_t)(readlane_l(w_bms, j0 + 1) - bm0);
-    const int32_t rb2 = (int32_t)(readlane_l(w_bms, j0 + 2) - bm0);
-    const int32_t rb3 = (int32_t)(readlane_l(w_bms, j0 + 3) - bm0);
-    const int32_t bcur = rl == 0 ? 0 : (rl == 1 ? rb1 : rb2);
-    const int32_t bnext = rl == 0 ? rb1 : (rl == 1 ? rb2 : rb3);
+    // row base times (grid-relative, mod 2^32)
+    const uint32_t rb0 = (uint32_t)__builtin_amdgcn_readlane(w_br, j0);
+    const uint32_t rb1 = (uint32_t)__builtin_amdgcn_readlane(w_br, j0 + 1);
+    const uint32_t rb2 = (uint32_t)__builtin_amdgcn_readlane(w_br, j0 + 2);
+    const uint32_t rb3 = (uint32_t)__builtin_amdgcn_readlane(w_br, j0 + 3);
+    const uint32_t bcur = rl == 0 ? rb0 : (rl == 1 ? rb1 : rb2);
+    const uint32_t bnext = rl == 0 ? rb1 : (rl == 1 ? rb2 : rb3);
     // ---- qualifiers -> timestamps, flags
     uint32_t q[K];
     if (qw == 2) {
@@ -522,16 +526,17 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
     }
     const uint32_t f0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(q[0] & 0xF));
     int odd = 0, mixed = 0;
-    int64_t t[K], v[K];
+    uint32_t t[K];
+    int64_t v[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       const bool in = j < nv;
       const uint32_t nib = qw == 2 ? (q[j] >> 12) : (q[j] >> 28);
       odd |= in && ((qw == 2) == (nib == 0xF));
       mixed |= in && ((q[j] & 0xF) != f0);
-      const int32_t off = qw == 2 ? (int32_t)((q[j] >> 4) * 1000u)
-                                  : (int32_t)((q[j] & 0x0FFFFFC0u) >> 6);
-      t[j] = bm0 + (int64_t)((j >= jb ? bnext : bcur) + off);
+      const uint32_t off = qw == 2 ? (q[j] >> 4) * 1000u
+                                   : (q[j] & 0x0FFFFFC0u) >> 6;
+      t[j] = (j >= jb ? bnext : bcur) + off;
     }
     if (__ballot(odd)) {
       fault |= ERR_CELLS_GENERIC;
@@ -603,10 +608,10 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
       break;
     }
     // ---- the downsample over [p, hs) (fold_member's ring bookkeeping)
-    const int32_t k_hi = fold_bucket(P, cells_pick<K>(t, sb - 1 - p));
+    const int32_t k_hi = bucket_rel(P, cells_pick<K>(t, sb - 1 - p));
     int32_t hs = sb;
     if (k_hi >= F.flushed + FOLD_WIN) {
-      const int32_t k_first = fold_bucket(P, cells_pick<K>(t, 0));
+      const int32_t k_first = bucket_rel(P, cells_pick<K>(t, 0));
       if (carry_ok && carry_key < k_first) {
         if (lane == 0) S.put(carry_key, carry.finish(&err));
         carry_key = INT32_MIN;
@@ -616,7 +621,9 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
       }
       fold_flush(P, F, limit);
       if (k_hi >= F.flushed + FOLD_WIN) {
-        const int64_t T = bucket_ts(P, F.flushed + FOLD_WIN);
+        // the ring's end (k_hi lies past it, so inside the narrow grid)
+        const uint32_t T =
+            (uint32_t)((int64_t)(F.flushed + FOLD_WIN) * P.interval);
         int cnt = 0;
 #pragma unroll
         for (int j = 0; j < K; ++j) cnt += (j < nv && t[j] < T) ? 1 : 0;
@@ -636,7 +643,7 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
       used = uni((int32_t)wave_sum(c));
     }
     const int32_t k_last =
-        hs == sb ? k_hi : fold_bucket(P, cells_pick<K>(t, hs - 1 - p));
+        hs == sb ? k_hi : bucket_rel(P, cells_pick<K>(t, hs - 1 - p));
     // a step cut at a row rule (not at a bucket edge) leaves the bucket of
     // its last point open: it carries into the next step (keep_open)
 #if defined(OTSDB_CELLS_ABL) && OTSDB_CELLS_ABL == 1  // timing: no reduction

@@ -728,9 +728,10 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       return fail(OTSDB_E_NO_SUCH_ELEMENT, "aggregator %d", spec->agg_id);
     NW = (NB + WB - 1) / WB;
   }
-  // the cells fold runs one window (no k_fold_prep over cells); wider grids
-  // from cells take k_bucketize_cells and the row pipeline
-  if (cells && NW > 1) {
+  // the cells fold runs one window (no k_fold_prep over cells) of a narrow
+  // grid (32-bit times); wider and calendar grids from cells take
+  // k_bucketize_cells and the row pipeline
+  if (cells && (NW > 1 || !P.narrow)) {
     fold = false;
     WB = NW = 0;
   }

@@ -244,6 +244,38 @@ DEV int bucket_narrow(const Params& P, int64_t ts) {
   return (int)q;
 }
 
+// Point times on the bucket grid: absolute ms (int64_t), or on narrow grids
+// ms since the grid base (uint32_t: the cells fold, whose 32-bit times save
+// the 64-bit adds, compares and registers of the absolute ones).
+DEV int bucket_rel(const Params& P, uint32_t rel) {
+  if (P.run_all) return 0;
+  const uint32_t iv = (uint32_t)P.interval;
+  uint32_t q = (uint32_t)((double)rel * P.inv_interval);
+  const uint32_t r = rel - q * iv;
+  q = ((int32_t)r < 0) ? q - 1 : (r >= iv ? q + 1 : q);
+  return (int)q;
+}
+DEV int tbucket_narrow(const Params& P, int64_t t) { return bucket_narrow(P, t); }
+DEV int tbucket_narrow(const Params& P, uint32_t t) { return bucket_rel(P, t); }
+DEV int64_t tbucket(const Params& P, int64_t t) { return bucket_of(P, t); }
+DEV int64_t tbucket(const Params& P, uint32_t t) { return bucket_rel(P, t); }
+// the start of bucket k on a fixed grid / its end for fold_lane
+DEV int64_t tstart_fixed(const Params& P, int64_t k, int64_t) {
+  return P.gbase + k * P.interval;
+}
+DEV uint32_t tstart_fixed(const Params& P, int64_t k, uint32_t) {
+  return (uint32_t)(k * P.interval);
+}
+DEV int64_t tbound(const Params& P, int64_t k, int64_t) {
+  return P.run_all ? INT64_MAX : bucket_ts(P, k);
+}
+DEV uint32_t tbound(const Params& P, int64_t k, uint32_t) {
+  return P.run_all ? 0xFFFFFFFFu : (uint32_t)(k * P.interval);
+}
+template <class TT> DEV TT tmin();
+template <> DEV int64_t tmin<int64_t>() { return INT64_MIN; }
+template <> DEV uint32_t tmin<uint32_t>() { return 0u; }
+
 DEV void wait_vmcnt(int n) {
   // s_waitcnt vmcnt(n) (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14,
   // expcnt and lgkmcnt at their no-wait maxima)
@@ -457,29 +489,28 @@ DEV void sink_flush(RowSink& S, int64_t& flushed, int64_t limit,
 // spans four or more buckets.
 // nv < K: only the first nv points are in range (the step reaches past the
 // end of the series / window); nv == 0 leaves the lane empty (nseg = 0).
-template <class M, int K, bool FLOATONLY>
+template <class M, int K, bool FLOATONLY, class TT = int64_t>
 DEV bool fold_fast(const Params& P, const BatchDev& B, int sf, int64_t i0,
-                   const int64_t* t, const int64_t* v, RowSink& S, int& err,
+                   const TT* t, const int64_t* v, RowSink& S, int& err,
                    int& nseg, int& cur_key, int& head_key, M& cur, M& head,
                    int nv = K) {
   if (nv <= 0) {
     nseg = 0;
     return true;
   }
-  int64_t tl = t[K - 1];
+  TT tl = t[K - 1];
   if (nv < K) {
 #pragma unroll
     for (int j = 0; j < K; ++j)
       if (j == nv - 1) tl = t[j];
   }
-  const int k0 = bucket_narrow(P, t[0]), k1 = bucket_narrow(P, tl);
+  const int k0 = tbucket_narrow(P, t[0]), k1 = tbucket_narrow(P, tl);
   if (k1 - k0 > 2) return false;
-  // starts of the tail bucket k1 and of the middle bucket k0+1 (INT64_MIN
-  // sends every point to the tail run)
-  const int64_t b_tail =
-      (k1 == k0) ? INT64_MIN : P.gbase + (int64_t)k1 * P.interval;
-  const int64_t b_mid =
-      (k1 == k0 + 2) ? P.gbase + (int64_t)(k0 + 1) * P.interval : b_tail;
+  // starts of the tail bucket k1 and of the middle bucket k0+1 (the lowest
+  // time sends every point to the tail run)
+  const TT b_tail = (k1 == k0) ? tmin<TT>() : tstart_fixed(P, k1, TT{});
+  const TT b_mid =
+      (k1 == k0 + 2) ? tstart_fixed(P, (int64_t)k0 + 1, TT{}) : b_tail;
   M h = M::init(), m = M::init(), c = M::init();
   bool any_mid = false;
   if (__ballot(k1 == k0 + 2) == 0) {
@@ -525,20 +556,20 @@ DEV bool fold_fast(const Params& P, const BatchDev& B, int sf, int64_t i0,
 // Folds the K points of one lane in order: the first run (which may continue
 // from the previous lane) goes to `head`, the last run (which may continue
 // into the next lane) stays in `cur`, runs in between close here.
-template <class M, int K, bool FLOATONLY, bool CHECKED>
+template <class M, int K, bool FLOATONLY, bool CHECKED, class TT = int64_t>
 DEV void fold_lane(const Params& P, const BatchDev& B, int sf, int64_t i0,
-                   int64_t lo, int64_t hi, const int64_t* t, const int64_t* v,
+                   int64_t lo, int64_t hi, const TT* t, const int64_t* v,
                    RowSink& S, int& err, int& nseg,
                    int& cur_key, int& head_key, M& cur, M& head) {
-  int64_t bnd = INT64_MIN;  // first timestamp past cur_key's bucket
+  TT bnd = tmin<TT>();  // first timestamp past cur_key's bucket
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     const int64_t i = i0 + j;
     if (CHECKED && (i < lo || i >= hi)) continue;
     int k = cur_key;
     if (nseg == 0 || t[j] >= bnd) {
-      k = (int)bucket_of(P, t[j]);
-      bnd = P.run_all ? INT64_MAX : bucket_ts(P, (int64_t)k + 1);
+      k = (int)tbucket(P, t[j]);
+      bnd = tbound(P, (int64_t)k + 1, TT{});
     }
     const double x = FLOATONLY ? bits_to_double(v[j]) : point_value(B, i, v[j], sf);
     if (nseg == 0) {
@@ -584,9 +615,9 @@ DEV void seg_scan_dpp(int key, M& st) {
 // of every lane (points i0 .. i0+K-1 of the series, step base `base`):
 // lane-local fold, the previous step's open bucket, the segmented wave scan
 // over the lanes' tail runs, the row writes and the new carry.
-template <class M, int K, int DPP>
+template <class M, int K, int DPP, class TT = int64_t>
 DEV void reduce_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
-                     int64_t hi, int64_t base, int64_t i0, const int64_t* t,
+                     int64_t hi, int64_t base, int64_t i0, const TT* t,
                      const int64_t* v, RowSink& S, int& err,
                      int& carry_key, M& carry, bool keep_open = false) {
   constexpr int PTS = 64 * K;
@@ -605,26 +636,30 @@ DEV void reduce_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
     const int64_t nr = hi - i0;
     const int nv = full ? K : (int)(nr < 0 ? 0 : (nr > K ? K : nr));
     if (P.narrow) {
-      done = fonly ? fold_fast<M, K, true>(P, B, sf, i0, t, v, S, err, nseg,
-                                           cur_key, head_key, cur, head, nv)
-                   : fold_fast<M, K, false>(P, B, sf, i0, t, v, S, err, nseg,
-                                            cur_key, head_key, cur, head, nv);
+      done = fonly
+                 ? fold_fast<M, K, true, TT>(P, B, sf, i0, t, v, S, err, nseg,
+                                             cur_key, head_key, cur, head, nv)
+                 : fold_fast<M, K, false, TT>(P, B, sf, i0, t, v, S, err,
+                                              nseg, cur_key, head_key, cur,
+                                              head, nv);
     }
     if (!done) {
       if (full && fonly)
-        fold_lane<M, K, true, false>(P, B, sf, i0, lo, hi, t, v, S,
-                                     err, nseg, cur_key, head_key, cur, head);
+        fold_lane<M, K, true, false, TT>(P, B, sf, i0, lo, hi, t, v, S,
+                                         err, nseg, cur_key, head_key, cur,
+                                         head);
       else if (full)
-        fold_lane<M, K, false, false>(P, B, sf, i0, lo, hi, t, v, S,
-                                      err, nseg, cur_key, head_key, cur,
-                                      head);
+        fold_lane<M, K, false, false, TT>(P, B, sf, i0, lo, hi, t, v, S,
+                                          err, nseg, cur_key, head_key, cur,
+                                          head);
       else
-        fold_lane<M, K, false, true>(P, B, sf, i0, lo, hi, t, v, S,
-                                     err, nseg, cur_key, head_key, cur, head);
+        fold_lane<M, K, false, true, TT>(P, B, sf, i0, lo, hi, t, v, S,
+                                         err, nseg, cur_key, head_key, cur,
+                                         head);
     }
   } else {
-    fold_lane<M, K, false, true>(P, B, sf, i0, lo, hi, t, v, S,
-                                 err, nseg, cur_key, head_key, cur, head);
+    fold_lane<M, K, false, true, TT>(P, B, sf, i0, lo, hi, t, v, S,
+                                     err, nseg, cur_key, head_key, cur, head);
   }
   if (nseg == 0) {  // lane wholly before lo (first step) or past hi
     cur_key = (i0 < lo) ? -1 : INT32_MAX;
