@@ -13,7 +13,7 @@ run_pass() {  # name counters...
   timeout -s KILL 150 rocprofv3 --pmc "$@" --output-format csv \
     -d "$OUT/$name" -o "$name" -- \
     python3 -u bench.py --config "$CFG" --steps 2 --warmup 1 \
-    --no-cpu-baseline ${PMC_NO_DECODE---no-decode} ${PMC_BENCH_ARGS} \
+    --no-cpu-baseline --no-extra ${PMC_NO_DECODE---no-decode} ${PMC_BENCH_ARGS} \
     > "$OUT/$name.log" 2>&1
 }
 for p in ${PMC_PASSES:-sq fetch write}; do

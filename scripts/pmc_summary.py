@@ -22,13 +22,24 @@ def short(name):
 
 
 def main(root):
-    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    # per kernel, only the dispatches of its largest grid: the bench's
+    # secondary figures launch the same kernels at smaller sizes, which
+    # would skew the per-launch mean of the workload's own dispatches
+    rows = []
     for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"),
                           recursive=True):
         with open(path) as f:
-            for row in csv.DictReader(f):
-                k = row.get("Kernel_Name", "")
-                acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+            rows.extend(csv.DictReader(f))
+    grid = collections.defaultdict(int)
+    for row in rows:
+        k = row.get("Kernel_Name", "")
+        grid[k] = max(grid[k], int(row.get("Grid_Size") or 0))
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for row in rows:
+        k = row.get("Kernel_Name", "")
+        if int(row.get("Grid_Size") or 0) != grid[k]:
+            continue
+        acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     out = {}
     for k, cs in acc.items():
         if ("bucketize" not in k and "k_fold" not in k
@@ -43,9 +54,8 @@ def main(root):
         out[k[:160]] = d
     # the figure bench.py reports as roofline.traffic: HBM bytes (read,
     # corrected, + written) per launch of the dominant kernel (the most
-    # dispatched downsample / fold variant)
-    best_k = max(out, key=lambda k: (out[k].get("dispatches", 0),
-                                     out[k].get("FETCH_SIZE", 0)), default=None)
+    # downsample / fold variant moving the most bytes)
+    best_k = max(out, key=lambda k: out[k].get("FETCH_SIZE", 0), default=None)
     best = out.get(best_k, {})
     if "hbm_read_bytes_corrected" in best and "hbm_write_bytes" in best:
         out = {"hbm_bytes_per_launch":
