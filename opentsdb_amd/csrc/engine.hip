@@ -1672,7 +1672,7 @@ otsdb_status compact_impl(otsdb_ctx* c, const otsdb_raw_rows* raw, int fix,
   for (int64_t* a : {gen_n, out_q, out_v, kept})
     HIP_TRY(hipMemsetAsync(a + R, 0, 8, st));
   if (R > 0)
-    hipLaunchKernelGGL(k_rows_plan, dim3(blocks_for(R, 4)), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_rows_plan, dim3(blocks_for(R, 256)), dim3(256), 0, st,
                        D, fix, kind, lone, gen_n, out_q, out_v, kept, first_err,
                        LS);
   HIP_TRY(hipGetLastError());
@@ -1713,8 +1713,32 @@ otsdb_status compact_impl(otsdb_ctx* c, const otsdb_raw_rows* raw, int fix,
   *n_out = nk;
   if (qbytes) *qbytes = tq;
   if (vbytes) *vbytes = tv;
+  int bytes = 1;
   if (own >= 0) {
-    if ((rc = cells_buffer(c, own, nk, tq, tv, owned))) return rc;
+    if ((rc = cells_buffer(c, own, nk, 0, 0, owned))) return rc;
+    // an engine-owned output aliases the input pools when it can
+    // (k_rows_alias): the common scan of single compacted columns moves no
+    // value bytes
+    unsigned long long* acc = LS.ctr + 2;  // 5 words after the counters
+    const unsigned long long init[5] = {~0ULL, 0ULL, ~0ULL, 0ULL, 0ULL};
+    HIP_TRY(hipMemcpyAsync(acc, init, sizeof(init), hipMemcpyHostToDevice, st));
+    if (R > 0)
+      hipLaunchKernelGGL(k_rows_alias,
+                         dim3((unsigned)std::min<int64_t>(blocks_for(R, 256), 2048)),
+                         dim3(256), 0, st, D, (const uint8_t*)kind,
+                         (const int64_t*)lone, (const int64_t*)oq_off,
+                         (const int64_t*)ov_off, acc);
+    HIP_TRY(hipGetLastError());
+    unsigned long long h[5];
+    HIP_TRY(hipMemcpyAsync(h, acc, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (nk > 0 && h[4] == 0 && h[0] == h[1] && h[2] == h[3]) {
+      bytes = 0;
+      owned->qual = const_cast<uint8_t*>(raw->qual) + h[0];
+      owned->val = const_cast<uint8_t*>(raw->val) + h[2];
+    } else if ((rc = cells_buffer(c, own, nk, tq, tv, owned))) {
+      return rc;
+    }
     o = owned;
     qcap = tq;
     vcap = tv;
@@ -1732,7 +1756,14 @@ otsdb_status compact_impl(otsdb_ctx* c, const otsdb_raw_rows* raw, int fix,
   const uint8_t* stq = ncell ? (uint8_t*)c->rows_scr + recb : nullptr;
   const uint8_t* stv = ncell ? stq + qb : nullptr;
   (void)rec;
-  if (R > 0 && nk > 0) {
+  if (R > 0 && nk > 0 && !bytes) {
+    hipLaunchKernelGGL(k_rows_meta, dim3(blocks_for(R, 256)), dim3(256), 0, st,
+                       R, raw->row_series, raw->row_base_s, (const uint8_t*)kind,
+                       (const int64_t*)oq_off, (const int64_t*)ov_off,
+                       (const int64_t*)k_off, o->row_series, o->row_base_s,
+                       o->qual_off, o->val_off);
+    HIP_TRY(hipGetLastError());
+  } else if (R > 0 && nk > 0) {
     // row_series is optional on the output
     hipLaunchKernelGGL(k_rows_write, dim3(blocks_for(R, 4)), dim3(256), 0, st,
                        D, fix, raw->row_series, raw->row_base_s,

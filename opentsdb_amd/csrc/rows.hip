@@ -424,15 +424,25 @@ DEV LoneOut lone_walk(const RawDev& D, int64_t c, int fix, uint8_t* oq,
   return o;
 }
 
+// The common LONE column, decided without the walk (k_rows_plan): every
+// qualifier has the width of the first (no MS_MIXED_COMPACT), time offsets
+// strictly increase (no repeated offset for the one-iterator heap to merge),
+// the value lengths add up to the column's value bytes less the meta byte,
+// and the meta byte is the 0 buildCompactedColumn writes for one resolution
+// (CompactionQueue.java:594-616).  Such a column is what a TSD compaction
+// wrote, and the merge rebuilds it byte for byte: VERBATIM.  Anything else
+// is decided by lone_walk's exact replay.  One 16-byte qualifier load per
+// lane (8 second or 4 ms qualifiers), 1 KB of qualifiers per pass.
+
 // ---------------------------------------------------------------- planning
-__global__ __launch_bounds__(256) void k_rows_plan(
-    RawDev D, int fix, uint8_t* __restrict__ kind, int64_t* __restrict__ lone,
-    int64_t* __restrict__ gen_n, int64_t* __restrict__ out_q,
-    int64_t* __restrict__ out_v, int64_t* __restrict__ kept,
-    unsigned long long* first_err, LargeSlots LS) {
+// The exact plan of one row (wave-level): column classification, the lone
+// column's one-iterator replay, GENERAL / LARGE cell counts.
+DEV void plan_row(const RawDev& D, int fix, int64_t r, uint8_t* __restrict__ kind,
+                  int64_t* __restrict__ lone, int64_t* __restrict__ gen_n,
+                  int64_t* __restrict__ out_q, int64_t* __restrict__ out_v,
+                  int64_t* __restrict__ kept, unsigned long long* first_err,
+                  const LargeSlots& LS) {
   const int lane = LANE;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= D.R) return;
   const int64_t c0 = D.row_col_off[r], c1 = D.row_col_off[r + 1];
   int64_t n_data = 0, cells = 0, first_c = -1;
   int first_type = CT_SKIP, first_fixed = 0, merge_bad = 0;
@@ -455,9 +465,13 @@ __global__ __launch_bounds__(256) void k_rows_plan(
     }
     n_data += __popcll(dm);
     cells += wave_sum_l(ci.type == CT_ONE || ci.type == CT_APPEND ? ci.cells : 0);
+  }
+  // multi-point columns of GENERAL rows: counted by a wave walk (a lone
+  // column is decided below, by lone_uniform or lone_walk)
+  for (int64_t cc = c0; !err && n_data > 1 && cc < c1; cc += 64) {
+    const int64_t c = cc + lane;
+    const ColInfo ci = c < c1 ? col_info(D, c) : ColInfo{CT_SKIP, 0, 0, 0};
     uint64_t mm = __ballot(ci.type == CT_MULTI);
-    // multi-point columns: counted by a wave walk (GENERAL rows only need
-    // the count; a lone column is walked below)
     while (mm) {
       const int b = __builtin_ctzll(mm);
       mm &= mm - 1;
@@ -534,6 +548,171 @@ __global__ __launch_bounds__(256) void k_rows_plan(
     return;
   }
   put(RK_GENERAL, 0, 0, cells);
+}
+
+// One 1 KB pass of a uniform-width column's qualifiers (this lane's 16
+// bytes w[], nb of them valid): widths, strictly increasing offsets across
+// lanes and from the previous pass (carry), value lengths.
+DEV void uniform_pass(const uint32_t* w, int nb, int qw, int32_t& carry,
+                      int& bad, int32_t& vsum) {
+  const int lane = LANE;
+  int32_t first = INT32_MAX, last = -1;
+  if (qw == 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (2 * j < nb) {
+        const uint32_t h = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFF;
+        const uint32_t qv = ((h & 0xFF) << 8) | (h >> 8);
+        const int32_t o = (int32_t)(qv >> 4);
+        bad |= (qv >> 12) == 0xF;  // an ms qualifier starts here
+        bad |= o <= last;
+        first = j == 0 ? o : first;
+        last = o;
+        vsum += (int32_t)(qv & 0x7) + 1;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (4 * j < nb) {
+        const uint32_t qv = __builtin_bswap32(w[j]);
+        const int32_t o = (int32_t)((qv & 0x0FFFFFC0u) >> 6);
+        bad |= (qv >> 28) != 0xF;  // a second qualifier starts here
+        bad |= o <= last;
+        first = j == 0 ? o : first;
+        last = o;
+        vsum += (int32_t)(qv & 0x7) + 1;
+      }
+    }
+  }
+  const int32_t pl = __shfl_up(last, 1);
+  const int32_t prev = lane == 0 ? carry : pl;
+  if (nb > 0 && first <= prev) bad = 1;
+  const uint64_t live = __ballot(nb > 0);
+  carry = __shfl(last, live ? 63 - __builtin_clzll(live) : 0);
+}
+
+// this lane's 16 qualifier bytes of a pass at byte a of a column of ql bytes
+// at qb (16-byte loads at any byte offset; byte loads at the pool's end)
+DEV int uniform_load(const uint8_t* qual, int64_t qb, int64_t ql, int64_t a,
+                     int64_t qend, uint32_t* w) {
+  w[0] = w[1] = w[2] = w[3] = 0;
+  const int nb = a >= ql ? 0 : (int)(ql - a < 16 ? ql - a : 16);
+  if (nb == 16 && qb + a + 16 <= qend) {
+    const uint4 x = *reinterpret_cast<const uint4*>(qual + qb + a);
+    w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+  } else {
+    for (int i = 0; i < nb; ++i)
+      w[i >> 2] |= (uint32_t)qual[qb + a + i] << (8 * (i & 3));
+  }
+  return nb;
+}
+
+// k_rows_plan: one wavefront per 64 rows.  Lanes read their rows' shapes
+// (thread per row); single compacted columns the merge would rebuild byte
+// for byte (lone_uniform's conditions) are decided VERBATIM by the wave
+// with four rows' qualifier passes in flight at a time; every other row
+// takes the exact plan (plan_row), one at a time.
+__global__ __launch_bounds__(256) void k_rows_plan(
+    RawDev D, int fix, uint8_t* __restrict__ kind, int64_t* __restrict__ lone,
+    int64_t* __restrict__ gen_n, int64_t* __restrict__ out_q,
+    int64_t* __restrict__ out_v, int64_t* __restrict__ kept,
+    unsigned long long* first_err, LargeSlots LS) {
+  const int lane = LANE;
+  const int64_t rb = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+  if (rb >= D.R) return;
+  const int64_t r = rb + lane;
+  const int64_t qend = D.col_qoff[D.row_col_off[D.R]];
+  bool cand = false;
+  int64_t c0 = 0, qb = 0, ql = 0, vl = 0;
+  int qw = 2;
+  if (r < D.R) {
+    c0 = D.row_col_off[r];
+    if (D.row_col_off[r + 1] - c0 == 1) {
+      qb = D.col_qoff[c0];
+      ql = D.col_qoff[c0 + 1] - qb;
+      const int64_t vb = D.col_voff[c0];
+      vl = D.col_voff[c0 + 1] - vb;
+      if (ql >= 4 && !(ql & 1) && vl >= 2) {
+        qw = (D.qual[qb] & 0xF0) == 0xF0 ? 4 : 2;
+        cand = !(ql & (qw - 1)) && ql >= 2 * qw && D.val[vb + vl - 1] == 0;
+      }
+    }
+  }
+  uint64_t done = 0;
+  uint64_t small = __ballot(cand && ql <= 1024);
+  uint64_t large = __ballot(cand && ql > 1024);
+  while (small) {  // four one-pass rows per round
+    int js[4];
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      js[i] = small ? __builtin_ctzll(small) : -1;
+      if (small) {
+        small &= small - 1;
+        ++k;
+      }
+    }
+    uint32_t w[4][4];
+    int nb[4], qwk[4];
+    int64_t vlk[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      nb[i] = 0;
+      qwk[i] = 2;
+      vlk[i] = 0;
+      w[i][0] = w[i][1] = w[i][2] = w[i][3] = 0;
+      if (i < k) {
+        const int64_t b = readlane_l(qb, js[i]), l = readlane_l(ql, js[i]);
+        qwk[i] = __builtin_amdgcn_readlane(qw, js[i]);
+        vlk[i] = readlane_l(vl, js[i]);
+        nb[i] = uniform_load(D.qual, b, l, 16 * lane, qend, w[i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i < k) {
+        int32_t carry = -1, vsum = 0;
+        int bad = 0;
+        uniform_pass(w[i], nb[i], qwk[i], carry, bad, vsum);
+        vsum = (int32_t)wave_sum_l(vsum);
+        if (!__ballot(bad) && (int64_t)vsum + 1 == vlk[i])
+          done |= 1ULL << js[i];
+      }
+    }
+  }
+  while (large) {  // multi-pass rows (long ms columns), one at a time
+    const int j = __builtin_ctzll(large);
+    large &= large - 1;
+    const int64_t b = readlane_l(qb, j), l = readlane_l(ql, j);
+    const int q = __builtin_amdgcn_readlane(qw, j);
+    int32_t carry = -1;
+    int32_t vsum = 0;
+    int bad = 0;
+    for (int64_t p = 0; p < l && !bad; p += 1024) {
+      uint32_t w[4];
+      const int nb = uniform_load(D.qual, b, l, p + 16 * lane, qend, w);
+      uniform_pass(w, nb, q, carry, bad, vsum);
+      bad = __ballot(bad) != 0;
+    }
+    vsum = (int32_t)wave_sum_l(vsum);
+    if (!bad && (int64_t)vsum + 1 == readlane_l(vl, j)) done |= 1ULL << j;
+  }
+  if ((done >> lane) & 1) {
+    kind[r] = RK_VERBATIM;
+    lone[r] = c0;
+    gen_n[r] = 0;
+    out_q[r] = ql;
+    out_v[r] = vl;
+    kept[r] = 1;
+  }
+  uint64_t rest = __ballot(r < D.R) & ~done;
+  while (rest) {
+    const int j = __builtin_ctzll(rest);
+    rest &= rest - 1;
+    plan_row(D, fix, rb + j, kind, lone, gen_n, out_q, out_v, kept, first_err,
+             LS);
+  }
 }
 
 // ---------------------------------------------------------- GENERAL rows
@@ -1205,6 +1384,83 @@ DEV void wave_copy(uint8_t* dst, const uint8_t* src, int64_t n) {
     *reinterpret_cast<uint4*>(dst + i) =
         *reinterpret_cast<const uint4*>(src + i);
   for (int64_t j = (n & ~(int64_t)15) + lane; j < n; j += 64) dst[j] = src[j];
+}
+
+// Can the compacted output alias the input pools?  Yes when every kept row
+// is VERBATIM and the kept columns sit in the input pools exactly as the
+// packed output would lay them out, at one byte shift per pool (a scanner's
+// rows of single compacted columns, back to back): acc[0..1] min / max of
+// the qualifier shift, acc[2..3] of the value shift, acc[4] != 0 when some
+// kept row is not VERBATIM.  One thread per row.
+__global__ __launch_bounds__(256) void k_rows_alias(
+    RawDev D, const uint8_t* __restrict__ kind, const int64_t* __restrict__ lone,
+    const int64_t* __restrict__ oq_off, const int64_t* __restrict__ ov_off,
+    unsigned long long* acc) {
+  // grid-stride over the rows, reduced per workgroup: one set of atomics per
+  // workgroup (same-address atomics from every wave serialise)
+  int64_t dq = INT64_MAX, dv = INT64_MAX, eq = INT64_MIN, ev = INT64_MIN;
+  int other = 0;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < D.R;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t kd = kind[r];
+    if (kd == RK_VERBATIM) {
+      const int64_t c = lone[r];
+      const int64_t x = D.col_qoff[c] - oq_off[r], y = D.col_voff[c] - ov_off[r];
+      dq = min(dq, x);
+      eq = max(eq, x);
+      dv = min(dv, y);
+      ev = max(ev, y);
+    } else if (kd != RK_EMPTY) {
+      other = 1;
+    }
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    dq = min(dq, (int64_t)__shfl_xor(dq, d));
+    dv = min(dv, (int64_t)__shfl_xor(dv, d));
+    eq = max(eq, (int64_t)__shfl_xor(eq, d));
+    ev = max(ev, (int64_t)__shfl_xor(ev, d));
+    other |= __shfl_xor(other, d);
+  }
+  __shared__ int64_t red[4][5];
+  const int wv = threadIdx.x >> 6;
+  if (LANE == 0) {
+    red[wv][0] = dq; red[wv][1] = eq; red[wv][2] = dv; red[wv][3] = ev;
+    red[wv][4] = other;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) {
+      dq = min(dq, red[i][0]); eq = max(eq, red[i][1]);
+      dv = min(dv, red[i][2]); ev = max(ev, red[i][3]);
+      other |= (int)red[i][4];
+    }
+    // shifts are >= 0: the output packs a subset of the input in order
+    if (dq != INT64_MAX) {
+      atomicMin(&acc[0], (unsigned long long)dq);
+      atomicMax(&acc[1], (unsigned long long)eq);
+      atomicMin(&acc[2], (unsigned long long)dv);
+      atomicMax(&acc[3], (unsigned long long)ev);
+    }
+    if (other) atomicOr(&acc[4], 1ULL);
+  }
+}
+
+// The per-row arrays of an aliased output (thread per row; no bytes move).
+__global__ __launch_bounds__(256) void k_rows_meta(
+    int64_t R, const int64_t* __restrict__ row_series,
+    const int64_t* __restrict__ row_base_s, const uint8_t* __restrict__ kind,
+    const int64_t* __restrict__ oq_off, const int64_t* __restrict__ ov_off,
+    const int64_t* __restrict__ k_off, int64_t* __restrict__ o_series,
+    int64_t* __restrict__ o_base, int64_t* __restrict__ o_qoff,
+    int64_t* __restrict__ o_voff) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R || kind[r] == RK_EMPTY) return;
+  const int64_t k = k_off[r];
+  if (o_series) o_series[k] = row_series ? row_series[r] : 0;
+  o_base[k] = row_base_s[r];
+  o_qoff[k] = oq_off[r];
+  o_voff[k] = ov_off[r];
 }
 
 __global__ __launch_bounds__(256) void k_rows_write(

@@ -124,6 +124,111 @@ def test_compaction_fuzz_errors_match_oracle(engine, seed):
     assert n_err > 5 and n_ok > 5
 
 
+def _uniform_rows(rng, n_rows):
+    """Single-column rows of compacted columns, mostly what a TSD compaction
+    writes (one qualifier width, strictly increasing offsets, meta 0) — the
+    k_rows_plan fast path — and near misses it must hand to the exact walk:
+    a meta byte of 1, a repeated offset, two offsets swapped, one ms point in
+    a seconds column, a value byte too many; long ms columns (thousands of
+    points, several 1 KB qualifier passes) and short ones."""
+    rows = []
+    for i in range(n_rows):
+        ms = rng.random() < 0.4
+        n = int(rng.choice([2, 3, 7, 8, 9, 63, 64, 65, 360, 511, 512, 513,
+                            2000, 4100])) if ms else int(rng.integers(2, 361))
+        if ms:
+            offs = np.sort(rng.choice(3600000, size=n, replace=False))
+        else:
+            offs = np.sort(rng.choice(3600, size=n, replace=False)) * 1000
+        kind = int(rng.integers(0, 6))
+        cs = [rows_fuzz.cell(rng, int(o), ms, rows_fuzz.enc_value(rng, kind))
+              for o in offs]
+        miss = int(rng.integers(0, 8))
+        meta = None
+        if miss == 1:
+            meta = 1
+        elif miss == 2 and n > 2:
+            cs[2] = rows_fuzz.cell(rng, int(offs[1]), ms, rows_fuzz.enc_value(rng, kind))
+        elif miss == 3 and n > 3:
+            cs[1], cs[2] = cs[2], cs[1]
+        elif miss == 4 and not ms and n > 4:
+            cs[3] = rows_fuzz.cell(rng, int(offs[3]) + 1, True,
+                                   rows_fuzz.enc_value(rng, kind))
+        q, v = rows_fuzz.compacted(cs, meta)
+        if miss == 5:
+            v = v[:-1] + b"\x07" + v[-1:]
+        rows.append((i, rows_fuzz.BASE + 3600 * (i % 7), [(q, v, 0)]))
+    return rows
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_compaction_uniform_columns(engine, seed):
+    """Compacted single-column rows through the fast uniform check and the
+    exact walk (fix_duplicates on, and off on rows without a repeated
+    offset): the bytes equal the oracle's, or both raise."""
+    rng = np.random.default_rng(seed)
+    rows = _uniform_rows(rng, 300)
+    for fix in (True, False):
+        ok, bad = [], []
+        for r in rows:
+            try:
+                _oracle_rows([r], fix)
+                ok.append(r)
+            except pyoracle.OracleError:
+                bad.append(r)
+        got = _gpu_compact(engine, ok, fix)
+        assert got == _oracle_rows(ok, fix)
+        for r in bad[:20]:
+            with pytest.raises((core.IllegalDataException,
+                                core.IllegalArgumentException)):
+                _gpu_compact(engine, [r], fix)
+
+
+@pytest.mark.parametrize("breaker", [None, "annotation", "merge"])
+def test_query_from_storage_rows_aliasing(engine, breaker):
+    """Storage rows of back-to-back single compacted columns (what a scan of
+    compacted data returns): the compacted output aliases the input pools
+    and no value byte moves; with an annotation column in between, or one
+    row that needs a merge, it is packed instead.  Either way the query
+    equals the oracle's over the same points."""
+    import torch
+    from opentsdb_amd.engine import DeviceResult
+    from tests.test_gpu_parity import compare
+    from tests.test_gpu_decode import _device_batch, _result_points
+    from tests import cells as C
+    rng = np.random.default_rng(5)
+    hb = datasets.random_batch(47, n_series=24, n_groups=4, span_ms=5 * 3600000,
+                               cadence_ms=10000)
+    hb.ts[:] = hb.ts - hb.ts % 1000
+    hb.is_float = np.ones(len(hb.ts), np.uint8)
+    rows = []
+    for s in range(hb.n_series):
+        a, b = hb.offsets[s], hb.offsets[s + 1]
+        for base, q, v in C.encode_series(hb.ts[a:b], hb.val[a:b],
+                                          hb.is_float[a:b]):
+            cols = [(q, v, 0)]
+            if breaker == "annotation" and len(rows) == 40:
+                cols = [(bytes([1, 0, 0]), b'{"a":1}', 1)] + cols
+            rows.append((s, base, cols))
+    if breaker == "merge":  # split one row into two columns
+        s, base, cols = rows[40]
+        pts = rows_fuzz.split_points(cols[0][0], cols[0][1])
+        h = len(pts) // 2
+        rows[40] = (s, base, [rows_fuzz.compacted(pts[:h]) + (0,),
+                              rows_fuzz.compacted(pts[h:]) + (1,)])
+    raw = storage.HostRawRows(rows, with_ts=True).to_device()
+    raw.n_series = hb.n_series
+    db = _device_batch(hb, "float")
+    t0, t1 = datasets.T0 + 600000, datasets.T0 + 5 * 3600000
+    spec = core.make_spec(t0, t1, core.Aggregators.get("sum"),
+                          core.DownsamplingSpecification("1m-avg"), t0, t1)
+    ref = pyoracle.group_by(spec, hb)
+    res = DeviceResult(torch, db.n_groups, 4 * len(hb.ts) + 64, "cuda")
+    storage.run_raw_device(engine, spec, raw, db, res)
+    compare(_result_points(res, db.n_groups), ref, False,
+            where="alias/%s" % breaker)
+
+
 def test_compaction_first_failing_row_decides(engine):
     """The first failing row in row order decides the exception (the
     scanner compacts rows in order)."""
