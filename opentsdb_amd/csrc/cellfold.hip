@@ -313,17 +313,6 @@ DEV uint32_t cells_pick(const uint32_t* t, int32_t rel) {
   return (uint32_t)__builtin_amdgcn_readlane((int)x, L);
 }
 
-DEV int wave_excl_scan(int x, int& total) {
-  int incl = x;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(incl, d);
-    if (LANE >= d) incl += y;
-  }
-  total = __shfl(incl, 63);
-  return incl - x;
-}
-
 // One member's points [pa, pb) straight from its compacted columns (the
 // cells counterpart of fold_member; NW == 1, so no window context).  The
 // grid is narrow (run_pipeline sends other grids to k_bucketize_cells):

@@ -60,6 +60,18 @@ DEV int64_t value_bits(uint64_t x, int vl, int fl) {
   }
 }
 
+// exclusive wave prefix sum of x; total = the wave's sum
+DEV int wave_excl_scan(int x, int& total) {
+  int incl = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(incl, d);
+    if (LANE >= d) incl += y;
+  }
+  total = __shfl(incl, 63);
+  return incl - x;
+}
+
 // Fast path of one column whose qualifiers all have the width of the first
 // (the common case: no MS_MIXED_COMPACT) — point i's qualifier is at
 // qw * i, no start-recurrence scan — and, for the write, whose values all
@@ -152,7 +164,10 @@ __global__ __launch_bounds__(256) void k_decode(
     }
     return;
   }
-  if (qlen > 0) {
+  // a multi-value column whose meta byte says seconds and ms are mixed
+  // (RowSeq.java:338-356) goes straight to the generic walk (the flag only
+  // steers; the walk validates either way)
+  if (qlen > 0 && !(qlen > 4 && vlen > 0 && (v[vlen - 1] & 1))) {
     int fbad = 0;
     if (decode_uniform(C, r, mode, q, qlen, C.val_off[r], vlen, base_ms,
                        row_count, row_out, fast, cap, ts, val, isf, fbad)) {
@@ -161,87 +176,116 @@ __global__ __launch_bounds__(256) void k_decode(
     }
   }
   if (mode == 0 && lane == 0) fast[r] = 0;
+  // Generic column (qualifier widths mixed, MS_MIXED_COMPACT): 8 two-byte
+  // units per lane, 512 per pass.  Each lane composes its units' maps
+  // start(u+1) = !(start(u) && ms(u)) sequentially, one wave scan of the
+  // lanes' maps gives every lane its entry state, the lane then walks its
+  // units; point counts and value offsets are lane prefix sums + wave scans.
   const int64_t units = qlen >> 1;
+  const int64_t vend = C.val_off[C.R];
+  const int64_t vb0 = C.val_off[r];
   int carry_start = 1;
-  int64_t carry_n = 0, carry_voff = 0;
+  int32_t carry_n = 0;
+  int64_t carry_voff = 0;
   int bad = 0;
   const int64_t out0 = mode ? row_out[r] : 0;
-  for (int64_t u0 = 0; u0 < units; u0 += 64) {
-    const int64_t u = u0 + lane;
-    const bool in = u < units;
-    const uint8_t b0 = in ? q[2 * u] : 0;
-    const int ms = in && ((b0 & 0xF0) == 0xF0);
-    // f_u(s) = !(s && ms_u)
-    int f = in ? (ms ? 0x1 : 0x3) : 0x2;  // identity for lanes past the row
-    int F = f;                               // inclusive composition
+  for (int64_t u0 = 0; u0 < units; u0 += 512) {
+    const int64_t ub = u0 + 8 * lane;
+    const int nu = ub >= units ? 0 : (int)(units - ub < 8 ? units - ub : 8);
+    // the lane's 16 bytes and the 4 after them (a 4-byte qualifier may
+    // start at the lane's last unit)
+    uint32_t w[5] = {0, 0, 0, 0, 0};
+    if (2 * ub + 20 <= qlen) {
+      const uint4 x = *reinterpret_cast<const uint4*>(q + 2 * ub);
+      w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+      w[4] = *reinterpret_cast<const uint32_t*>(q + 2 * ub + 16);
+    } else if (nu > 0) {
+      for (int i = 0; i < 20; ++i)
+        if (2 * ub + i < qlen) w[i >> 2] |= (uint32_t)q[2 * ub + i] << (8 * (i & 3));
+    }
+    auto byte_at = [&](int k) { return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu; };
+    int F = 0x2;  // identity
+    uint32_t msb = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int ms = i < nu && (byte_at(2 * i) & 0xF0) == 0xF0;
+      msb |= (uint32_t)ms << i;
+      if (i < nu) F = fmap_compose(ms ? 0x1 : 0x3, F);
+    }
+    int G = F;  // inclusive composition over the lanes
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-      const int g = __shfl_up(F, d);
-      if (lane >= d) F = fmap_compose(F, g);
+      const int g = __shfl_up(G, d);
+      if (lane >= d) G = fmap_compose(G, g);
     }
-    int Fex = __shfl_up(F, 1);
-    if (lane == 0) Fex = 0x2;  // identity
-    const int start = in && fmap_apply(Fex, carry_start);
-    // a 4-byte qualifier must fit in the row
-    if (start && ms && u + 1 >= units) bad = 1;
-    uint32_t qv = 0;
-    int vl = 0;
-    if (start) {
-      if (ms) {
-        if (u + 1 < units)
-          qv = ((uint32_t)b0 << 24) | ((uint32_t)q[2 * u + 1] << 16) |
-               ((uint32_t)q[2 * u + 2] << 8) | (uint32_t)q[2 * u + 3];
-      } else {
-        qv = ((uint32_t)b0 << 8) | (uint32_t)q[2 * u + 1];
+    int Gex = __shfl_up(G, 1);
+    if (lane == 0) Gex = 0x2;
+    int st = fmap_apply(Gex, carry_start);
+    // the lane's points: starts, qualifiers, value lengths
+    uint32_t startm = 0;
+    int np = 0, vs = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i < nu && st) {
+        startm |= 1u << i;
+        const int ms = (msb >> i) & 1;
+        if (ms && ub + i + 1 >= units) bad = 1;  // cut by the column end
+        const uint32_t qv =
+            ms ? (byte_at(2 * i) << 24) | (byte_at(2 * i + 1) << 16) |
+                     (byte_at(2 * i + 2) << 8) | byte_at(2 * i + 3)
+               : (byte_at(2 * i) << 8) | byte_at(2 * i + 1);
+        const int vl = (int)(qv & 0x7) + 1;
+        if (qv & 0x8) bad |= !(vl == 4 || vl == 8);
+        else bad |= !(vl == 1 || vl == 2 || vl == 4 || vl == 8);
+        ++np;
+        vs += vl;
       }
-      vl = (int)(qv & 0x7) + 1;
-      // RowSeq.extractIntegerValue / extractFloatingPointValue lengths
-      if (qv & 0x8) bad |= !(vl == 4 || vl == 8);
-      else bad |= !(vl == 1 || vl == 2 || vl == 4 || vl == 8);
+      if (i < nu) st = !(st && ((msb >> i) & 1));
     }
-    // exclusive scans: point index and value offset
-    const uint64_t sm = __ballot(start);
-    const int64_t idx = carry_n + __popcll(sm & ((1ULL << lane) - 1));
-    int64_t vo = vl;
+    int tn, tv;
+    const int np_ex = wave_excl_scan(np, tn);
+    const int vs_ex = wave_excl_scan(vs, tv);
+    if (mode == 1 || vs > 0) {
+      int k = 0, vo = 0;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int64_t y = __shfl_up(vo, d);
-      if (lane >= d) vo += y;
-    }
-    const int64_t voff = carry_voff + vo - vl;
-    if (start && voff + vl > vlen) bad = 1;
-    if (mode == 1 && start && !bad) {
-      const int64_t o = out0 + idx;
-      if (o < cap) {
-        const uint8_t* p = v + voff;
-        int64_t t;
-        if (ms) t = base_ms + (int64_t)((qv & 0x0FFFFFC0u) >> 6);
-        else t = base_ms + (int64_t)((qv & 0xFFFFu) >> 4) * 1000;
-        int64_t bits = 0;
-        const int fl = (qv & 0x8) != 0;
-        uint64_t x = 0;
-        for (int i = 0; i < vl; ++i) x = (x << 8) | p[i];
-        if (!fl) {  // big-endian signed 1/2/4/8 bytes (RowSeq.java:233-245)
-          switch (vl) {
-            case 1: bits = (int8_t)x; break;
-            case 2: bits = (int16_t)x; break;
-            case 4: bits = (int32_t)x; break;
-            case 8: bits = (int64_t)x; break;
-            default: bad = 1;
+      for (int i = 0; i < 8; ++i) {
+        if ((startm >> i) & 1) {
+          const int ms = (msb >> i) & 1;
+          const uint32_t qv =
+              ms ? (byte_at(2 * i) << 24) | (byte_at(2 * i + 1) << 16) |
+                       (byte_at(2 * i + 2) << 8) | byte_at(2 * i + 3)
+                 : (byte_at(2 * i) << 8) | byte_at(2 * i + 1);
+          const int vl = (int)(qv & 0x7) + 1;
+          const int64_t voff = carry_voff + vs_ex + vo;
+          if (voff + vl > vlen) bad = 1;
+          if (mode == 1 && !bad) {
+            const int64_t o = out0 + carry_n + np_ex + k;
+            if (o < cap) {
+              const int64_t a = vb0 + voff;
+              uint64_t x;
+              if (a + 8 <= vend) {
+                x = __builtin_bswap64(*reinterpret_cast<const uint64_t*>(C.val + a));
+              } else {
+                x = 0;
+                for (int b = 0; b < 8; ++b)
+                  x = (x << 8) | (a + b < vend ? (uint64_t)C.val[a + b] : 0);
+              }
+              x >>= 64 - 8 * vl;
+              const int fl = (qv & 0x8) != 0;
+              ts[o] = ms ? base_ms + (int64_t)((qv & 0x0FFFFFC0u) >> 6)
+                         : base_ms + (int64_t)((qv & 0xFFFFu) >> 4) * 1000;
+              val[o] = value_bits(x, vl, fl);
+              isf[o] = (uint8_t)fl;
+            }
           }
-        } else {    // float widened / double (RowSeq.java:256-266)
-          if (vl == 4) bits = __double_as_longlong((double)__uint_as_float((uint32_t)x));
-          else if (vl == 8) bits = (int64_t)x;
-          else bad = 1;
+          ++k;
+          vo += vl;
         }
-        ts[o] = t;
-        val[o] = bits;
-        isf[o] = (uint8_t)fl;
       }
     }
-    carry_n += __popcll(sm);
-    carry_voff += __shfl(vo, 63);
-    carry_start = fmap_apply(__shfl(F, 63), carry_start);
+    carry_n += tn;
+    carry_voff += tv;
+    carry_start = fmap_apply(__shfl(G, 63), carry_start);
   }
   if (mode == 0) {
     // all value bytes consumed, the meta byte of multi-value columns aside

@@ -1365,10 +1365,13 @@ otsdb_status run_device_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
 
 // otsdb_decode_cells_device without the lock (also the fallback of the
 // fused cells query)
+// counted: an earlier call on the same cells (ts_ms null) left the row
+// counts, output offsets and uniform flags in the context's decode workspace
+// and the series offsets in `offsets`: only the write pass runs.
 otsdb_status decode_impl(otsdb_ctx* c, const otsdb_cells* cells,
                          int64_t n_series, int64_t* offsets, int64_t* ts_ms,
                          int64_t* val, uint8_t* is_float, int64_t capacity,
-                         hipStream_t st) {
+                         hipStream_t st, bool counted = false) {
   const int64_t R = cells->n_rows, S = n_series;
   if (R < 0 || S < 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "negative sizes");
   // workspace: row counts, row output offsets, uniform-column flags and the
@@ -1387,6 +1390,15 @@ otsdb_status decode_impl(otsdb_ctx* c, const otsdb_cells* cells,
   void* tmp = (void*)(((uintptr_t)(fast + R) + 63) & ~(uintptr_t)63);
   CellsDev C{R, cells->row_series, cells->row_base_s, cells->qual_off,
              cells->qual, cells->val_off, cells->val};
+  if (counted) {
+    if (R > 0)
+      hipLaunchKernelGGL(k_decode, dim3(blocks_for(R, 4)), dim3(256), 0, st, C,
+                         1, row_count, (const int64_t*)row_out, fast, capacity,
+                         ts_ms, val, is_float, c->d_err);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+    return OTSDB_OK;
+  }
   HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), st));
   if (R > 0) {
     hipLaunchKernelGGL(k_decode, dim3(blocks_for(R, 4)), dim3(256), 0, st, C,
@@ -1493,7 +1505,7 @@ otsdb_status run_cells_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
   int64_t* ts = (int64_t*)c->cells_col;
   int64_t* vv = (int64_t*)((char*)c->cells_col + col);
   uint8_t* isf = (uint8_t*)((char*)c->cells_col + 2 * col);
-  rc = decode_impl(c, cells, S, offs, ts, vv, isf, N, st);
+  rc = decode_impl(c, cells, S, offs, ts, vv, isf, N, st, true);
   dec_tm.reset();
   if (rc) return rc;
   otsdb_batch cb = *b;
