@@ -487,6 +487,29 @@ def test_percentiles_fill_several_large_groups(engine):
             check(engine, spec, b2, True, where="selfill/%s/%s" % (agg, fill))
 
 
+@pytest.mark.parametrize("n_series,n_groups", [(150, 2), (333, 5)])
+def test_percentiles_fill_keys_fold_windows(engine, n_series, n_groups):
+    """Fill-mode percentiles with every group large over wide grids (6 h of
+    1 m / 10 s buckets: 360 / 2,160 of them) — the keys transpose's fill and
+    counts per (bucket, 64-member tile) with group boundaries inside tiles,
+    series that start late or end early (the fill before / after them), NaN
+    values, empty series (not kept): bit-exact with the oracle."""
+    b = datasets.random_batch(83 + n_series, n_series=n_series,
+                              n_groups=n_groups, span_ms=6 * 3600 * 1000,
+                              cadence_ms=20000, nan_frac=0.03,
+                              empty_frac=0.05)
+    end = datasets.T0 + 6 * 3600 * 1000
+    # order-free downsamplers: bit-exact; avg over 3 points a bucket: the
+    # downsample's lane-tree sums, within 1e-12
+    for agg, interval, ds in (("p99", "1m", "max"), ("median", "1m", "min"),
+                              ("p50", "10s", "first"), ("ep95r3", "1m", "max"),
+                              ("p99", "1m", "avg")):
+        for fill in ("nan", "zero"):
+            spec = _spec(agg, ds, fill, end=end, interval=interval)
+            check(engine, spec, b, ds != "avg", where="kfold%d/%s/%s/%s/%s" % (
+                n_series, agg, interval, ds, fill))
+
+
 def test_got_infinity(engine):
     """AggregationIterator.doubleValue throws on +-Infinity
     (AggregationIterator.java:640-643)."""
