@@ -10,6 +10,9 @@
 #ifndef OTSDB_CELLS_WAVES
 #define OTSDB_CELLS_WAVES 1
 #endif
+#ifndef OTSDB_RING_NT  // tuning builds: 2 = non-temporal row stores
+#define OTSDB_RING_NT 0
+#endif
 #ifndef OTSDB_DS_PART
 #define OTSDB_DS_PART 0  // 0: launch_ds kernels, 1: the cells fold
 #endif
@@ -69,14 +72,14 @@ bool launch_ds(DsKernel k, const DsLaunch& a) {
       OTSDB_DBG(a.st, "k_prep");
       return true;
     case DS_RING:  // production: LDS ring sink, sentinel rows, DPP scan
-      hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 1, 0, 1, 256>),
+      hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, OTSDB_RING_NT, 1, 0, 1, 256>),
                          dim3(ds_blocks(S, 4)), dim3(256), 0, a.st, a.P, a.B,
                          a.SM, a.R);
       return true;
     case DS_RATE:
       // launch-bounded to 128 VGPRs (4 waves / SIMD instead of the 3 its 140
       // VGPRs allow; 8 cold spills): C4 bucketize 14.1 -> 13.3 ms
-      hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, 0, 4, 0, 1, 1024, 512, 1>),
+      hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, OTSDB_RING_NT, 4, 0, 1, 1024, 512, 1>),
                          dim3(ds_blocks(S, 4)), dim3(256), 0, a.st, a.P, a.B,
                          a.SM, a.R);
       return true;

@@ -444,8 +444,13 @@ DEV void rate_flush(const Params& P, RowSink& S, RateState& R, int64_t f,
   const double held = il >= 0 ? lv : (R.carry_k >= 0 ? R.carry_kv : R.r0_val);
   if (inb) {
     const bool real = k && b != R.r0_idx;
-    S.rowv[b] = real ? kv : held;
-    S.rows[b] = real ? ST_REAL : ST_INTERP;
+    if (S.nt) {
+      __builtin_nontemporal_store(real ? kv : held, &S.rowv[b]);
+      __builtin_nontemporal_store((uint8_t)(real ? ST_REAL : ST_INTERP), &S.rows[b]);
+    } else {
+      S.rowv[b] = real ? kv : held;
+      S.rows[b] = real ? ST_REAL : ST_INTERP;
+    }
   }
   if (km) {
     const int l = 63 - __builtin_clzll(km);

@@ -50,9 +50,13 @@ struct CellsFold {
 // (2,048 x 24-byte dev / diff states + ring + marks: 57 KB, within the
 // 64 KB a workgroup may hold; the states are dynamic LDS sized for the
 // grid, fold_lds_bytes)
+#ifndef OTSDB_FOLD_WB_MAX  // tuning builds: a smaller window cap
+#define OTSDB_FOLD_WB_MAX 2048
+#endif
 template <class A>
 constexpr int fold_wb() {
-  return sizeof(A) <= 24 ? 2048 : 1024;
+  return sizeof(A) <= 24 ? OTSDB_FOLD_WB_MAX
+                         : (OTSDB_FOLD_WB_MAX < 1024 ? OTSDB_FOLD_WB_MAX : 1024);
 }
 
 // the fold's window: P.fold_wb buckets when the engine narrowed it (more

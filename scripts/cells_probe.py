@@ -15,6 +15,9 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--series", type=int, default=100000)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--named", action="store_true",
+                    help="the metric's named query sum:1m-avg (LERP) instead "
+                         "of the config's")
     ap.add_argument("--variants", default="",
                     help="comma list of OTSDB_CELLS_VARIANT values (variants "
                          "build), timed interleaved")
@@ -30,8 +33,14 @@ def main():
     cells = workload.encode_cells_device(eng, db)
     db.ts = db.val = None
     torch.cuda.empty_cache()
-    spec = workload.query_spec(a.config)
-    res = DeviceResult(torch, db.n_groups, db.n_groups * 2100, "cuda")
+    if a.named:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import bench  # noqa: E402
+        spec = bench.named_spec(a.config)
+    else:
+        spec = workload.query_spec(a.config)
+    nbk = 10200 if a.named else 2100
+    res = DeviceResult(torch, db.n_groups, db.n_groups * nbk, "cuda")
     cb = cells.n_bytes
     vs = [v for v in a.variants.split(",") if v] or [None]
     ref = None
@@ -61,6 +70,8 @@ def main():
             eng.lib.otsdb_prof_read(eng.ctx, ms, nn, 8, 1)
             eng.lib.otsdb_prof_enable(eng.ctx, 0)
             kb = ms[0] / max(nn[0], 1) / 1e3
+            print("stages ms:", [round(ms[i] / max(nn[i], 1), 3) for i in range(8)],
+                  flush=True)
             times[v].append(kb)
             print("variant %s round %d: %d pts %.3f GB compacted; query %.2f ms "
                   "(%.1f Gpts/s); k_bucketize_cells %.2f ms = %.0f GB/s "

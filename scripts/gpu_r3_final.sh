@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-3 final evidence on one box, in order: PMC traffic of the dominant
+# kernels (C2 fold, C4 rate bucketize, the cells fold) copied into profiles/
+# so the bench lines that follow report this build's traffic; every config's
+# bench line; rocprofv3 kernel stats C2-C5 and of the storage-row / mixed
+# paths; the GPU test suite.  Stops at the first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+PMC_CFG=C2 PMC_PASSES="sq fetch write" bash scripts/gpu_pmc.sh > gpurun_out/pmc_c2.log 2>&1 || { tail -5 gpurun_out/pmc_c2.log; exit 1; }
+cp gpurun_out/pmc_C2/summary.json profiles/pmc_C2.json
+PMC_CFG=C4 PMC_PASSES="sq fetch write" bash scripts/gpu_pmc.sh > gpurun_out/pmc_c4.log 2>&1 || { tail -5 gpurun_out/pmc_c4.log; exit 1; }
+cp gpurun_out/pmc_C4/summary.json profiles/pmc_C4.json
+bash scripts/gpu_pmc_cells.sh > gpurun_out/pmc_cells.log 2>&1 || { tail -5 gpurun_out/pmc_cells.log; exit 1; }
+echo "pmc ok"
+NO_PROF=1 STEPS=10 CPU_S=${CPU_S:-10} bash scripts/gpu_bench_all.sh || exit $?
+CONFIGS="C2 C3 C4 C5" bash scripts/gpu_kernel_stats.sh > gpurun_out/ks_all.log 2>&1 || { tail -5 gpurun_out/ks_all.log; exit 1; }
+SERIES=100000 bash scripts/gpu_rows_prof.sh > gpurun_out/rows_prof.out 2>&1 || { tail -5 gpurun_out/rows_prof.out; exit 1; }
+echo "kernel stats ok"
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread \
+  -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+tail -1 gpurun_out/pytest_gpu.log
+exit $rc
