@@ -208,6 +208,166 @@ __global__ __launch_bounds__(256) void k_cells_prep(Params P, CellsFold CF,
   store(true, lo, hi, rlo, vlo, qw, vl0, of_has, of_ts, of_val);
 }
 
+// ------------------------------------------------------------ fold prep
+// k_cells_fold_prep: one thread per (series, inner window boundary j) of a
+// grid wider than one fold window — k_fold_prep's WinCtx (the first point of
+// window j, the series' real buckets either side, folded sequentially from
+// the points like the Downsampler does) plus the cells stream's cursor there
+// (row, value byte offset, value length), from the series' qualifier stream.
+// A row whose qualifier width is not the series' raises ERR_CELLS_GENERIC
+// (the generic decode takes the batch, as in k_cells_prep).
+template <class M>
+__global__ __launch_bounds__(256) void k_cells_fold_prep(
+    Params P, CellsFold CF, int64_t S, SeriesMeta SM, int64_t NW, int64_t WB,
+    WinCtx* __restrict__ wc, int* err_word) {
+  const int64_t nbd = NW - 1;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t s = idx / nbd;
+  if (s >= S) return;
+  const int64_t j = idx - s * nbd + 1;
+  const int64_t o = s * nbd + j - 1;
+  const CellsDev& C = CF.C;
+  WinCtx c{0, INT64_MIN, 0.0, INT64_MIN, 0.0};
+  const bool keep = SM.keep[s];
+  const int64_t lo = keep ? SM.lo[s] : 0, hi = keep ? SM.hi[s] : 0;
+  CF.wrlo[o] = CF.rlo[s];
+  CF.wvlo[o] = CF.vlo[s];
+  CF.wvl0[o] = CF.vl0[s];
+  if (lo >= hi) {
+    c.bnd = lo;
+    wc[o] = c;
+    return;
+  }
+  const int64_t r0 = CF.series_row[s], r1 = CF.series_row[s + 1];
+  const int64_t qb = C.qual_off[r0];
+  const int qw = CF.qw[s], qsh = qw == 4 ? 2 : 1;
+  const int64_t Ns = (C.qual_off[r1] - qb) >> qsh;
+  const int64_t vend = C.val_off[C.R];
+  bool bad = false;
+  auto row_ok = [&](int64_t r) {
+    const int64_t a = C.qual_off[r], l = C.qual_off[r + 1] - a;
+    if (l <= 0 || (l & (qw - 1))) return false;
+    return ((C.qual[a] & 0xF0) == 0xF0 ? 4 : 2) == qw;
+  };
+  auto row_of = [&](int64_t p) {  // the last r with qual_off[r] <= qb+qw*p
+    int64_t a = r0, b = r1 - 1;
+    const int64_t x = qb + qw * p;
+    while (a < b) {
+      const int64_t m = (a + b + 1) >> 1;
+      if (C.qual_off[m] <= x) a = m;
+      else b = m - 1;
+    }
+    return a;
+  };
+  auto first_pt = [&](int64_t r) { return (C.qual_off[r] - qb) >> qsh; };
+  auto qual = [&](int64_t p) { return cells_qual_at(C, qb + qw * p, qw); };
+  auto ts_in = [&](int64_t p, int64_t r) {
+    return qual_ts(C.row_base_s[r] * 1000, qw, qual(p));
+  };
+  // the value byte offset of point p of row r: the row's offset + the
+  // lengths of the row's points before p, 16 qualifier bytes a load
+  const int64_t qend = C.qual_off[C.R];
+  auto voff_of = [&](int64_t p, int64_t r) {
+    int64_t v = C.val_off[r];
+    int64_t a = qb + qw * first_pt(r);
+    const int64_t e = qb + qw * p;
+    for (; a + 16 <= e && a + 16 <= qend; a += 16) {
+      const uint4 x = *reinterpret_cast<const uint4*>(C.qual + a);
+      const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        // the flags byte of each qualifier: the last of its qw bytes
+        if (qw == 2) v += ((w[i] >> 8) & 7) + ((w[i] >> 24) & 7) + 2;
+        else v += ((w[i] >> 24) & 7) + 1;
+      }
+    }
+    for (; a < e; a += qw) v += (C.qual[a + qw - 1] & 0x7) + 1;
+    return v;
+  };
+  // sequential fold of points [a, e) with ts < e_ts from point a of row r at
+  // value offset v, rows crossed in order
+  auto fold_run = [&](int64_t a, int64_t r, int64_t v, int64_t e, int64_t e_ts,
+                      int* err) {
+    M st = M::init();
+    int64_t next = r + 1 < r1 ? first_pt(r + 1) : Ns;
+    for (int64_t i = a; i < e; ++i) {
+      if (i == next) {
+        ++r;
+        bad |= !row_ok(r);
+        v = C.val_off[r];
+        next = r + 1 < r1 ? first_pt(r + 1) : Ns;
+      }
+      const uint32_t q = qual(i);
+      if (qual_ts(C.row_base_s[r] * 1000, qw, q) >= e_ts) break;
+      const int l = (int)(q & 0x7) + 1;
+      st.push(bits_to_double(dbits_of(load_be(C.val, v, l, vend), l, (q & 0x8) != 0)));
+      v += l;
+    }
+    return st.finish(err);
+  };
+  // the first point at or after the window start T: the row holding T (the
+  // last row whose base is <= T; bases increase), then its points; none
+  // there: the next row's first point
+  const int64_t T = bucket_ts(P, j * WB);
+  int64_t r;
+  {
+    int64_t ra = r0, rb = r1 - 1;
+    while (ra < rb) {
+      const int64_t m = (ra + rb + 1) >> 1;
+      if (C.row_base_s[m] * 1000 <= T) ra = m;
+      else rb = m - 1;
+    }
+    r = ra;
+  }
+  bad |= !row_ok(r);
+  int64_t p;
+  {
+    int64_t pa = first_pt(r);
+    int64_t pb = r + 1 < r1 ? first_pt(r + 1) : Ns;
+    while (pa < pb) {
+      const int64_t m = pa + ((pb - pa) >> 1);
+      if (ts_in(m, r) < T) pa = m + 1;
+      else pb = m;
+    }
+    p = pa;
+    if (r + 1 < r1 && p == first_pt(r + 1)) ++r;  // the next row's first
+  }
+  if (p < lo || p > hi) {  // the seek / stop bounds cut the window: clamp
+    p = p < lo ? lo : hi;
+    r = p < Ns ? row_of(p) : r1 - 1;
+  }
+  c.bnd = p;
+  int err = 0;
+  if (p > lo) {
+    // the bucket of point p - 1 and its points [q, p), scanning back
+    int64_t rq = (p - 1 >= first_pt(r) || r == r0) ? r : r - 1;
+    if (p - 1 < first_pt(rq)) rq = row_of(p - 1);
+    const int64_t bt = bucket_ts(P, bucket_of(P, ts_in(p - 1, rq)));
+    int64_t q = p - 1;
+    while (q > lo) {
+      int64_t rr = rq;
+      if (q - 1 < first_pt(rq)) rr = rq - 1;
+      if (ts_in(q - 1, rr) < bt) break;
+      --q;
+      rq = rr;
+    }
+    c.prev_ts = bt;
+    c.prev_val = fold_run(q, rq, voff_of(q, rq), p, INT64_MAX, &err);
+  }
+  if (p < hi) {
+    const int64_t k = bucket_of(P, ts_in(p, r));
+    const int64_t vp = voff_of(p, r);
+    c.next_ts = bucket_ts(P, k);
+    c.next_val = fold_run(p, r, vp, hi, bucket_ts(P, k + 1), &err);
+    // the stream's cursor at point p
+    CF.wrlo[o] = r;
+    CF.wvlo[o] = vp;
+    CF.wvl0[o] = (uint8_t)((qual(p) & 0x7) + 1);
+  }
+  if (bad) atomicOr(err_word, ERR_CELLS_GENERIC);
+  wc[o] = c;
+}
+
 // ---------------------------------------------------------------- stream
 // The lane's value bytes from byte a of the pool as dwords: NL 16-byte loads
 // (unaligned) for K values, one more for a run that skips a meta byte

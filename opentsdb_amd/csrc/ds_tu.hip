@@ -43,6 +43,13 @@ bool launch_cells(DsKernel k, const DsLaunch& a) {
                            0, a.st, a.P, a.cf, S, a.SM, a.err);
       OTSDB_DBG(a.st, "k_cells_prep");
       return true;
+    case DS_CELLS_FOLD_PREP:
+      if (a.NW > 1 && S > 0)
+        hipLaunchKernelGGL(k_cells_fold_prep<M>,
+                           dim3(ds_blocks(S * (a.NW - 1), 256)), dim3(256), 0,
+                           a.st, a.P, a.cf, S, a.SM, a.NW, a.WB, a.wc, a.err);
+      OTSDB_DBG(a.st, "k_cells_fold_prep");
+      return true;
     case DS_CELLS_FOLD:
       return with_monoid(a.agg_id, [&](auto tag) {
         using A = decltype(tag);

@@ -728,10 +728,10 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       return fail(OTSDB_E_NO_SUCH_ELEMENT, "aggregator %d", spec->agg_id);
     NW = (NB + WB - 1) / WB;
   }
-  // the cells fold runs one window (no k_fold_prep over cells) of a narrow
-  // grid (32-bit times); wider and calendar grids from cells take
-  // k_bucketize_cells and the row pipeline
-  if (cells && (NW > 1 || !P.narrow)) {
+  // the cells fold runs on narrow grids (32-bit times), windows after the
+  // first starting from k_cells_fold_prep's cursors; calendar grids from
+  // cells take k_bucketize_cells and the row pipeline
+  if (cells && !P.narrow) {
     fold = false;
     WB = NW = 0;
   }
@@ -743,7 +743,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   // few tiles (small queries, e.g. C1's 100 groups of 10 series): narrower
   // fold windows give the grid more workgroups — each window's workgroup
   // streams only that window's points (k_fold_prep hands it the context)
-  if (fold && !cfold && T.T > 0 && NB > kFoldMinWindow &&
+  if (fold && T.T > 0 && NB > kFoldMinWindow &&
       T.T * NW < kFoldMinBlocks) {
     const int64_t want = (kFoldMinBlocks + T.T - 1) / T.T;  // windows
     int64_t wb = (NB + want - 1) / want;
@@ -797,6 +797,11 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       CF.vlo = cv.take<int64_t>(S);
       CF.qw = cv.take<uint8_t>(S);
       CF.vl0 = cv.take<uint8_t>(S);
+      if (NW > 1) {
+        CF.wrlo = cv.take<int64_t>((size_t)S * (NW - 1));
+        CF.wvlo = cv.take<int64_t>((size_t)S * (NW - 1));
+        CF.wvl0 = cv.take<uint8_t>((size_t)S * (NW - 1));
+      }
     }
     if (two_level) {
       W.comb = cv.take<Packed>((size_t)n_comb * kCombineSlices * NB);
@@ -847,6 +852,12 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         if (cfold) {
           a.cf = CF;
           launch_cells<M>(DS_CELLS_PREP, a);
+          if (NW > 1) {
+            a.wc = wc;
+            a.NW = NW;
+            a.WB = WB;
+            launch_cells<M>(DS_CELLS_FOLD_PREP, a);
+          }
         } else {
           launch_ds<M>(DS_PREP, a);
           if (NW > 1) {

@@ -587,10 +587,17 @@ __global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
         c.qb = CF.C.qual_off[CF.series_row[s]];
         c.vb0 = CF.C.val_off[CF.series_row[s]];
         c.r1 = CF.series_row[s + 1];
-        c.rlo = CF.rlo[s];
-        c.vcur = CF.vlo[s];
+        if (win > 0) {  // the cursor at the window's first point
+          const int64_t o = s * nbd + win - 1;
+          c.rlo = CF.wrlo[o];
+          c.vcur = CF.wvlo[o];
+          c.vl0 = CF.wvl0[o];
+        } else {
+          c.rlo = CF.rlo[s];
+          c.vcur = CF.vlo[s];
+          c.vl0 = CF.vl0[s];
+        }
         c.qw = CF.qw[s];
-        c.vl0 = CF.vl0[s];
         c.qend = CF.C.qual_off[CF.C.R];
         c.vend = CF.C.val_off[CF.C.R];
         cm[CELLS ? w : 0] = c;

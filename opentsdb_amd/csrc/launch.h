@@ -44,6 +44,11 @@ struct CellsFold {
   int64_t* vlo;               // byte offset in C.val of point lo's value
   uint8_t* qw;                // qualifier width of the series (2 / 4)
   uint8_t* vl0;               // value length of point lo (first guess)
+  // grids of several fold windows: the stream's cursor at each inner window
+  // boundary (per (series, boundary), k_cells_fold_prep)
+  int64_t* wrlo;
+  int64_t* wvlo;
+  uint8_t* wvl0;
 };
 
 // buckets per fold window: the aggregator states of a window live in LDS
@@ -88,7 +93,8 @@ enum DsKernel {
   DS_FOLD_PREP,  // k_fold_prep: window boundaries of the ordered fold
   DS_FOLD,       // k_fold: downsample + contribution + ordered aggregator
   DS_CELLS_PREP, // k_cells_prep: bounds / cursors of a cells fold
-  DS_CELLS_FOLD  // k_fold fed straight from compacted columns
+  DS_CELLS_FOLD, // k_fold fed straight from compacted columns
+  DS_CELLS_FOLD_PREP  // k_cells_fold_prep: window boundaries of a cells fold
 };
 
 struct DsLaunch {

@@ -233,6 +233,42 @@ def test_fused_cells_query(engine, agg, ds, rate, kind, seconds):
     compare(got, ref, exact, where="fused/%s/%s" % (agg, ds), floor=fl)
 
 
+@pytest.mark.parametrize("n_series,n_groups", [(40, 4), (1100, 1100)])
+@pytest.mark.parametrize("agg,ds", [("sum", "1m-avg"), ("zimsum", "1m-sum"),
+                                    ("avg", "1m-max"), ("max", "1m-min-nan"),
+                                    ("dev", "1m-avg-zero"), ("count", "1m-count")])
+def test_fused_cells_query_multi_window(engine, n_series, n_groups, agg, ds):
+    """The cells fold over grids of several fold windows: two days of 1 m
+    buckets (2,880 > one 2,048-bucket window; few tiles: narrowed windows of
+    128+ buckets; 1,100 single-series groups: two full windows), windows
+    starting from k_cells_fold_prep's cursors (row, value offset, length)
+    and boundary context (the real buckets either side, LERP across the
+    boundary, fills), against the oracle."""
+    import torch
+    from opentsdb_amd import workload
+    from opentsdb_amd.engine import DeviceResult
+    from tests.test_gpu_parity import compare
+    hb = datasets.random_batch(31, n_series=n_series, n_groups=n_groups,
+                               span_ms=2 * 86400000, cadence_ms=20000)
+    hb.ts[:] = hb.ts - hb.ts % 1000
+    for s in range(hb.n_series):
+        a, b = hb.offsets[s], hb.offsets[s + 1]
+        assert (np.diff(hb.ts[a:b]) > 0).all()
+    hb.is_float = np.ones(len(hb.ts), np.uint8)
+    db = _device_batch(hb, "float")
+    cells_d = workload.encode_cells_device(engine, db)
+    t0, t1 = datasets.T0 + 600000, datasets.T0 + 2 * 86400000 - 300000
+    spec = core.make_spec(t0, t1, core.Aggregators.get(agg),
+                          core.DownsamplingSpecification(ds), t0, t1)
+    ref = pyoracle.group_by(spec, hb)
+    res = DeviceResult(torch, db.n_groups, 4 * len(hb.ts) + 64, "cuda")
+    workload.run_cells_device(engine, spec, cells_d, db, res)
+    got = _result_points(res, db.n_groups)
+    exact = ds.split("-")[1] in ("max", "min", "count") and agg in (
+        "max", "count")
+    compare(got, ref, exact, where="cellsmw/%d/%s/%s" % (n_series, agg, ds))
+
+
 def test_fused_cells_corrupt_column(engine):
     """A column whose value bytes do not match its qualifiers:
     IllegalDataException, as the decode (Internal.java:307-321)."""
