@@ -305,32 +305,37 @@ __global__ __launch_bounds__(256) void k_cells_fold_prep(
     }
     return st.finish(err);
   };
-  // the first point at or after the window start T: the row holding T (the
-  // last row whose base is <= T; bases increase), then its points; none
-  // there: the next row's first point
+  // the first point at or after the window start T: the first row whose
+  // last point is >= T (points increase across the series' rows; bases may
+  // repeat — Span.addRow keeps a second RowSeq of one row key), then its
+  // first point >= T
   const int64_t T = bucket_ts(P, j * WB);
-  int64_t r;
+  auto last_ts = [&](int64_t r) {
+    return ts_in((r + 1 < r1 ? first_pt(r + 1) : Ns) - 1, r);
+  };
+  int64_t r, p;
   {
-    int64_t ra = r0, rb = r1 - 1;
+    int64_t ra = r0, rb = r1;  // first r with last_ts(r) >= T, r1 if none
     while (ra < rb) {
-      const int64_t m = (ra + rb + 1) >> 1;
-      if (C.row_base_s[m] * 1000 <= T) ra = m;
-      else rb = m - 1;
+      const int64_t m = ra + ((rb - ra) >> 1);
+      if (last_ts(m) < T) ra = m + 1;
+      else rb = m;
     }
     r = ra;
   }
-  bad |= !row_ok(r);
-  int64_t p;
-  {
+  if (r >= r1) {
+    r = r1 - 1;
+    p = Ns;
+  } else {
+    bad |= !row_ok(r);
     int64_t pa = first_pt(r);
-    int64_t pb = r + 1 < r1 ? first_pt(r + 1) : Ns;
+    int64_t pb = (r + 1 < r1 ? first_pt(r + 1) : Ns) - 1;  // ts(pb) >= T
     while (pa < pb) {
       const int64_t m = pa + ((pb - pa) >> 1);
       if (ts_in(m, r) < T) pa = m + 1;
       else pb = m;
     }
     p = pa;
-    if (r + 1 < r1 && p == first_pt(r + 1)) ++r;  // the next row's first
   }
   if (p < lo || p > hi) {  // the seek / stop bounds cut the window: clamp
     p = p < lo ? lo : hi;

@@ -117,6 +117,10 @@ __global__ __launch_bounds__(256) void k_keys_transpose(
   };
   load(0);
   for (int64_t b0 = 0; b0 < nb; b0 += 64) {
+    // the keys of this thread's 16 members at bucket b0 + bi, and their
+    // min / max / count (the tile's per-bucket partial, from registers)
+    uint64_t mn = KEY_NONE, mx = 0;
+    uint32_t nk = 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int mi = r * 4 + w;
@@ -131,6 +135,16 @@ __global__ __launch_bounds__(256) void k_keys_transpose(
         k = (st[r] && !is_nan(v[r])) ? dkey(v[r]) : KEY_NONE;
       }
       tile[mi][bi] = k;
+      if (k != KEY_NONE) {
+        mn = k < mn ? k : mn;
+        mx = k > mx ? k : mx;
+        ++nk;
+      }
+    }
+    if (mm) {
+      s_mm[w][bi][0] = mn;
+      s_mm[w][bi][1] = mx;
+      s_cnt[w][bi] = nk;
     }
     __syncthreads();
     if (b0 + 64 < nb) load(b0 + 64);
@@ -141,36 +155,17 @@ __global__ __launch_bounds__(256) void k_keys_transpose(
       const int64_t b = b0 + bj;
       if (m < M && b < nb) keys[b * M + m] = tile[bi][bj];
     }
-    if (mm) {
-      // the tile's min / max key (and, FILL, count) per bucket over its
-      // non-NONE keys: each thread folds 16 members of bucket column bi
-      uint64_t mn = KEY_NONE, mx = 0;
-      uint32_t nk = 0;
+    if (mm && tid < 64 && b0 + tid < nb) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint64_t x = tile[w * 16 + i][bi];
-        if (x != KEY_NONE) {
-          mn = x < mn ? x : mn;
-          mx = x > mx ? x : mx;
-          ++nk;
-        }
+      for (int q = 1; q < 4; ++q) {
+        mn = s_mm[q][tid][0] < mn ? s_mm[q][tid][0] : mn;
+        mx = s_mm[q][tid][1] > mx ? s_mm[q][tid][1] : mx;
+        nk += s_cnt[q][tid];
       }
-      s_mm[w][bi][0] = mn;
-      s_mm[w][bi][1] = mx;
-      s_cnt[w][bi] = nk;
-      __syncthreads();
-      if (tid < 64 && b0 + tid < nb) {
-#pragma unroll
-        for (int q = 1; q < 4; ++q) {
-          mn = s_mm[q][tid][0] < mn ? s_mm[q][tid][0] : mn;
-          mx = s_mm[q][tid][1] > mx ? s_mm[q][tid][1] : mx;
-          nk += s_cnt[q][tid];
-        }
-        const int64_t oi = (b0 + tid) * ntiles + blockIdx.x;
-        mm[2 * oi] = mn;
-        mm[2 * oi + 1] = mx;
-        if (FILL) F.cnt[oi] = nk;
-      }
+      const int64_t oi = (b0 + tid) * ntiles + blockIdx.x;
+      mm[2 * oi] = mn;
+      mm[2 * oi + 1] = mx;
+      if (FILL) F.cnt[oi] = nk;
     }
     __syncthreads();
   }
