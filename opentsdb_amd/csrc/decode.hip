@@ -85,7 +85,7 @@ DEV bool decode_uniform(const CellsDev& C, int64_t r, int mode,
                         const int64_t* row_out, uint8_t* fast, int64_t cap,
                         int64_t* ts, int64_t* val, uint8_t* isf, int& bad) {
   const int lane = LANE;
-  if (mode == 1 && !fast[r]) return false;
+  if (mode == 1 && fast[r] != 1) return false;
   const int qw = ((q[0] & 0xF0) == 0xF0) ? 4 : 2;
   if (qlen % qw || ((uintptr_t)q & 1)) return false;
   const int64_t n = qlen / qw;
@@ -144,11 +144,17 @@ DEV bool decode_uniform(const CellsDev& C, int64_t r, int mode,
 
 // one wavefront per row; mode 0 counts (and validates), mode 1 writes
 #ifndef OTSDB_DS_TU
+// fast[r]: 1 = one qualifier width and one value length (k_decode writes
+// by direct indexing); 0 = one width, lengths mixed (counted by k_decode,
+// written by k_decode_generic); 2 = widths mixed (k_decode_generic counts
+// and writes).  flags[0] / flags[1]: some row is 2 / some data row is not 1
+// (plain stores of 1: the engine launches k_decode_generic only then, so the
+// common batch keeps k_decode's small register footprint).
 __global__ __launch_bounds__(256) void k_decode(
     CellsDev C, int mode, int64_t* __restrict__ row_count,
     const int64_t* __restrict__ row_out, uint8_t* __restrict__ fast,
     int64_t cap, int64_t* __restrict__ ts, int64_t* __restrict__ val,
-    uint8_t* __restrict__ isf, int* err_word) {
+    uint8_t* __restrict__ isf, int* err_word, int* __restrict__ flags) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= C.R) return;
@@ -160,7 +166,7 @@ __global__ __launch_bounds__(256) void k_decode(
   if (qlen & 1) {  // not a data-point column (Internal.java:262-264)
     if (mode == 0 && lane == 0) {
       row_count[r] = 0;
-      fast[r] = 0;
+      fast[r] = 1;  // nothing to write
     }
     return;
   }
@@ -172,10 +178,34 @@ __global__ __launch_bounds__(256) void k_decode(
     if (decode_uniform(C, r, mode, q, qlen, C.val_off[r], vlen, base_ms,
                        row_count, row_out, fast, cap, ts, val, isf, fbad)) {
       if (__ballot(fbad) && lane == 0) atomicOr(err_word, ERR_CORRUPT_CELL);
+      if (mode == 0 && lane == 0 && !fast[r]) flags[1] = 1;
       return;
     }
   }
-  if (mode == 0 && lane == 0) fast[r] = 0;
+  if (mode == 0 && lane == 0) {
+    fast[r] = 2;
+    flags[0] = 1;
+    flags[1] = 1;
+  }
+}
+
+// The generic walk (rows k_decode left to it, see fast[] above): mode 0
+// counts and validates the rows of mixed qualifier widths, mode 1 writes
+// every row not written by k_decode.  One wavefront per row.
+__global__ __launch_bounds__(256) void k_decode_generic(
+    CellsDev C, int mode, int64_t* __restrict__ row_count,
+    const int64_t* __restrict__ row_out, const uint8_t* __restrict__ fast,
+    int64_t cap, int64_t* __restrict__ ts, int64_t* __restrict__ val,
+    uint8_t* __restrict__ isf, int* err_word) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= C.R) return;
+  const uint8_t fr = fast[r];
+  if (mode == 0 ? fr != 2 : fr == 1) return;
+  const uint8_t* q = C.qual + C.qual_off[r];
+  const int64_t qlen = C.qual_off[r + 1] - C.qual_off[r];
+  const int64_t vlen = C.val_off[r + 1] - C.val_off[r];
+  const int64_t base_ms = C.row_base_s[r] * 1000;
   // Generic column (qualifier widths mixed, MS_MIXED_COMPACT): 8 two-byte
   // units per lane, 512 per pass.  Each lane composes its units' maps
   // start(u+1) = !(start(u) && ms(u)) sequentially, one wave scan of the

@@ -174,6 +174,7 @@ struct otsdb_ctx {
   size_t acal_cap = 0;   // chain positions and bucket-start timestamps
   void* dec_ws = nullptr;  // decode workspace
   size_t dec_ws_cap = 0;
+  int dec_generic = 0;  // the last decode count pass: bit 0 / 1, k_decode_generic counts / writes
   void* ws2 = nullptr;     // raw group-by: candidates, sort, selection slab
   size_t ws2_cap = 0;
   void* rows_ws = nullptr;  // storage-row compaction / span assembly: per-row
@@ -1392,30 +1393,51 @@ otsdb_status decode_impl(otsdb_ctx* c, const otsdb_cells* cells,
                                   (int64_t*)nullptr, (int64_t)0,
                                   (size_t)(R + 1), rocprim::plus<int64_t>(),
                                   st));
-  const size_t ws_need = (size_t)(2 * R + 2) * 8 + (size_t)R + 64 + scan_tmp;
+  const size_t ws_need = (size_t)(2 * R + 2) * 8 + (size_t)R + 128 + scan_tmp;
   otsdb_status rc = ensure(&c->dec_ws, &c->dec_ws_cap, ws_need);
   if (rc) return rc;
   int64_t* row_count = (int64_t*)c->dec_ws;
   int64_t* row_out = row_count + (R + 1);
   uint8_t* fast = (uint8_t*)(row_out + (R + 1));
-  void* tmp = (void*)(((uintptr_t)(fast + R) + 63) & ~(uintptr_t)63);
+  int* flags = (int*)(((uintptr_t)(fast + R) + 15) & ~(uintptr_t)15);
+  void* tmp = (void*)(((uintptr_t)(flags + 4) + 63) & ~(uintptr_t)63);
   CellsDev C{R, cells->row_series, cells->row_base_s, cells->qual_off,
              cells->qual, cells->val_off, cells->val};
-  if (counted) {
-    if (R > 0)
+  // the write pass: k_decode for the uniform rows, k_decode_generic for the
+  // rest when the count pass saw any (c->dec_generic)
+  auto write_pass = [&]() -> otsdb_status {
+    if (R > 0) {
       hipLaunchKernelGGL(k_decode, dim3(blocks_for(R, 4)), dim3(256), 0, st, C,
                          1, row_count, (const int64_t*)row_out, fast, capacity,
-                         ts_ms, val, is_float, c->d_err);
+                         ts_ms, val, is_float, c->d_err, flags);
+      if (c->dec_generic & 2)
+        hipLaunchKernelGGL(k_decode_generic, dim3(blocks_for(R, 4)), dim3(256),
+                           0, st, C, 1, row_count, (const int64_t*)row_out,
+                           (const uint8_t*)fast, capacity, ts_ms, val, is_float,
+                           c->d_err);
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(st));
     return OTSDB_OK;
-  }
+  };
+  if (counted) return write_pass();
   HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), st));
+  HIP_TRY(hipMemsetAsync(flags, 0, 2 * sizeof(int), st));
+  c->dec_generic = 0;
   if (R > 0) {
     hipLaunchKernelGGL(k_decode, dim3(blocks_for(R, 4)), dim3(256), 0, st, C,
                        0, row_count, (const int64_t*)nullptr, fast, (int64_t)0,
                        (int64_t*)nullptr, (int64_t*)nullptr,
-                       (uint8_t*)nullptr, c->d_err);
+                       (uint8_t*)nullptr, c->d_err, flags);
+    int hf[2];
+    HIP_TRY(hipMemcpyAsync(hf, flags, sizeof(hf), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    c->dec_generic = (hf[0] ? 1 : 0) | (hf[1] ? 2 : 0);
+    if (c->dec_generic & 1)
+      hipLaunchKernelGGL(k_decode_generic, dim3(blocks_for(R, 4)), dim3(256), 0,
+                         st, C, 0, row_count, (const int64_t*)nullptr,
+                         (const uint8_t*)fast, (int64_t)0, (int64_t*)nullptr,
+                         (int64_t*)nullptr, (uint8_t*)nullptr, c->d_err);
     // row_count[R] = 0, so row_out[R] = the total
     HIP_TRY(hipMemsetAsync(row_count + R, 0, 8, st));
     HIP_TRY(rocprim::exclusive_scan(tmp, scan_tmp, (const int64_t*)row_count,
@@ -1440,13 +1462,7 @@ otsdb_status decode_impl(otsdb_ctx* c, const otsdb_cells* cells,
   if (total > capacity)
     return fail(OTSDB_E_CAPACITY, "decode capacity %lld < %lld points",
                 (long long)capacity, (long long)total);
-  if (R > 0)
-    hipLaunchKernelGGL(k_decode, dim3(blocks_for(R, 4)), dim3(256), 0, st, C,
-                       1, row_count, (const int64_t*)row_out, fast, capacity,
-                       ts_ms, val, is_float, c->d_err);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(st));
-  return OTSDB_OK;
+  return write_pass();
 }
 
 // Query straight from compacted columns: the fused decode + downsample when
