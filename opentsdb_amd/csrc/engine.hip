@@ -1710,10 +1710,21 @@ otsdb_status compact_impl(otsdb_ctx* c, const otsdb_raw_rows* raw, int fix,
   HIP_TRY(hipMemsetAsync(LS.ctr, 0, 16, st));
   for (int64_t* a : {gen_n, out_q, out_v, kept})
     HIP_TRY(hipMemsetAsync(a + R, 0, 8, st));
-  if (R > 0)
-    hipLaunchKernelGGL(k_rows_plan, dim3(blocks_for(R, 256)), dim3(256), 0, st,
-                       D, fix, kind, lone, gen_n, out_q, out_v, kept, first_err,
-                       LS);
+  if (R > 0) {
+    // the verbatim columns first (64 rows a wavefront), the exact plan only
+    // when some row is left (a flag read: one sync)
+    int* pend = (int*)(LS.ctr + 8);
+    HIP_TRY(hipMemsetAsync(pend, 0, sizeof(int), st));
+    hipLaunchKernelGGL(k_rows_uniform, dim3(blocks_for(R, 256)), dim3(256), 0,
+                       st, D, kind, lone, gen_n, out_q, out_v, kept, pend);
+    int hp = 0;
+    HIP_TRY(hipMemcpyAsync(&hp, pend, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (hp)
+      hipLaunchKernelGGL(k_rows_plan, dim3(blocks_for(R, 4)), dim3(256), 0, st,
+                         D, fix, kind, lone, gen_n, out_q, out_v, kept,
+                         first_err, LS);
+  }
   HIP_TRY(hipGetLastError());
   if ((rc = scan_excl(tmp, tmpb, gen_n, gen_base, R, st))) return rc;
   HIP_TRY(hipMemcpyAsync(&c->h_small[0], gen_base + R, 8, hipMemcpyDeviceToHost, st));

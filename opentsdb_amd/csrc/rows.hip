@@ -81,7 +81,8 @@ struct RawDev {
 // row status codes (otsdb_status values)
 enum : int { RS_ILLEGAL_DATA = 1, RS_ILLEGAL_ARGUMENT = 3, RS_UNSUPPORTED = 5 };
 enum : uint8_t {
-  RK_EMPTY = 0, RK_VERBATIM = 1, RK_LONE = 2, RK_GENERAL = 3, RK_LARGE = 4
+  RK_EMPTY = 0, RK_VERBATIM = 1, RK_LONE = 2, RK_GENERAL = 3, RK_LARGE = 4,
+  RK_PENDING = 5  // k_rows_uniform left the row to k_rows_plan
 };
 // column types
 enum : int { CT_SKIP = 0, CT_APPEND = 1, CT_ONE = 2, CT_MULTI = 3 };
@@ -139,6 +140,12 @@ DEV int64_t wave_incl_scan(int64_t x) {
     const int64_t y = __shfl_up(x, d);
     if (lane >= d) x += y;
   }
+  return x;
+}
+
+DEV int32_t wave_sum_i(int32_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
   return x;
 }
 
@@ -608,16 +615,18 @@ DEV int uniform_load(const uint8_t* qual, int64_t qb, int64_t ql, int64_t a,
   return nb;
 }
 
-// k_rows_plan: one wavefront per 64 rows.  Lanes read their rows' shapes
+// k_rows_uniform: one wavefront per 64 rows.  Lanes read their rows' shapes
 // (thread per row); single compacted columns the merge would rebuild byte
 // for byte (lone_uniform's conditions) are decided VERBATIM by the wave
-// with four rows' qualifier passes in flight at a time; every other row
-// takes the exact plan (plan_row), one at a time.
-__global__ __launch_bounds__(256) void k_rows_plan(
-    RawDev D, int fix, uint8_t* __restrict__ kind, int64_t* __restrict__ lone,
+// with four rows' qualifier passes in flight at a time.  Every other row is
+// marked RK_PENDING (pending[0] = 1) for k_rows_plan's exact plan — a
+// separate kernel, so this one keeps a small register footprint (more
+// waves in flight for its dependent loads).
+__global__ __launch_bounds__(256) void k_rows_uniform(
+    RawDev D, uint8_t* __restrict__ kind, int64_t* __restrict__ lone,
     int64_t* __restrict__ gen_n, int64_t* __restrict__ out_q,
     int64_t* __restrict__ out_v, int64_t* __restrict__ kept,
-    unsigned long long* first_err, LargeSlots LS) {
+    int* __restrict__ pending) {
   const int lane = LANE;
   const int64_t rb = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
   if (rb >= D.R) return;
@@ -675,7 +684,7 @@ __global__ __launch_bounds__(256) void k_rows_plan(
         int32_t carry = -1, vsum = 0;
         int bad = 0;
         uniform_pass(w[i], nb[i], qwk[i], carry, bad, vsum);
-        vsum = (int32_t)wave_sum_l(vsum);
+        vsum = wave_sum_i(vsum);
         if (!__ballot(bad) && (int64_t)vsum + 1 == vlk[i])
           done |= 1ULL << js[i];
       }
@@ -695,24 +704,34 @@ __global__ __launch_bounds__(256) void k_rows_plan(
       uniform_pass(w, nb, q, carry, bad, vsum);
       bad = __ballot(bad) != 0;
     }
-    vsum = (int32_t)wave_sum_l(vsum);
+    vsum = wave_sum_i(vsum);
     if (!bad && (int64_t)vsum + 1 == readlane_l(vl, j)) done |= 1ULL << j;
   }
-  if ((done >> lane) & 1) {
-    kind[r] = RK_VERBATIM;
-    lone[r] = c0;
-    gen_n[r] = 0;
-    out_q[r] = ql;
-    out_v[r] = vl;
-    kept[r] = 1;
+  if (r < D.R) {
+    if ((done >> lane) & 1) {
+      kind[r] = RK_VERBATIM;
+      lone[r] = c0;
+      gen_n[r] = 0;
+      out_q[r] = ql;
+      out_v[r] = vl;
+      kept[r] = 1;
+    } else {
+      kind[r] = RK_PENDING;
+    }
   }
-  uint64_t rest = __ballot(r < D.R) & ~done;
-  while (rest) {
-    const int j = __builtin_ctzll(rest);
-    rest &= rest - 1;
-    plan_row(D, fix, rb + j, kind, lone, gen_n, out_q, out_v, kept, first_err,
-             LS);
-  }
+  if (__ballot(r < D.R) & ~done && lane == 0) pending[0] = 1;
+}
+
+// k_rows_plan: the exact plan of the rows k_rows_uniform left pending, one
+// wavefront per row.
+__global__ __launch_bounds__(256) void k_rows_plan(
+    RawDev D, int fix, uint8_t* __restrict__ kind, int64_t* __restrict__ lone,
+    int64_t* __restrict__ gen_n, int64_t* __restrict__ out_q,
+    int64_t* __restrict__ out_v, int64_t* __restrict__ kept,
+    unsigned long long* first_err, LargeSlots LS) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= D.R || kind[r] != RK_PENDING) return;
+  plan_row(D, fix, r, kind, lone, gen_n, out_q, out_v, kept, first_err, LS);
 }
 
 // ---------------------------------------------------------- GENERAL rows
