@@ -35,7 +35,11 @@
 // each offset.  A row holding a column whose cells go back in time takes an
 // exact emulation of the heap (wave arg-min over the column heads per step).
 //
-// Kernels (one wavefront per storage row):
+// Kernels (one wavefront per storage row unless said otherwise):
+//   k_rows_uniform  64 rows per wavefront: single compacted columns the
+//                   merge rebuilds byte for byte (one qualifier width,
+//                   strictly increasing offsets, lengths adding up, meta 0)
+//                   are VERBATIM; the rest are left to k_rows_plan;
 //   k_rows_plan     classifies the row: EMPTY (no data point: dropped, like
 //                   the scanner drops a null compaction), VERBATIM (the
 //                   noMergesOrFixups case), LONE (one data column: its cells
