@@ -219,25 +219,33 @@ __global__ __launch_bounds__(256) void k_decode_generic(
   int64_t carry_voff = 0;
   int bad = 0;
   const int64_t out0 = mode ? row_out[r] : 0;
-  for (int64_t u0 = 0; u0 < units; u0 += 512) {
-    const int64_t ub = u0 + 8 * lane;
-    const int nu = ub >= units ? 0 : (int)(units - ub < 8 ? units - ub : 8);
-    // the lane's 16 bytes and the 4 after them (a 4-byte qualifier may
+  constexpr int GU = 8;  // two-byte units per lane, 512 a pass (16 — a
+                        // 360-point mixed row in one pass — measured
+                        // slower: 162 vs 140 ms for C2's mixed cells)
+  for (int64_t u0 = 0; u0 < units; u0 += 64 * GU) {
+    const int64_t ub = u0 + GU * lane;
+    const int nu = ub >= units ? 0 : (int)(units - ub < GU ? units - ub : GU);
+    // the lane's 2*GU bytes and the 4 after them (a 4-byte qualifier may
     // start at the lane's last unit)
-    uint32_t w[5] = {0, 0, 0, 0, 0};
-    if (2 * ub + 20 <= qlen) {
-      const uint4 x = *reinterpret_cast<const uint4*>(q + 2 * ub);
-      w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
-      w[4] = *reinterpret_cast<const uint32_t*>(q + 2 * ub + 16);
+    uint32_t w[GU / 2 + 1];
+#pragma unroll
+    for (int i = 0; i <= GU / 2; ++i) w[i] = 0;
+    if (2 * ub + 2 * GU + 4 <= qlen) {
+#pragma unroll
+      for (int i = 0; i < GU / 8; ++i) {
+        const uint4 x = *reinterpret_cast<const uint4*>(q + 2 * ub + 16 * i);
+        w[4 * i] = x.x; w[4 * i + 1] = x.y; w[4 * i + 2] = x.z; w[4 * i + 3] = x.w;
+      }
+      w[GU / 2] = *reinterpret_cast<const uint32_t*>(q + 2 * ub + 2 * GU);
     } else if (nu > 0) {
-      for (int i = 0; i < 20; ++i)
+      for (int i = 0; i < 2 * GU + 4; ++i)
         if (2 * ub + i < qlen) w[i >> 2] |= (uint32_t)q[2 * ub + i] << (8 * (i & 3));
     }
     auto byte_at = [&](int k) { return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu; };
     int F = 0x2;  // identity
     uint32_t msb = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < GU; ++i) {
       const int ms = i < nu && (byte_at(2 * i) & 0xF0) == 0xF0;
       msb |= (uint32_t)ms << i;
       if (i < nu) F = fmap_compose(ms ? 0x1 : 0x3, F);
@@ -255,7 +263,7 @@ __global__ __launch_bounds__(256) void k_decode_generic(
     uint32_t startm = 0;
     int np = 0, vs = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < GU; ++i) {
       if (i < nu && st) {
         startm |= 1u << i;
         const int ms = (msb >> i) & 1;
@@ -278,7 +286,7 @@ __global__ __launch_bounds__(256) void k_decode_generic(
     if (mode == 1 || vs > 0) {
       int k = 0, vo = 0;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < GU; ++i) {
         if ((startm >> i) & 1) {
           const int ms = (msb >> i) & 1;
           const uint32_t qv =
