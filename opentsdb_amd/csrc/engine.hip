@@ -2379,8 +2379,9 @@ otsdb_status otsdb_sel_hist_device(otsdb_ctx* c, int32_t pass,
                          (const uint64_t*)S.W.keys, (const SelState*)S.W.sel,
                          hist_out);
   }
+  // no host sync: the caller's collective on the same stream consumes
+  // hist_out (RCCL enqueues behind it; a gloo staging copy waits for it)
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(st));
   return OTSDB_OK;
 }
 
