@@ -109,3 +109,55 @@ def _rate_case(seed):
 def test_random_rate_sweep(engine, seed):
     b, spec, exact, where = _rate_case(seed)
     check(engine, spec, b, exact, where=where, floor="contributions")
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_random_cells_sweep(engine, seed):
+    """The general sweep's queries over the same points stored as RowSeq
+    bytes: storage rows (otsdb_agg_run_raw_device — columns scattered,
+    appended, split row keys: compaction, span assembly) and, when every
+    series has one value type, device-encoded compacted cells
+    (otsdb_agg_run_cells_device).  Whole-second data takes the cells fold
+    (one window, several, narrowed ones), ms data rows of mixed qualifier
+    widths and the generic decode; rate and percentile downsampling the row
+    kernel.  Against the oracle on the same points."""
+    import torch
+    from opentsdb_amd import storage, workload
+    from opentsdb_amd.engine import DeviceResult
+    from oracle import pyoracle
+    from tests.test_gpu_decode import _device_batch, _result_points
+    from tests.test_gpu_parity import compare, contribution_floor
+    from tests.test_gpu_rows import _raw_from_hb
+    b, spec, exact, where = _case(seed)
+    rng = np.random.default_rng(3000 + seed)
+    if rng.random() < 0.7:  # whole seconds: 2-byte qualifiers
+        ts2 = b.ts - b.ts % 1000
+        if all((np.diff(ts2[b.offsets[s]:b.offsets[s + 1]]) > 0).all()
+               for s in range(b.n_series)):
+            b.ts[:] = ts2
+    try:
+        ref = pyoracle.group_by(spec, b)
+    except pyoracle.OracleError:
+        return  # a rejected query: covered by the columnar sweep
+    fl = contribution_floor(spec, b, ref)
+    db = None
+    types = [np.unique(b.is_float[b.offsets[s]:b.offsets[s + 1]])
+             for s in range(b.n_series)]
+    if all(len(t) <= 1 for t in types):
+        kinds = {int(t[0]) for t in types if len(t)}
+        if len(kinds) <= 1:
+            kind = "float" if kinds != {0} else "int"
+            db = _device_batch(b, kind)
+            cells = workload.encode_cells_device(engine, db)
+            res = DeviceResult(torch, b.n_groups, 4 * len(b.ts) + 4096, "cuda")
+            workload.run_cells_device(engine, spec, cells, db, res)
+            compare(_result_points(res, b.n_groups), ref, exact,
+                    where="cells/" + where, floor=fl)
+    raw = storage.HostRawRows(_raw_from_hb(rng, b), with_ts=True).to_device()
+    raw.n_series = b.n_series
+    if db is None:
+        db = _device_batch(b, "float")  # groups only: the rows hold the types
+    res = DeviceResult(torch, b.n_groups, 4 * len(b.ts) + 4096, "cuda")
+    storage.run_raw_device(engine, spec, raw, db, res)
+    compare(_result_points(res, b.n_groups), ref, exact, where="rows/" + where,
+            floor=fl)
