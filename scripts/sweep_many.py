@@ -8,7 +8,7 @@ import traceback
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
 from opentsdb_amd.engine import Engine  # noqa: E402
-from tests.test_gpu_parity import check, cancel_floor  # noqa: E402
+from tests.test_gpu_parity import check  # noqa: E402
 from tests.test_gpu_sweep import _case, _rate_case  # noqa: E402
 
 
@@ -24,11 +24,11 @@ def main():
         if general:
             b, spec, exact, where = _case(seed)
         else:
-            b, spec, where = _rate_case(seed)
-            exact = False
+            b, spec, exact, where = _rate_case(seed)
         try:
-            check(e, spec, b, exact, where=where,
-                  floor=cancel_floor(b, 2000))
+            # the suite's comparator: 1e-12 relative, the contributions'
+            # floor only where they have both signs
+            check(e, spec, b, exact, where=where, floor="contributions")
         except Exception as ex:  # noqa: BLE001
             bad += 1
             msg = str(ex).splitlines()[0][:300]
