@@ -49,7 +49,7 @@ __global__ void k_cal_anchor(int64_t start_ms, int64_t end_ms,
   const bool keep = p1 > p0 && B.ts[p0] <= end_ms && B.ts[p1 - 1] >= start_ms;
   int64_t lo = p1, pos = 0, cend = 0;
   if (keep) {
-    lo = lower_bound_ends(B.ts, p0, p1, seek_ts);
+    lo = lower_bound_interp(B.ts, p0, p1, seek_ts);
     if (lo < p1) {
       const int64_t j = last_le(A.anchors, 0, A.n_anchors, B.ts[lo]);
       if (j < 0) {

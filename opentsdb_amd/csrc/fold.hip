@@ -94,13 +94,13 @@ __global__ __launch_bounds__(256) void k_fold_prep(Params P, BatchDev B,
     return;
   }
   const int sf = B.series_float ? (int)B.series_float[s] : 1;
-  const int64_t p = lower_bound_ends(B.ts, lo, hi, bucket_ts(P, j * WB));
+  const int64_t p = lower_bound_interp(B.ts, lo, hi, bucket_ts(P, j * WB));
   c.bnd = p;
   int err = 0;
   if (p > lo) {
     const int64_t k = bucket_of(P, B.ts[p - 1]);
     const int64_t bt = bucket_ts(P, k);
-    const int64_t q = lower_bound_ends(B.ts, lo, p - 1, bt);
+    const int64_t q = lower_bound_back(B.ts, lo, p, bt);
     M st = M::init();
     for (int64_t i = q; i < p; ++i) st.push(point_value(B, i, B.val[i], sf));
     c.prev_ts = bt;

@@ -65,14 +65,60 @@ DEV int64_t lower_bound(const int64_t* ts, int64_t a, int64_t b, int64_t t) {
   return a;
 }
 
-// lower_bound that first tests the ends of [a, b): when the whole series
+// lower_bound over [a, b) that first tests the ends: when the whole series
 // lies on one side of t (every series of a whole-range query) no search runs
-// — the dependent-load chain of the binary search was most of k_prep
-DEV int64_t lower_bound_ends(const int64_t* ts, int64_t a, int64_t b,
+// — the dependent-load chain of the binary search was most of k_prep.
+// Otherwise an interpolated first probe: series sampled at a near-regular
+// interval put the answer within a few points of the linear guess, so a
+// gallop from it brackets the answer in 2-3 dependent loads instead of
+// log2(n) ≈ 12 (k_fold_prep's window edges).  Same result as lower_bound
+// for any sorted input: the guess only picks where the bracketing starts.
+DEV int64_t lower_bound_interp(const int64_t* ts, int64_t a, int64_t b,
+                               int64_t t) {
+  if (a >= b) return a;
+  const int64_t ta = ts[a];
+  if (ta >= t) return a;
+  const int64_t tb = ts[b - 1];
+  if (tb < t) return b;
+  int64_t lo = a, hi = b - 1;  // ts[lo] < t <= ts[hi]
+  if (hi - lo > 1) {
+    const double f = (double)(t - ta) / (double)(tb - ta);
+    int64_t g = lo + (int64_t)(f * (double)(hi - lo));
+    g = g <= lo ? lo + 1 : (g >= hi ? hi - 1 : g);
+    if (ts[g] < t) {
+      lo = g;
+      for (int64_t step = 1;; step <<= 1) {
+        const int64_t h = lo + step;
+        if (h >= hi) break;
+        if (ts[h] >= t) { hi = h; break; }
+        lo = h;
+      }
+    } else {
+      hi = g;
+      for (int64_t step = 1;; step <<= 1) {
+        const int64_t l = hi - step;
+        if (l <= lo) break;
+        if (ts[l] < t) { lo = l; break; }
+        hi = l;
+      }
+    }
+  }
+  return lower_bound(ts, lo + 1, hi, t);
+}
+
+// lower bound of t in [a, b) found by galloping back from b - 1: the start
+// of the bucket that holds ts[b - 1] lies a few points before it
+DEV int64_t lower_bound_back(const int64_t* ts, int64_t a, int64_t b,
                              int64_t t) {
-  if (a >= b || ts[a] >= t) return a;
-  if (ts[b - 1] < t) return b;
-  return lower_bound(ts, a + 1, b - 1, t);
+  if (a >= b || ts[b - 1] < t) return b;
+  int64_t hi = b - 1, lo = a - 1;  // ts[hi] >= t; ts[lo] < t (lo = a-1: none)
+  for (int64_t step = 1;; step <<= 1) {
+    const int64_t l = hi - step;
+    if (l <= lo) break;
+    if (ts[l] < t) { lo = l; break; }
+    hi = l;
+  }
+  return lower_bound(ts, lo + 1, hi, t);
 }
 
 DEV int64_t wave_incl_max(int64_t x) {
@@ -161,8 +207,8 @@ __global__ void k_prep(Params P, BatchDev B, SeriesMeta SM, int* err_word) {
   int64_t of_ts = 0;
   double of_val = 0.0;
   if (keep) {
-    lo = lower_bound_ends(B.ts, p0, p1, P.seek_ts);
-    hi = lower_bound_ends(B.ts, lo, p1, P.stop_ts);
+    lo = lower_bound_interp(B.ts, p0, p1, P.seek_ts);
+    hi = lower_bound_interp(B.ts, lo, p1, P.stop_ts);
     if (!P.run_all && P.fill == 0 && hi < p1) {
       const int sf = B.series_float ? (int)B.series_float[s] : 1;
       const int64_t t = B.ts[hi];
