@@ -810,8 +810,8 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     }
     if (sel_large) {
       W.keys = cv.take<uint64_t>((size_t)goff.back() * NB);
-      W.key_mm = cv.take<uint64_t>((size_t)((goff.back() + 63) / 64) * NB * 2);
-      W.key_cnt = cv.take<uint32_t>((size_t)((goff.back() + 63) / 64) * NB);
+      W.key_mm = cv.take<uint64_t>((size_t)((goff.back() + KT_M - 1) / KT_M) * NB * 2);
+      W.key_cnt = cv.take<uint32_t>((size_t)((goff.back() + KT_M - 1) / KT_M) * NB);
       W.lg_kept = cv.take<uint32_t>((size_t)T.LG + 1);
       W.sel = cv.take<SelState>((size_t)T.LG * NB);
       W.hist = cv.take<uint32_t>((size_t)T.LG * NB * 512);
@@ -961,8 +961,8 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         SelFill F{W.SM.keep, W.SM.kf, W.SM.kl, P.fill_value, W.key_cnt,
                   T.lg_off, T.LG, W.lg_kept};
         if (M > 0)
-          hipLaunchKernelGGL(k_keys_transpose<true>, dim3(blocks_for(M, 64)),
-                             dim3(256), 0, st, NB, M, d_members, W.R, W.keys,
+          hipLaunchKernelGGL(k_keys_transpose<true>, dim3(blocks_for(M, KT_M)),
+                             dim3(KT_THREADS), 0, st, NB, M, d_members, W.R, W.keys,
                              W.key_mm, F);
         hipLaunchKernelGGL(k_seg_select, dim3((unsigned)NSEG), dim3(SS_THREADS),
                            0, st, NB, M, T.LG, T.lg_g, T.lg_off, T.lg_k,
@@ -989,8 +989,8 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         const int64_t M = goff.back();
         if (M > 0)
           hipLaunchKernelGGL(k_keys_transpose<false>,
-                             dim3(blocks_for(M, 64)),
-                             dim3(256), 0, st, NB, M, d_members, W.R, W.keys,
+                             dim3(blocks_for(M, KT_M)),
+                             dim3(KT_THREADS), 0, st, NB, M, d_members, W.R, W.keys,
                              nullptr, SelFill{});
         HIP_TRY(hipGetLastError());
         return OTSDB_OK;
@@ -1006,8 +1006,8 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         const int64_t M = goff.back();
         const int64_t NSEG = T.LG * NB;
         hipLaunchKernelGGL(k_keys_transpose<false>,
-                           dim3(blocks_for(M, 64)),
-                           dim3(256), 0, st, NB, M, d_members, W.R, W.keys,
+                           dim3(blocks_for(M, KT_M)),
+                           dim3(KT_THREADS), 0, st, NB, M, d_members, W.R, W.keys,
                            W.key_mm, SelFill{});
         hipLaunchKernelGGL(k_sel_init, dim3(blocks_for(NSEG, 256)), dim3(256),
                            0, st, NB, T.LG, T.lg_g, (const double*)W.out_val,

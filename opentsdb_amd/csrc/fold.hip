@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void k_fold_prep(Params P, BatchDev B,
   if (p > lo) {
     const int64_t k = bucket_of(P, B.ts[p - 1]);
     const int64_t bt = bucket_ts(P, k);
-    const int64_t q = lower_bound_back(B.ts, lo, p, bt);
+    const int64_t q = lower_bound_interp(B.ts, lo, p, bt);
     M st = M::init();
     for (int64_t i = q; i < p; ++i) st.push(point_value(B, i, B.val[i], sf));
     c.prev_ts = bt;

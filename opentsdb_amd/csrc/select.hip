@@ -23,6 +23,13 @@ namespace otsdb {
 
 constexpr uint64_t KEY_NONE = ~0ULL;
 constexpr int SEL_CHUNK = 8192;  // keys per histogram block
+#ifndef OTSDB_KT_M  // members per k_keys_transpose tile: 64 (4 waves) or 128
+#define OTSDB_KT_M 64  // (8 waves, 1 KB key runs per bucket)
+#endif
+constexpr int KT_M = OTSDB_KT_M;
+constexpr int KT_WAVES = KT_M / 16;  // each wave loads 16 members' rows
+constexpr int KT_THREADS = 64 * KT_WAVES;
+static_assert(KT_M == 64 || KT_M == 128, "keys transpose tile");
 
 DEV uint64_t dkey(double v) {  // total order, -0.0 < 0.0 (Double.compareTo)
   const uint64_t u = (uint64_t)__double_as_longlong(v);
@@ -50,26 +57,26 @@ struct SelFill {
   uint32_t* kept;          // [n_lg] the group has a kept series
 };
 
-// One workgroup per 64 members sweeps their rows tile by tile (64 buckets):
+// One workgroup per KT_M members sweeps their rows tile by tile (64 buckets):
 // the members' row offsets are read once, and the next tile's values and
 // states are loaded into registers before the current tile leaves LDS, so
 // each wave keeps a tile's loads in flight while it stores the previous one.
 // mm (optional): per (bucket, tile) min / max non-NONE key, k_seg_select's
 // first pass.
 template <bool FILL>
-__global__ __launch_bounds__(256) void k_keys_transpose(
+__global__ __launch_bounds__(KT_THREADS) void k_keys_transpose(
     int64_t nb, int64_t M, const int64_t* __restrict__ members, Rows R,
     uint64_t* __restrict__ keys, uint64_t* __restrict__ mm, SelFill F) {
-  __shared__ uint64_t tile[64][65];
-  __shared__ int64_t s_row[64];
-  __shared__ int32_t s_kf[64], s_kl[64];
-  __shared__ uint64_t s_mm[4][64][2];
-  __shared__ uint32_t s_cnt[4][64];
+  __shared__ uint64_t tile[KT_M][65];
+  __shared__ int64_t s_row[KT_M];
+  __shared__ int32_t s_kf[KT_M], s_kl[KT_M];
+  __shared__ uint64_t s_mm[KT_WAVES][64][2];
+  __shared__ uint32_t s_cnt[KT_WAVES][64];
   const int64_t ntiles = gridDim.x;
   const int tid = threadIdx.x;
-  const int64_t m0 = (int64_t)blockIdx.x * 64;
+  const int64_t m0 = (int64_t)blockIdx.x * KT_M;
   const int bi = tid & 63, w = tid >> 6;
-  if (tid < 64) {
+  if (tid < KT_M) {
     const int64_t m = m0 + tid;
     const int64_t sr = m < M ? members[m] : -1;
     s_row[tid] = sr >= 0 ? sr * nb : -1;
@@ -95,7 +102,7 @@ __global__ __launch_bounds__(256) void k_keys_transpose(
       while (todo) {
         const int lead = __builtin_ctzll(todo);
         const int64_t gl = readlane_l(g, lead);
-        if (tid == lead && !F.kept[gl]) atomicOr(&F.kept[gl], 1u);
+        if (bi == lead && !F.kept[gl]) atomicOr(&F.kept[gl], 1u);
         todo &= ~__ballot(kp && g == gl);
       }
     }
@@ -107,7 +114,7 @@ __global__ __launch_bounds__(256) void k_keys_transpose(
     const int64_t b = b0 + bi;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int64_t ro = s_row[r * 4 + w];
+      const int64_t ro = s_row[r * KT_WAVES + w];
       const bool in = ro >= 0 && b < nb;
       // loads unconditional in shape: the 16 rows' loads all go out at once
       const int64_t off = in ? ro + b : 0;
@@ -123,7 +130,7 @@ __global__ __launch_bounds__(256) void k_keys_transpose(
     uint32_t nk = 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int mi = r * 4 + w;
+      const int mi = r * KT_WAVES + w;
       uint64_t k;
       if (FILL) {
         const int64_t b = b0 + bi;
@@ -148,16 +155,18 @@ __global__ __launch_bounds__(256) void k_keys_transpose(
     }
     __syncthreads();
     if (b0 + 64 < nb) load(b0 + 64);
-    const int64_t m = m0 + bi;
+    // stores: KT_M consecutive members per bucket, 4 buckets at a time
+    const int sm = tid % KT_M, sg = tid / KT_M;
+    const int64_t m = m0 + sm;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int bj = r * 4 + w;
+      const int bj = r * 4 + sg;
       const int64_t b = b0 + bj;
-      if (m < M && b < nb) keys[b * M + m] = tile[bi][bj];
+      if (m < M && b < nb) keys[b * M + m] = tile[sm][bj];
     }
     if (mm && tid < 64 && b0 + tid < nb) {
 #pragma unroll
-      for (int q = 1; q < 4; ++q) {
+      for (int q = 1; q < KT_WAVES; ++q) {
         mn = s_mm[q][tid][0] < mn ? s_mm[q][tid][0] : mn;
         mx = s_mm[q][tid][1] > mx ? s_mm[q][tid][1] : mx;
         nk += s_cnt[q][tid];
@@ -543,7 +552,7 @@ __global__ __launch_bounds__(SS_THREADS) void k_seg_select(
     if (((k - head) & 1) && tid == 0) f(col[k - 1]);
   };
   // (1) min / max (fused: and count) over the non-NONE keys: from
-  // k_keys_transpose's per-(64-member tile, bucket) partials for the tiles
+  // k_keys_transpose's per-(KT_M-member tile, bucket) partials for the tiles
   // wholly inside the segment, the keys of the partial tiles at its ends
   // directly
   uint64_t mn = ~0ULL, mx = 0;
@@ -555,8 +564,8 @@ __global__ __launch_bounds__(SS_THREADS) void k_seg_select(
       mx = key > mx ? key : mx;
       ++nn;
     };
-    const int64_t o0 = lg_off[lg], ntiles = (M + 63) / 64;
-    const int64_t t_lo = (o0 + 63) / 64, t_hi = (o0 + k) / 64;
+    const int64_t o0 = lg_off[lg], ntiles = (M + KT_M - 1) / KT_M;
+    const int64_t t_lo = (o0 + KT_M - 1) / KT_M, t_hi = (o0 + k) / KT_M;
     if (mm && t_hi > t_lo) {
       const uint64_t* pm = mm + 2 * (b * ntiles);
       for (int64_t t = t_lo + tid; t < t_hi; t += SS_THREADS) {
@@ -564,7 +573,7 @@ __global__ __launch_bounds__(SS_THREADS) void k_seg_select(
         mx = pm[2 * t + 1] > mx ? pm[2 * t + 1] : mx;
         if (fused) nn += cnt_p[b * ntiles + t];
       }
-      const int64_t e0 = t_lo * 64 - o0, e1 = t_hi * 64 - o0;
+      const int64_t e0 = t_lo * KT_M - o0, e1 = t_hi * KT_M - o0;
       for (int64_t i = tid; i < e0; i += SS_THREADS) fold(col[i]);
       for (int64_t i = e1 + tid; i < k; i += SS_THREADS) fold(col[i]);
     } else {
