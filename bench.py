@@ -298,7 +298,8 @@ def decode_figure(eng, config, n_series, reps=5):
                 "): query-time compaction, span assembly, the cells fold",
         "value": n / dr, "unit": "data points/s", "ms_per_query": dr * 1e3,
         "stage_ms": {k: v for k, v in zip(STAGES, st_raw) if v},
-        "kernels": "k_rows_plan + k_rows_write (compaction), k_span_plan "
+        "kernels": "k_rows_uniform (+ k_rows_plan / k_rows_write for the rows "
+                   "it cannot alias: compaction), k_span_plan "
                    "(assembly), k_cells_prep + k_fold<cells>"}
     fold_ms = st_raw[0]
     if fold_ms:
