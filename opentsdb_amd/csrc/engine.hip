@@ -99,6 +99,16 @@ constexpr int64_t kChunk = 256;  // series per cross-series chunk
 // day of points leave the last round of workgroups half empty (C3 fold:
 // 256 -> 2.9 ms, 64 -> 2.57 ms, 32 -> 2.53 ms)
 constexpr int64_t kFoldChunk = 32;
+// Order-sensitive aggregators whose merge of partial states is
+// ill-conditioned (dev: Chan's merge of Welford runs over offset data lands
+// ~1e-11 from the reference's one sequential pass, Aggregators.java:547-568)
+// reduce a group's members in ONE sequential chain per (group, bucket) while
+// the group fits: fold tiles of up to kOrderedFoldChunk members (the LDS
+// progress marks of one workgroup), then the row path's k_group with chunks
+// of up to kOrderedChunk members (one thread walks them in SpanCmp order).
+// Larger groups, and groups spanning ranks, merge ordered chunk partials.
+constexpr int64_t kOrderedFoldChunk = 256;
+constexpr int64_t kOrderedChunk = 16384;
 // below this many (tile, window) workgroups the fold narrows its windows,
 // down to kFoldMinWindow buckets
 constexpr int64_t kFoldMinBlocks = 2048;
@@ -156,6 +166,7 @@ struct otsdb_ctx {
   int64_t max_chunks = 0;  // most chunks in one group
   bool tiles_sel_all = false;
   int64_t tiles_chunk = 0;
+  int64_t tiles_whole = 0;
   std::mutex mu;  // one query at a time per context
   // stage timing (otsdb_prof_*)
   bool prof = false;
@@ -472,10 +483,13 @@ otsdb_status plan_anchored(const otsdb_query_spec* s, AnchoredPlan* A) {
 
 // sel_all: every group (even one without local members) joins the radix
 // select lists — the cross-rank selection protocol needs global segments
+// whole_upto: groups of at most this many members are one tile (one
+// sequential chain), larger ones are cut into chunks of `chunk`
 otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff,
-                         bool sel_all = false, int64_t chunk = kChunk) {
+                         bool sel_all = false, int64_t chunk = kChunk,
+                         int64_t whole_upto = 0) {
   if (c->d_tiles && goff == c->goff_cache && sel_all == c->tiles_sel_all &&
-      chunk == c->tiles_chunk)
+      chunk == c->tiles_chunk && whole_upto == c->tiles_whole)
     return OTSDB_OK;
   const int64_t G = (int64_t)goff.size() - 1;
   std::vector<int64_t> tg, tm0, tm1, mg, mt0, mt1, ag, at0, at1;
@@ -484,10 +498,11 @@ otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff,
   for (int64_t g = 0; g < G; ++g) {
     const int64_t a = goff[g], b = goff[g + 1];
     const int64_t t0 = (int64_t)tg.size();
-    for (int64_t m = a; m < b; m += chunk) {
+    const int64_t ch = (b - a <= whole_upto) ? std::max<int64_t>(b - a, 1) : chunk;
+    for (int64_t m = a; m < b; m += ch) {
       tg.push_back(g);
       tm0.push_back(m);
-      tm1.push_back(std::min(b, m + chunk));
+      tm1.push_back(std::min(b, m + ch));
     }
     const int64_t t1 = (int64_t)tg.size();
     for (int64_t t = t0; t < t1; ++t) single.push_back(t1 - t0 == 1);
@@ -545,6 +560,7 @@ otsdb_status build_tiles(otsdb_ctx* c, const std::vector<int64_t>& goff,
   c->goff_cache = goff;
   c->tiles_sel_all = sel_all;
   c->tiles_chunk = chunk;
+  c->tiles_whole = whole_upto;
   c->n_tiles = T;
   c->n_multi = MG;
   c->n_large = LG;
@@ -736,8 +752,25 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     fold = false;
     WB = NW = 0;
   }
+  bool ordered = false;
+  with_monoid(spec->agg_id, [&](auto tag) {
+    ordered = decltype(tag)::kOrdered;
+  });
+  if (ordered && fold) {
+    // a group past one fold tile takes the row path (one chain per bucket)
+    // when its bucket matrix fits
+    int64_t kmax = 0;
+    for (size_t g = 0; g + 1 < goff.size(); ++g)
+      kmax = std::max(kmax, goff[g + 1] - goff[g]);
+    if (kmax > kOrderedFoldChunk && (double)S * (double)NB <= 2.0e10) {
+      fold = false;
+      WB = NW = 0;
+    }
+  }
   const bool cfold = cells && fold;
-  otsdb_status rc = build_tiles(c, goff, mode == 2, fold ? kFoldChunk : kChunk);
+  otsdb_status rc = build_tiles(
+      c, goff, mode == 2, fold ? kFoldChunk : kChunk,
+      ordered ? (fold ? kOrderedFoldChunk : kOrderedChunk) : 0);
   if (rc) return rc;
   const Tiles T = tiles_of(c, G);
   P.fold_wb = 0;  // (P may come from an earlier pipeline run)

@@ -662,6 +662,81 @@ DEV void seg_scan_dpp(int key, M& st) {
   seg_step_dpp<0x142, 0xA>(key, st);  // row_bcast:15 -> rows 1, 3
   seg_step_dpp<0x143, 0xC>(key, st);  // row_bcast:31 -> rows 2, 3
 }
+// ---- kOrdered monoids (dev): a bucket's points in the reference's order.
+// Downsampler.ValuesInInterval feeds one bucket's values to runDouble in
+// time order (Downsampler.java:461-479) and StdDev folds them in one
+// sequential Welford pass (Aggregators.java:547-568).  The lane-local fold
+// already leaves every run that STARTS inside a lane exact: buckets closed
+// inside a lane, and each lane's tail run.  What the tree would merge is
+// replayed instead: a lane whose points all continue its predecessor's
+// bucket re-pushes them onto the predecessor's state (wave_shr:1), one round
+// per lane of the longest such chain; then every head run is pushed onto its
+// predecessor's final state.  Lane 0's predecessor is the previous step's
+// open bucket (the carry).  Cost: (longest chain + 1) x K pushes per step
+// (a 5 m bucket of 10 s points spans <= 3 whole lanes).
+template <class M, int K>
+DEV M push_run(M st, const BatchDev& B, int sf, int64_t i0, const int64_t* v,
+               uint32_t mask) {
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    if ((mask >> j) & 1u) st.push(point_value(B, i0 + j, v[j], sf));
+  return st;
+}
+template <class M>
+DEV M shr1_state(M st, const M& lane0) {
+  st.template dpp<0x138, 0xF>();  // wave_shr:1
+  return LANE == 0 ? lane0 : st;
+}
+template <class M, int K, class TT>
+DEV void ordered_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
+                      int64_t hi, int64_t i0, const TT* t, const int64_t* v,
+                      RowSink& S, int& err, int nseg, int key, int head_key,
+                      const M& cur, M head, int& carry_key, M& carry) {
+  const int lane = LANE;
+  // the lane's points in [lo, hi), and those of its head run
+  uint32_t vm = 0, hm = 0;
+  if (nseg >= 1) {
+    const TT hb = tbound(P, (int64_t)head_key + 1, TT{});
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int64_t i = i0 + j;
+      const bool ok = i >= lo && i < hi;
+      vm |= (ok ? 1u : 0u) << j;
+      hm |= (ok && t[j] < hb ? 1u : 0u) << j;
+    }
+  }
+  const bool carry_in = carry_key >= 0 && carry_key < P.nb;
+  const M in0 = carry_in ? carry : M::init();
+  // the predecessor's tail key (lane 0: the carry's)
+  const int pkey = dpp32<0x138, 0xF>(carry_in ? carry_key : INT32_MIN, key);
+  // lanes wholly inside their predecessor's bucket (nseg == 0: lanes past
+  // hi that keep_open points at the open bucket, pushing nothing)
+  const bool pass = nseg <= 1 && pkey == key;
+  M out = cur;
+  int rounds = 0;
+  for (uint64_t x = __ballot(pass); x; x &= x << 1) ++rounds;
+  for (int r = 0; r < rounds; ++r) {
+    const M in = shr1_state(out, in0);
+    if (pass) out = push_run<M, K>(in, B, sf, i0, v, vm);
+  }
+  const M fin = shr1_state(out, in0);
+  if (nseg >= 2) {  // head run closes inside this lane
+    if (pkey == head_key) head = push_run<M, K>(fin, B, sf, i0, v, hm);
+    S.put(head_key, head.finish(&err));
+  }
+  if (lane == 0 && carry_in && !(nseg >= 1 && carry_key == head_key))
+    S.put(carry_key, carry.finish(&err));
+  const int next_head = dpp32<0x130, 0xF>(INT32_MIN, head_key);  // wave_shl:1
+  if (nseg >= 1 && lane < 63 && next_head != key) S.put(key, out.finish(&err));
+  Packed p = out.pack();
+  carry_key = __builtin_amdgcn_readlane(key, 63);
+  p.x = readlane_d(p.x, 63);
+  p.y = readlane_d(p.y, 63);
+  p.z = readlane_d(p.z, 63);
+  p.w = readlane_l(p.w, 63);
+  carry = M::unpack(p);
+}
+
 // One step of the bucket reduction over the K consecutive points t[], v[]
 // of every lane (points i0 .. i0+K-1 of the series, step base `base`):
 // lane-local fold, the previous step's open bucket, the segmented wave scan
@@ -733,6 +808,11 @@ DEV void reduce_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
         head_key = k;
       }
     }
+  }
+  if constexpr (M::kOrdered) {
+    ordered_step<M, K, TT>(P, B, sf, lo, hi, i0, t, v, S, err, nseg, cur_key,
+                           head_key, cur, head, carry_key, carry);
+    return;
   }
   // ---- previous step's open bucket
   if (lane == 0) {
@@ -1409,19 +1489,21 @@ __global__ __launch_bounds__(256) void k_group(
   M st = M::init();
   int emit = 0;
   int64_t m = m0;
-  for (; m + 4 <= m1; m += 4) {
-    int64_t off[4];
-    uint8_t sv[4];
-    double v[4];
+  // (the chain is latency-bound on the gathers: 8 members' loads in flight;
+  // chunks of dev groups run up to kOrderedChunk members)
+  for (; m + 8 <= m1; m += 8) {
+    int64_t off[8];
+    uint8_t sv[8];
+    double v[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) off[u] = members[m + u] * nb + b;
+    for (int u = 0; u < 8; ++u) off[u] = members[m + u] * nb + b;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 8; ++u) {
       sv[u] = R.state[off[u]];
       v[u] = R.val[off[u]];
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 8; ++u) {
       if (sv[u]) {
         st.push(v[u]);
         emit |= sv[u] == ST_REAL;

@@ -8,7 +8,13 @@
 // reduction inside a chunk: bit-exact vs the reference for groups of up to
 // CHUNK series); combine() where it reduces in a tree (downsample buckets in
 // a wavefront, chunk and rank merges) — exact for min/max/count/first/last/
-// diff, within 1e-12 relative for sum/avg/dev/mult/squareSum (north star).
+// diff, within 1e-12 relative for sum/avg/mult/squareSum (north star).
+// kOrdered monoids (dev) never take the tree inside a downsample bucket:
+// Welford over offset data (counters near 2^32 with a spread of 10^4) is
+// ill-conditioned, and the reference's own sequential result lies ~1e-11
+// from the exact one, so any other order — Chan's merge included, even in
+// exact arithmetic — lands ~1e-11 from the reference's.  reduce_step hands
+// the running state from lane to lane in point order instead (bit-exact).
 //
 // The 32-byte otsdb_partial {x, y, z, w} is the exchange format between
 // chunks and between ranks (RCCL); pack/unpack map each state onto it.
@@ -63,6 +69,7 @@ struct Packed {
 // SquareSum (:264-295), Count (:620-647): (s, n) with NaN skipping.
 template <int KIND>  // 0 sum, 1 avg, 2 squareSum, 3 count
 struct MSum {
+  static constexpr bool kOrdered = false;
   double s;
   int32_t n;
   DEV static MSum init() { return {0.0, 0}; }
@@ -106,6 +113,7 @@ struct MSum {
 // Min/MimMin (:297-328), Max/MimMax (:330-360).
 template <bool MAX>
 struct MMinMax {
+  static constexpr bool kOrdered = false;
   double m;
   DEV static MMinMax init() { return {MAX ? -__builtin_inf() : __builtin_inf()}; }
   DEV static MMinMax from(double v) {
@@ -134,6 +142,7 @@ struct MMinMax {
 // StdDev.runDouble (:498-571): Welford from the first non-NaN value,
 // population sigma; Chan et al. merge for runs.
 struct MDev {
+  static constexpr bool kOrdered = true;
   double mean, m2;
   int32_t n;
   DEV static MDev init() { return {0.0, 0.0, 0}; }
@@ -192,6 +201,7 @@ struct MDev {
 // First (:810-829), Last (:831-852): NaN is NOT skipped.
 template <bool LAST>
 struct MFirstLast {
+  static constexpr bool kOrdered = false;
   double v;
   int64_t has;
   DEV static MFirstLast init() { return {0.0, 0}; }
@@ -224,6 +234,7 @@ struct MFirstLast {
 // ---------------------------------------------------------------- mult
 // Multiply.runDouble (:476-484): product of every value, NaN included.
 struct MMult {
+  static constexpr bool kOrdered = false;
   double p;
   int64_t has;
   DEV static MMult init() { return {1.0, 0}; }
@@ -258,6 +269,7 @@ struct MMult {
 // Diff.runDouble (:598-618): last value minus the first non-NaN value;
 // 0 when the first non-NaN value is the last value.
 struct MDiff {
+  static constexpr bool kOrdered = false;
   double fnn, last;
   int64_t flags;  // bit0 has_any, bit1 has_fnn, bit2 has_after_fnn
   DEV static MDiff init() { return {0.0, 0.0, 0}; }
@@ -310,6 +322,7 @@ struct MDiff {
 // ---------------------------------------------------------------- none
 // None.runDouble (:439-461): exactly one value, else IllegalDataException.
 struct MNone {
+  static constexpr bool kOrdered = false;
   double v;
   int32_t n;
   DEV static MNone init() { return {0.0, 0}; }

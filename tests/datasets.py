@@ -53,6 +53,12 @@ def random_batch(seed, n_series=40, n_groups=5, span_ms=3 * 3600 * 1000,
                 v[rng.random(m) < nan_frac] = np.nan
             bits = v.view(np.int64)
             f = np.ones(m, np.uint8)
+        elif value_kind == "offset":
+            # large values with a small spread (a gauge of ~3e9 moving by
+            # < 1e4): Welford's result depends on its order at ~1e-11
+            v = 3.0e9 + rng.random(m) * 1.0e4
+            bits = v.view(np.int64)
+            f = np.ones(m, np.uint8)
         elif value_kind == "int":
             bits = rng.integers(-50, 100, m).astype(np.int64)
             f = np.zeros(m, np.uint8)

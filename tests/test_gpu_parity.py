@@ -62,8 +62,12 @@ def cancel_floor(batch, terms):
     return 1e-12 * terms * float(mags.max())
 
 
+# downsampling functions the engine computes bit-identically to the
+# reference: order-free ones, and dev (one sequential Welford pass per
+# bucket in point order, Aggregators.java:547-568) and diff (one subtraction)
 ORDER_FREE_DS = {"min", "max", "mimmin", "mimmax", "first", "last", "count",
-                 "median", "p50", "p75", "p90", "p95", "p99", "p999"}
+                 "median", "p50", "p75", "p90", "p95", "p99", "p999",
+                 "dev", "diff"}
 
 
 def _spec_variant(spec, **kw):
@@ -81,8 +85,8 @@ def _member_scales(spec, batch):
     seeked to the window start like AggregationIterator.java:421-437) — the
     value the aggregator is fed and the magnitude its rounding is relative
     to.  A downsampled value's scale is |value|, or n x max|raw value| of
-    its bucket when the downsampling function subtracts internally (dev,
-    diff, or a sum over raw values of both signs); a rate's is
+    its bucket when it is a sum over raw values of both signs (dev and diff
+    buckets are bit-exact: no scale beyond |value|); a rate's is
     (scale(v0) + scale(v1)) / dt of the two bucket values it differences
     (counterMax added at a counter wrap, RateSpan.java:121-180)."""
     from opentsdb_amd import core as _core
@@ -130,7 +134,7 @@ def _member_scales(spec, batch):
                 _, n = view(v_cnt)
                 mn, mx, n = np.nan_to_num(mn), np.nan_to_num(mx), np.nan_to_num(n)
                 raw = np.maximum(np.abs(mn), np.abs(mx)) * np.maximum(n, 1)
-                cancels = (ds_name in ("dev", "diff")) | ((mn < 0) & (mx > 0))
+                cancels = (mn < 0) & (mx > 0)
                 scale = np.where(cancels, np.maximum(scale, raw), scale)
             if not spec.rate:
                 views.append((dts, dv, scale))
@@ -163,8 +167,8 @@ def contribution_floor(spec, batch, ref):
     a downsampled value or a rate was computed from when that computation
     subtracts).  Nonzero only where rounding can be amplified: the
     contributions have both signs, the aggregator subtracts (dev, diff), or
-    a contribution's own computation does (rates; dev / diff downsampling;
-    sums over raw values of both signs).  Elsewhere the comparator is the
+    a contribution's own computation does (rates; sums over raw values of
+    both signs).  Elsewhere the comparator is the
     pure 1e-12 relative bound (a sum of same-signed terms keeps its relative
     error)."""
     interp = spec.interp
@@ -332,8 +336,10 @@ def test_downsample_functions(engine, ds):
                                   nan_frac=0.05 if kind == "float" else 0)
         for agg in ("sum", "min"):
             spec = _spec(agg, ds, interval="5m")
-            exact = ds in ORDER_FREE or (kind == "int" and ds not in (
-                "dev", "mult"))
+            # dev / diff buckets are bit-exact (dev: one Welford pass in
+            # point order) and the fold feeds them in SpanCmp order
+            exact = ds in ORDER_FREE or ds in ("dev", "diff") or (
+                kind == "int" and ds != "mult")
             # diff buckets and integer data (-50..100) make mixed-sign sums:
             # 30 points per 5 m bucket x 10 series per group
             fl = (cancel_floor(b, 300) if (ds == "diff" or kind == "int")
@@ -404,8 +410,8 @@ def test_rate(engine, ri, fill):
         for aligned in (True, False):
             start = datasets.T0 + (0 if aligned else 61000)
             spec = _spec(agg, ds, fill, start=start, rate=True, ro=RATES[ri])
-            exact = agg != "dev"
-            check(engine, spec, b, exact,
+            # dev over a group of 10: one chain per bucket (bit-exact)
+            check(engine, spec, b, True,
                   where="rate%d/%s/%s/%s" % (ri, fill, agg, aligned))
 
 
@@ -421,14 +427,16 @@ def test_run_all(engine):
 
 def test_big_groups_chunked(engine):
     """Groups larger than one 256-series chunk: chunk partials merged in
-    order (exact for order-free aggregators, 1e-12 otherwise)."""
+    order (exact for order-free aggregators, 1e-12 otherwise; dev reduces
+    the 700 members in one chain per bucket: exact)."""
     b = datasets.random_batch(71, n_series=700, big_group=True,
                               span_ms=3600 * 1000, cadence_ms=30000)
     for agg in ("sum", "avg", "dev", "min", "count", "first", "last", "diff"):
         spec = _spec(agg, "max", end=datasets.T0 + 3600 * 1000)
         # chunk partials merge in order (1e-12); diff: cancellation
         fl = cancel_floor(b, 2) if agg == "diff" else 0.0
-        check(engine, spec, b, agg in ORDER_FREE, where="big/" + agg, floor=fl)
+        check(engine, spec, b, agg in ORDER_FREE or agg == "dev",
+              where="big/" + agg, floor=fl)
 
 
 def test_huge_group_two_level_combine(engine):
@@ -728,7 +736,9 @@ def test_fold_order_cancellation(engine, agg):
     spec = _spec(agg, "avg")
     one_tile = _cancel_batch(7)
     check(engine, spec, one_tile, exact=True, where="cancel/%s/1tile" % agg)
-    many = _cancel_batch(203)  # four 64-member tiles + a partial one
+    many = _cancel_batch(203)  # six 32-member tiles + a partial one
+    if agg == "dev":  # one 256-member tile: the reference's order
+        check(engine, spec, many, exact=True, where="cancel/dev/203")
     first = engine.run(spec, many)
     for _ in range(2):
         again = engine.run(spec, many)

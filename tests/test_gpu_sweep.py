@@ -28,7 +28,10 @@ DSF = ["avg", "sum", "min", "max", "count", "first", "last", "dev",
        "zimsum", "mimmax", "median", "p90"]
 FILLS = ["none", "none", "nan", "null", "zero"]
 INTERVALS = ["30s", "1m", "2m", "5m", "7m", "13m", "1h"]
-EXACT_DS = ("min", "max", "count", "first", "last", "mimmax", "median", "p90")
+# downsamplers computed bit-identically to the reference: order-free ones,
+# and dev (one sequential Welford pass per bucket, in point order)
+EXACT_DS = ("min", "max", "count", "first", "last", "mimmax", "median", "p90",
+            "dev")
 EXACT_AGG = ("min", "max", "mimmin", "mimmax", "count", "first", "last",
              "median", "p50", "p95", "p99", "ep90r3", "ep99r7")
 
@@ -72,6 +75,17 @@ def test_random_query_sweep(engine, seed):
     b, spec, exact, where = _case(seed)
     # 1e-12 relative; an absolute 1e-12 x sum|contributions| only at points
     # whose contributions have both signs (contribution_floor)
+    check(engine, spec, b, exact, where=where, floor="contributions")
+
+
+@pytest.mark.parametrize("seed", [5266])
+def test_sweep_regressions(engine, seed):
+    """Seeds sweep_many.py found diverging.  5266: `mult` of 4 series' 5 m
+    `dev` of counter rates (increments of 0-1,000 on ~3e9 every 10 s) — the
+    dev buckets were merged in a lane tree (Chan's formula) where the
+    reference runs one sequential Welford pass; on such offset data the two
+    orders differ at ~1e-10 (now replayed in point order: bit-exact)."""
+    b, spec, exact, where = _case(seed)
     check(engine, spec, b, exact, where=where, floor="contributions")
 
 
