@@ -102,3 +102,59 @@ def test_contribution_floor_is_set_where_signs_meet():
             n_nonzero += int((f > 0).sum())
             n_points += len(f)
     assert 0 < n_nonzero < n_points
+
+
+def _tree_dev(xs, run=8):
+    """A bucket's population sigma from Welford runs of `run` consecutive
+    points merged with Chan's formula (the lane tree the engine no longer
+    uses for dev)."""
+    n, mean, m2 = 0, 0.0, 0.0
+    for i in range(0, len(xs), run):
+        c = xs[i:i + run]
+        cn, cm, cm2 = 1, c[0], 0.0
+        for x in c[1:]:
+            cn += 1
+            nm = cm + (x - cm) / cn
+            cm2 += (x - cm) * (x - nm)
+            cm = nm
+        if n == 0:
+            n, mean, m2 = cn, cm, cm2
+            continue
+        d = cm - mean
+        tot = n + cn
+        mean = mean + d * (cn / tot)
+        m2 = m2 + cm2 + d * d * (n * cn / tot)
+        n = tot
+    return 0.0 if n < 2 else float(np.sqrt(m2 / n))
+
+
+def test_comparator_rejects_a_reordered_welford():
+    """dev downsampling replayed in another order (runs of 8 merged with
+    Chan's formula) over counters near 2^32: the comparator, run with the
+    sweeps' floor, rejects it (the round-3 floor of n x max|raw| per dev
+    bucket let exactly this through: sweep seed 5266)."""
+    from opentsdb_amd import core
+    from opentsdb_amd.batch import groups_from_ids
+    from tests import datasets
+    b = datasets.random_batch(5266, n_series=6, n_groups=6, counter=True,
+                              empty_frac=0.0, outside=False)
+    g_off, members = groups_from_ids(np.arange(6), 6)  # a group per series
+    b.group_offsets, b.group_members = g_off, members
+    t0, t1 = datasets.T0, datasets.T0 + 3 * 3600 * 1000
+    spec = core.make_spec(t0, t1, core.Aggregators.get("sum"),
+                          core.DownsamplingSpecification("5m-dev"), t0, t1)
+    ref = pyoracle.group_by(spec, b)
+    fl = contribution_floor(spec, b, ref)
+    mut = []
+    for g, r in enumerate(ref):
+        s = int(members[g])
+        ts = b.ts[b.offsets[s]:b.offsets[s + 1]]
+        v = b.val[b.offsets[s]:b.offsets[s + 1]].astype(np.float64)
+        m = r.copy()
+        for k, bt in enumerate(r["ts"]):
+            sel = (ts >= bt) & (ts < bt + 300000)
+            m["bits"][k] = np.float64(_tree_dev(list(v[sel]))).view(np.int64)
+        mut.append(m)
+    assert any((m["bits"] != r["bits"]).any() for m, r in zip(mut, ref))
+    with pytest.raises(AssertionError):
+        compare([_Res(p) for p in mut], ref, False, "reordered-dev", fl)
