@@ -370,6 +370,26 @@ def mixed_cells_figure(eng, config, n_series, db_groups, res, reps):
     return out
 
 
+def host_cpus():
+    """nproc, the CPUs this process may run on, and the CPU model."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    return {"nproc": os.cpu_count() or 1, "affinity_cpus": aff,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "cpu_model": model}
+
+
 def cpu_baseline(config, target_s):
     """The oracle (iterator-faithful C restatement of the reference's
     single-threaded per-group evaluation) timed on a bounded sample of the
@@ -402,7 +422,14 @@ def cpu_baseline(config, target_s):
     # (ii) of SURVEY §8d: the same sample with whole groups sharded over the
     # host threads (ctypes drops the GIL inside the oracle call).  Only for
     # host-grouped configs: the reference evaluates one group on one thread.
-    threads = min(16, os.cpu_count() or 1)
+    # every host thread this process may use: its CPU affinity, bounded by
+    # the box's per-GPU share (OMP_NUM_THREADS is set to it there; nproc and
+    # os.cpu_count() report the whole machine)
+    host = host_cpus()
+    threads = host["affinity_cpus"]
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
+    out["host"] = host
     if workload.CONFIGS[config]["group"] == "host" and n >= 10 * threads > 10:
         from concurrent.futures import ThreadPoolExecutor
         cut = [((n // 10) * i // threads) * 10 for i in range(threads + 1)]

@@ -181,6 +181,8 @@ struct otsdb_ctx {
   size_t cells_col_cap = 0;
   void* cal = nullptr;  // calendar bucket edges of the current query
   size_t cal_cap = 0;
+  void* acal_fill = nullptr;  // stage A' (calendar fill): compacted batch
+  size_t acal_fill_cap = 0;
   void* acal = nullptr;  // per-series calendar: chains, anchors, series'
   size_t acal_cap = 0;   // chain positions and bucket-start timestamps
   void* dec_ws = nullptr;  // decode workspace
@@ -283,9 +285,6 @@ otsdb_status check_spec(const otsdb_query_spec* s) {
     if (s->cal_anchors[0] > s->start_ms)
       return fail(OTSDB_E_ILLEGAL_ARGUMENT,
                   "no calendar anchor at or before start_ms");
-    if (s->fill != OTSDB_FILL_NONE)
-      return fail(OTSDB_E_UNSUPPORTED,
-                  "fill policies over per-series calendar grids");
   } else if (s->use_calendar && !s->run_all) {
     if (!s->cal_edges || s->n_cal_edges < 2)
       return fail(OTSDB_E_UNSUPPORTED,
@@ -440,6 +439,11 @@ otsdb_status make_params(const otsdb_query_spec* s, Params* P,
 struct AnchoredPlan {
   std::vector<int64_t> U, chain_end;
   int64_t seek_ts = 0;
+  int64_t stop_b = 0;  // stage B's stop bound (NONE: U's first edge > end)
+  // fill != none: FillingDownsampler's own grid FD (U then holds FD, then
+  // the table's end t_end and t_end + 1: calendar.hip)
+  std::vector<int64_t> FD;
+  int64_t t_end = 0;
   otsdb_query_spec derived;
 };
 
@@ -472,6 +476,37 @@ otsdb_status plan_anchored(const otsdb_query_spec* s, AnchoredPlan* A) {
   if (e[k] == INT64_MAX)
     return fail(OTSDB_E_UNSUPPORTED, "calendar chain ends before the seek");
   A->seek_ts = e[k];
+  if (s->fill != OTSDB_FILL_NONE) {
+    // FillingDownsampler.java:113-135: previousInterval(start) = e[k0], then
+    // the chain's steps while < previousInterval(end), advanced once when
+    // the two coincide
+    const int64_t k0 = s->cal_anchor_edge[j];
+    const int64_t je = (int64_t)(std::upper_bound(s->cal_anchors,
+                                                  s->cal_anchors + na,
+                                                  s->end_ms) -
+                                 s->cal_anchors) - 1;
+    int64_t end_ts = s->cal_anchors[je];
+    if (end_ts == e[k0]) {
+      if (e[k0 + 1] == INT64_MAX)
+        return fail(OTSDB_E_UNSUPPORTED, "calendar chain ends at the start");
+      end_ts = e[k0 + 1];
+    }
+    A->FD.clear();
+    int64_t kk = k0;
+    for (; e[kk] != INT64_MAX && e[kk] < end_ts; ++kk) A->FD.push_back(e[kk]);
+    if (e[kk] == INT64_MAX)
+      return fail(OTSDB_E_UNSUPPORTED, "calendar chain ends before the window");
+    // every point stage A' keeps lies on an FD edge: the last bucket's end
+    // only has to lie past it (and at end_ms, so the table's grid ends there)
+    A->t_end = std::max(s->end_ms, A->FD.back() + 1);
+    A->U = A->FD;
+    A->U.push_back(A->t_end);
+    A->U.push_back(A->t_end + 1);
+  }
+  {
+    const auto it = std::upper_bound(A->U.begin(), A->U.end(), s->end_ms);
+    A->stop_b = it == A->U.end() ? INT64_MAX : *it;
+  }
   A->derived = *s;
   A->derived.cal_edges = A->U.data();
   A->derived.n_cal_edges = (int64_t)A->U.size();
@@ -1316,6 +1351,88 @@ otsdb_status run_device_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
                              const otsdb_batch* b, otsdb_result* out,
                              std::vector<int64_t>& goff);
 
+otsdb_status scan_excl(void* tmp, size_t tmp_bytes, const int64_t* in,
+                       int64_t* out, int64_t n, hipStream_t st);
+size_t scan_tmp_bytes(int64_t n, hipStream_t st);
+
+// FillingDownsampler over per-series grids (calendar.hip, stage A'): the
+// points whose own bucket starts on the filling grid, compacted, then the
+// filling calendar pipeline over that grid.
+otsdb_status run_anchored_fill(otsdb_ctx* c, const AnchoredPlan& A,
+                               const otsdb_batch* b, int64_t* vts,
+                               const AnchoredCal& AC,
+                               const std::vector<void*>& pp, otsdb_result* out,
+                               std::vector<int64_t>& goff) {
+  hipStream_t st = c->stream;
+  const otsdb_query_spec* spec = &A.derived;
+  const int64_t S = b->n_series;
+  int64_t Np = 0;
+  if (S > 0) {
+    HIP_TRY(hipMemcpyAsync(&Np, b->offsets + S, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  const int64_t nfd = (int64_t)A.FD.size();
+  const size_t tmpb = scan_tmp_bytes(S, st);
+  // (upper bound of the compacted copy: every point + 2 per series)
+  const int64_t Nc = Np + 2 * S;
+  auto carve = [&](char* base) {
+    Carve cv{base};
+    void* p[7];
+    p[0] = cv.take<int64_t>(nfd);
+    p[1] = cv.take<uint8_t>(std::max<int64_t>(Np, 1));
+    p[2] = cv.take<int64_t>(S + 1);
+    p[3] = cv.take<int64_t>(S + 1);
+    p[4] = cv.take<int64_t>(std::max<int64_t>(Nc, 2));
+    p[5] = cv.take<int64_t>(std::max<int64_t>(Nc, 2));
+    p[6] = cv.take<uint8_t>(std::max<int64_t>(Nc, 1));
+    void* t = cv.take<char>(tmpb);
+    return std::make_pair(cv.off + 256, std::vector<void*>{p[0], p[1], p[2], p[3],
+                                                          p[4], p[5], p[6], t});
+  };
+  otsdb_status rc = ensure(&c->acal_fill, &c->acal_fill_cap, carve(nullptr).first);
+  if (rc) return rc;
+  auto q = carve((char*)c->acal_fill).second;
+  int64_t* fd = (int64_t*)q[0];
+  uint8_t* on = (uint8_t*)q[1];
+  int64_t* cnt = (int64_t*)q[2];
+  int64_t* offs = (int64_t*)q[3];
+  int64_t* ts2 = (int64_t*)q[4];
+  int64_t* val2 = (int64_t*)q[5];
+  uint8_t* isf2 = b->is_float ? (uint8_t*)q[6] : nullptr;
+  HIP_TRY(hipMemcpyAsync(fd, A.FD.data(), 8 * nfd, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(cnt + S, 0, 8, st));
+  BatchDev B{S, b->offsets, b->ts_ms, b->val, b->is_float, b->series_float};
+  if (S > 0) {
+    hipLaunchKernelGGL(k_cal_fill_count, dim3(blocks_for(S, 4)), dim3(256), 0,
+                       st, spec->start_ms, spec->end_ms, B, AC,
+                       (const int64_t*)pp[4], (const int64_t*)pp[5],
+                       (const int64_t*)pp[6], fd, nfd, vts, on, cnt, c->d_err);
+    rc = scan_excl(q[7], tmpb, cnt, offs, S, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_cal_fill_write, dim3(blocks_for(S, 4)), dim3(256), 0,
+                       st, spec->start_ms, A.t_end, B, (const int64_t*)vts, on,
+                       (const int64_t*)offs, ts2, val2, isf2);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (c->h_small[0] & ERR_CAL_RANGE)
+      return fail(OTSDB_E_UNSUPPORTED,
+                  "a point lies before its series' calendar chain");
+  }
+  otsdb_batch vb = *b;
+  vb.n_points = 0;
+  if (S > 0) {
+    HIP_TRY(hipMemcpyAsync(&vb.n_points, offs + S, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  vb.offsets = offs;
+  vb.ts_ms = ts2;
+  vb.val = val2;
+  vb.is_float = isf2;
+  return run_device_impl(c, spec, &vb, out, goff);
+}
+
 // Per-series calendar grids: stage A rewrites the timestamps to the series'
 // own bucket starts (calendar.hip), stage B runs the calendar pipeline over
 // the union grid.
@@ -1365,10 +1482,11 @@ otsdb_status run_anchored(otsdb_ctx* c, const otsdb_query_spec* spec,
                        st, spec->start_ms, spec->end_ms, A.seek_ts, B, AC,
                        (int64_t*)pp[4], (int64_t*)pp[5], (int64_t*)pp[6],
                        c->d_err);
-    hipLaunchKernelGGL(k_cal_vts, dim3(blocks_for(S, 4)), dim3(256), 0, st,
-                       spec->start_ms, B, AC, (const int64_t*)pp[4],
-                       (const int64_t*)pp[5], (const int64_t*)pp[6], vts,
-                       c->d_err);
+    if (A.FD.empty())
+      hipLaunchKernelGGL(k_cal_vts, dim3(blocks_for(S, 4)), dim3(256), 0, st,
+                         spec->start_ms, A.stop_b, (int)spec->rate, B, AC,
+                         (const int64_t*)pp[4], (const int64_t*)pp[5],
+                         (const int64_t*)pp[6], vts, c->d_err);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
                            hipMemcpyDeviceToHost, st));
@@ -1379,6 +1497,7 @@ otsdb_status run_anchored(otsdb_ctx* c, const otsdb_query_spec* spec,
   }
   otsdb_batch vb = *b;
   vb.ts_ms = vts;
+  if (!A.FD.empty()) return run_anchored_fill(c, A, b, vts, AC, pp, out, goff);
   return run_device_impl(c, &A.derived, &vb, out, goff);
 }
 
@@ -2052,6 +2171,7 @@ void otsdb_ctx_destroy(otsdb_ctx* c) {
   if (c->ws2) hipFree(c->ws2);
   if (c->cal) hipFree(c->cal);
   if (c->acal) hipFree(c->acal);
+  if (c->acal_fill) hipFree(c->acal_fill);
   if (c->cells_ws) hipFree(c->cells_ws);
   if (c->cells_col) hipFree(c->cells_col);
   if (c->rows_ws) hipFree(c->rows_ws);
