@@ -1161,7 +1161,8 @@ otsdb_status finish(otsdb_ctx* c, int64_t G, otsdb_result* out) {
     return fail(OTSDB_E_ILLEGAL_STATE, "Got Infinity");
   if (err & ERR_RAW_DUP)
     return fail(OTSDB_E_UNSUPPORTED,
-                "timestamps do not increase inside a span (raw group-by)");
+                "raw group-by: timestamps decrease inside a span, or a "
+                "timestamp repeats more than 65,536 times");
   if (err & ERR_X1_MASK)
     return fail(OTSDB_E_ILLEGAL_STATE, "x1 beyond the millisecond mask");
   if (err & ERR_SEL_TOO_BIG)
@@ -1265,7 +1266,10 @@ otsdb_status run_raw(otsdb_ctx* c, const otsdb_query_spec* spec,
     return fail(OTSDB_E_UNSUPPORTED, "raw group-by over %lld candidate points",
                 (long long)C);
   // ---- phase 2 workspace: candidates, sort temp, emitted-point groups
-  const int end_bit = std::max(1, 64 - __builtin_clzll((uint64_t)std::max<int64_t>(spec->end_ms, 1)));
+  // keys (ts << 16) | occurrence (raw.hip); candidates have ts <= end_ms
+  if (spec->end_ms >= kRawTsMax)
+    return fail(OTSDB_E_UNSUPPORTED, "raw group-by past 2^47 ms");
+  const int end_bit = kOccBits + std::max(1, 64 - __builtin_clzll((uint64_t)std::max<int64_t>(spec->end_ms, 1)));
   size_t sort_tmp = 0;
   if (C > 0)
     HIP_TRY(rocprim::segmented_radix_sort_keys(
@@ -1273,12 +1277,13 @@ otsdb_status run_raw(otsdb_ctx* c, const otsdb_query_spec* spec,
         (unsigned)C, (unsigned)G, segb, sege, 0, end_bit, st));
   uint64_t *kin, *kout;
   void* tmp;
-  int32_t* ugrp;
+  int32_t *ugrp, *uocc;
   auto carve2 = [&](char* base) {
     Carve cv{base};
     kin = cv.take<uint64_t>(C + 1);
     kout = cv.take<uint64_t>(C + 1);
     ugrp = cv.take<int32_t>(C + 1);
+    uocc = cv.take<int32_t>(C + 1);
     tmp = cv.take<char>(sort_tmp + 1);
     return cv.off + 256;
   };
@@ -1298,14 +1303,15 @@ otsdb_status run_raw(otsdb_ctx* c, const otsdb_query_spec* spec,
   hipLaunchKernelGGL(k_raw_unique, dim3(blocks_for(G, 4)), dim3(256), 0, st, G,
                      (const int64_t*)segb, (const int64_t*)sege,
                      (const uint64_t*)kout, counts, (const int64_t*)nullptr,
-                     (int64_t)0, (int64_t*)nullptr, (int32_t*)nullptr, 0);
+                     (int64_t)0, (int64_t*)nullptr, (int32_t*)nullptr,
+                     (int32_t*)nullptr, 0);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, G,
                      (const int64_t*)counts, out->offsets);
   hipLaunchKernelGGL(k_raw_unique, dim3(blocks_for(G, 4)), dim3(256), 0, st, G,
                      (const int64_t*)segb, (const int64_t*)sege,
                      (const uint64_t*)kout, counts,
                      (const int64_t*)out->offsets, out->capacity, out->ts, ugrp,
-                     1);
+                     uocc, 1);
   HIP_TRY(hipMemcpyAsync(&c->h_small[2], out->offsets + G, 8,
                          hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
@@ -1327,7 +1333,8 @@ otsdb_status run_raw(otsdb_ctx* c, const otsdb_query_spec* spec,
         hipLaunchKernelGGL(k_raw_select, dim3((unsigned)nb), dim3(64), 0, st, P,
                            V, median, u0, n_out, b->group_offsets,
                            b->group_members, (const int32_t*)ugrp,
-                           (const int64_t*)out->ts, out->val, out->is_int,
+                           (const int32_t*)uocc, (const int64_t*)out->ts,
+                           out->val, out->is_int,
                            (uint64_t*)c->dec_ws, std::max<int64_t>(kmax, 1),
                            c->d_err);
       }
@@ -1337,8 +1344,9 @@ otsdb_status run_raw(otsdb_ctx* c, const otsdb_query_spec* spec,
         hipLaunchKernelGGL(k_raw_eval<Mo>, dim3(blocks_for(n_out, 256)),
                            dim3(256), 0, st, P, V, (int)spec->agg_id, mixed,
                            n_out, b->group_offsets, b->group_members,
-                           (const int32_t*)ugrp, (const int64_t*)out->ts,
-                           out->val, out->is_int, c->d_err);
+                           (const int32_t*)ugrp, (const int32_t*)uocc,
+                           (const int64_t*)out->ts, out->val, out->is_int,
+                           c->d_err);
       });
       if (!ok) return fail(OTSDB_E_NO_SUCH_ELEMENT, "aggregator %d", spec->agg_id);
     }

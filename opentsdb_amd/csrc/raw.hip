@@ -196,9 +196,21 @@ __global__ void k_raw_cand_count(Params P, RawView V, int64_t M,
   count[m] = b - a;
 }
 
-// one wavefront per member: copy the candidate timestamps; a timestamp that
-// does not increase inside a span flags ERR_RAW_DUP (the Java iterator would
-// emit a repeated timestamp; E_UNSUPPORTED hands such spans back to it)
+// Repeated timestamps inside a span.  The iterator's next() moves every
+// span whose "next" slot holds the minimum timestamp, one point each
+// (AggregationIterator.java:514-588): a timestamp held k times by one span
+// is emitted k times, the m-th emission moving that span's m-th copy into
+// its current slot while the other spans keep theirs.  An emission is the
+// pair (x, m) — m the occurrence of x inside the span that holds it — and
+// the candidates carry it as the key (x << 16) | m: the group's distinct
+// keys, in order, are its emissions.
+constexpr int kOccBits = 16;
+constexpr int64_t kOccMax = (int64_t)1 << kOccBits;
+constexpr int64_t kRawTsMax = (int64_t)1 << (63 - kOccBits);
+
+// one wavefront per member: the candidate keys; a timestamp that decreases
+// inside a span, a run of more than 2^16 copies or a timestamp past 2^47 ms
+// flags ERR_RAW_DUP (E_UNSUPPORTED)
 __global__ __launch_bounds__(256) void k_raw_cand_fill(
     Params P, RawView V, int64_t M, const int64_t* __restrict__ members,
     const int64_t* __restrict__ cand_off, uint64_t* __restrict__ keys,
@@ -212,8 +224,12 @@ __global__ __launch_bounds__(256) void k_raw_cand_fill(
   int bad = 0;
   for (int64_t i = a + lane; i < b; i += 64) {
     const int64_t t = V.ts[i];
-    keys[o + i] = (uint64_t)t;
-    if (i > a && V.ts[i - 1] >= t) bad = 1;
+    // occurrence of t: the copies before it in the span (from its seek:
+    // copies before the first candidate were never in the next slot)
+    int64_t occ = 0;
+    while (i - occ > a && V.ts[i - occ - 1] == t && occ < kOccMax) ++occ;
+    keys[o + i] = ((uint64_t)t << kOccBits) | (uint64_t)occ;
+    if ((i > a && V.ts[i - 1] > t) || occ >= kOccMax || t >= kRawTsMax) bad = 1;
   }
   if (__ballot(bad) && lane == 0) atomicOr(err_word, ERR_RAW_DUP);
 }
@@ -229,14 +245,14 @@ __global__ void k_raw_segments(int64_t G, const int64_t* __restrict__ goff,
   seg_e[g] = cand_off[goff[g + 1]];
 }
 
-// one wavefront per group: distinct sorted candidates.  mode 0 counts,
-// mode 1 writes the emitted timestamps and their group.
+// one wavefront per group: distinct sorted candidate keys.  mode 0 counts,
+// mode 1 writes the emitted timestamps, their occurrence and their group.
 __global__ __launch_bounds__(256) void k_raw_unique(
     int64_t G, const int64_t* __restrict__ seg_b,
     const int64_t* __restrict__ seg_e, const uint64_t* __restrict__ sorted,
     int64_t* __restrict__ counts, const int64_t* __restrict__ out_off,
     int64_t cap, int64_t* __restrict__ out_ts, int32_t* __restrict__ ugrp,
-    int mode) {
+    int32_t* __restrict__ uocc, int mode) {
   const int lane = LANE;
   const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (g >= G) return;
@@ -249,7 +265,8 @@ __global__ __launch_bounds__(256) void k_raw_unique(
     if (mode && d) {
       const int64_t p = pos + __popcll(m & ((1ULL << lane) - 1));
       if (p < cap) {
-        out_ts[p] = (int64_t)sorted[i];
+        out_ts[p] = (int64_t)(sorted[i] >> kOccBits);
+        uocc[p] = (int32_t)(sorted[i] & (kOccMax - 1));
         ugrp[p] = (int32_t)g;
       }
     }
@@ -259,21 +276,26 @@ __global__ __launch_bounds__(256) void k_raw_unique(
 }
 
 // ------------------------------------------------------------------------
-// One span's slots at emission x (AggregationIterator.next/moveToNext):
+// One span's slots at emission (x, occ) (AggregationIterator.next/
+// moveToNext):
 //   state 0: not started (x < first point): current slot empty, next slot
 //            holds the first point
 //   state 1: contributing (first <= x <= last, or any x with a rate span
 //            whose junk first rate sits in the current slot): current = the
 //            latest point <= x (the junk rate before the second rate point),
-//            next = the one after it, if any
-//   state 2: ended / empty: both slots empty (zeroed / TIME_MASK)
+//            next = the one after it, if any.  With k copies of x in the
+//            span, emission (x, occ) holds copy min(occ, k - 1).
+//   state 2: ended / empty: both slots empty (zeroed / TIME_MASK).  A span
+//            expires at the next() after its last point entered the current
+//            slot (:519-526): after emission (last, k - 1).
 // ------------------------------------------------------------------------
 struct Slots {
   int state;
   int64_t cur, nxt;  // point indices; nxt = -1 when the slot is TIME_MASK
 };
 
-DEV Slots span_slots(const Params& P, const RawView& V, int64_t s, int64_t x) {
+DEV Slots span_slots(const Params& P, const RawView& V, int64_t s, int64_t x,
+                     int occ) {
   Slots r{2, -1, -1};
   const int64_t a = V.lo[s], b = V.hi[s];
   if (P.rate) {
@@ -292,6 +314,18 @@ DEV Slots span_slots(const Params& P, const RawView& V, int64_t s, int64_t x) {
   }
   r.state = 1;
   r.cur = last_le(V.ts, a, b, x);
+  if (V.ts[r.cur] == x && (occ > 0 || (r.cur > a && V.ts[r.cur - 1] == x))) {
+    // copies of x: [f, r.cur]; emission occ holds copy occ
+    int64_t f = r.cur;
+    while (f > a && V.ts[f - 1] == x) --f;
+    if (r.cur - f >= occ) {
+      r.cur = f + occ;
+    } else if (r.cur == b - 1) {  // fewer copies: the last point expired
+      r.state = 2;
+      r.cur = r.nxt = -1;
+      return r;
+    }
+  }
   r.nxt = r.cur + 1 < b ? r.cur + 1 : -1;
   return r;
 }
@@ -397,13 +431,14 @@ template <class M>
 __global__ __launch_bounds__(256) void k_raw_eval(
     Params P, RawView V, int agg, int mixed, int64_t n_out,
     const int64_t* __restrict__ goff, const int64_t* __restrict__ members,
-    const int32_t* __restrict__ ugrp, const int64_t* __restrict__ out_ts,
-    int64_t* __restrict__ out_val, uint8_t* __restrict__ out_isint,
-    int* err_word) {
+    const int32_t* __restrict__ ugrp, const int32_t* __restrict__ uocc,
+    const int64_t* __restrict__ out_ts, int64_t* __restrict__ out_val,
+    uint8_t* __restrict__ out_isint, int* err_word) {
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= n_out) return;
   const int32_t g = ugrp[u];
   const int64_t x = out_ts[u];
+  const int occ = uocc[u];
   const int64_t m0 = goff[g], m1 = goff[g + 1];
   int err = 0;
   // isInteger: decided over every span's slots before any value is read
@@ -411,7 +446,7 @@ __global__ __launch_bounds__(256) void k_raw_eval(
   if (is_int && mixed) {
     for (int64_t m = m0; m < m1 && is_int; ++m) {
       const int64_t s = members[m];
-      is_int = !slots_float(V, s, span_slots(P, V, s, x));
+      is_int = !slots_float(V, s, span_slots(P, V, s, x, occ));
     }
   }
   int64_t bits;
@@ -419,7 +454,7 @@ __global__ __launch_bounds__(256) void k_raw_eval(
     LongAcc acc(agg);
     for (int64_t m = m0; m < m1; ++m) {
       const int64_t s = members[m];
-      const Slots q = span_slots(P, V, s, x);
+      const Slots q = span_slots(P, V, s, x, occ);
       if (q.state == 1) acc.push(span_long(P, V, q, x, &err));
     }
     bits = acc.finish(&err);
@@ -427,7 +462,7 @@ __global__ __launch_bounds__(256) void k_raw_eval(
     M st = M::init();
     for (int64_t m = m0; m < m1; ++m) {
       const int64_t s = members[m];
-      const Slots q = span_slots(P, V, s, x);
+      const Slots q = span_slots(P, V, s, x, occ);
       if (q.state == 1) st.push(span_double(P, V, s, q, x, &err));
     }
     const double r = st.finish(&err);
@@ -465,15 +500,17 @@ DEV double pct_position(double p, int64_t n, int est) {
 __global__ __launch_bounds__(64) void k_raw_select(
     Params P, RawView V, int median, int64_t u0, int64_t n_out,
     const int64_t* __restrict__ goff, const int64_t* __restrict__ members,
-    const int32_t* __restrict__ ugrp, const int64_t* __restrict__ out_ts,
-    int64_t* __restrict__ out_val, uint8_t* __restrict__ out_isint,
-    uint64_t* __restrict__ slab, int64_t kmax, int* err_word) {
+    const int32_t* __restrict__ ugrp, const int32_t* __restrict__ uocc,
+    const int64_t* __restrict__ out_ts, int64_t* __restrict__ out_val,
+    uint8_t* __restrict__ out_isint, uint64_t* __restrict__ slab,
+    int64_t kmax, int* err_word) {
   __shared__ uint32_t hist[256];
   const int lane = LANE;
   const int64_t u = u0 + blockIdx.x;
   if (u >= n_out) return;
   const int32_t g = ugrp[u];
   const int64_t x = out_ts[u];
+  const int occ = uocc[u];
   const int64_t m0 = goff[g], m1 = goff[g + 1];
   int err = 0;
   int fl = 0;
@@ -481,7 +518,7 @@ __global__ __launch_bounds__(64) void k_raw_select(
   if (typed)
     for (int64_t m = m0 + lane; m < m1; m += 64) {
       const int64_t s = members[m];
-      fl |= slots_float(V, s, span_slots(P, V, s, x));
+      fl |= slots_float(V, s, span_slots(P, V, s, x, occ));
     }
   const bool is_int = typed && __ballot(fl) == 0;
   uint64_t* keys = slab + (int64_t)blockIdx.x * kmax;
@@ -492,7 +529,7 @@ __global__ __launch_bounds__(64) void k_raw_select(
     uint64_t key = 0;
     if (m < m1) {
       const int64_t s = members[m];
-      const Slots q = span_slots(P, V, s, x);
+      const Slots q = span_slots(P, V, s, x, occ);
       if (q.state == 1) {
         if (is_int) {
           const int64_t v = span_long(P, V, q, x, &err);

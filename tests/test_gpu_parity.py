@@ -616,14 +616,59 @@ def test_raw_windows_and_big_groups(engine):
               where="rawbig/" + agg)
 
 
-def test_raw_duplicate_timestamps_unsupported(engine):
+def _dup_batch(seed, kind, n_series=16, n_groups=3):
+    """random_batch with repeated timestamps: runs of 2-4 copies of a point
+    (new values) inside spans, at span ends and at the window's edges."""
     from opentsdb_amd.batch import HostBatch
-    t = datasets.T0
-    groups = [[[(t, 1, 0), (t + 1000, 2, 0), (t + 1000, 3, 0)],
-               [(t, 5, 0), (t + 2000, 6, 0)]]]
-    b = HostBatch.from_groups(groups)
-    with pytest.raises(core.UnsupportedOperationException):
-        engine.run(_raw("sum", end=t + 5000), b)
+    b = datasets.random_batch(seed, n_series=n_series, n_groups=n_groups,
+                              value_kind=kind, cadence_ms=37000)
+    rng = np.random.default_rng(seed)
+    offs, ts, val, isf = [0], [], [], []
+    for s in range(b.n_series):
+        t = b.ts[b.offsets[s]:b.offsets[s + 1]]
+        v = b.val[b.offsets[s]:b.offsets[s + 1]]
+        f = b.is_float[b.offsets[s]:b.offsets[s + 1]]
+        reps = np.ones(len(t), np.int64)
+        if len(t):
+            pick = rng.random(len(t)) < 0.08
+            if rng.random() < 0.5:
+                pick[-1] = True  # copies of the span's last point
+            reps[pick] = rng.integers(2, 5, int(pick.sum()))
+        idx = np.repeat(np.arange(len(t)), reps)
+        t2, f2 = t[idx], f[idx]
+        v2 = v[idx].copy()
+        first = np.r_[True, idx[1:] != idx[:-1]] if len(idx) else idx
+        newv = (rng.random(len(idx)) * 100.0).view(np.int64) if kind != "int" \
+            else rng.integers(-50, 100, len(idx)).astype(np.int64)
+        v2[~first] = np.where(f2[~first] == 1, newv[~first],
+                              rng.integers(0, 100, len(idx))[~first])
+        ts.append(t2)
+        val.append(v2)
+        isf.append(f2)
+        offs.append(offs[-1] + len(t2))
+    return HostBatch(np.array(offs, np.int64), np.concatenate(ts),
+                     np.concatenate(val), np.concatenate(isf), None,
+                     b.group_offsets, b.group_members)
+
+
+@pytest.mark.parametrize("kind", ["float", "int", "mixed"])
+def test_raw_repeated_timestamps(engine, kind):
+    """A span holding a timestamp k times: the iterator emits it k times,
+    the m-th emission taking that span's m-th copy while the other spans
+    hold theirs (or interpolate), and a span whose last point is repeated
+    expires after its last copy (AggregationIterator.java:514-588) —
+    against the oracle's line-by-line iterator, bit-exact."""
+    b = _dup_batch(113, kind)
+    assert (np.diff(b.ts)[np.diff(b.ts) == 0]).size > 0
+    for agg in ("sum", "avg", "max", "dev", "count", "first", "last", "diff",
+                "mimmin", "p90", "median"):
+        for interp in (None, core.Interpolation.PREV):
+            spec = _raw(agg, start=datasets.T0 + 37000 * 3, interp=interp)
+            check(engine, spec, b, True,
+                  where="rawdup/%s/%s/%s" % (kind, agg, interp))
+    # downsampled: repeated timestamps fall into one bucket, in order
+    check(engine, _spec("sum", "dev", interval="5m"), b, True,
+          where="dsdup/%s" % kind)
 
 
 # ------------------------------------------------------------ generator
