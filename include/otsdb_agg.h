@@ -171,9 +171,14 @@ typedef struct {
    * the window, or just the ones the batch's series take), and so must
    * previousInterval(start_ms) (the seek, Downsampler.java:419-429).  Series
    * grids then differ, and the output timestamps are the union of the
-   * series' bucket starts (AggregationIterator.next).  FillingDownsampler
-   * fills over such grids (fill != NONE) -> OTSDB_E_UNSUPPORTED, as do the
-   * multi-GPU partial / selection entry points.  HOST memory.             */
+   * series' bucket starts (AggregationIterator.next).  With fill != NONE
+   * the FillingDownsampler's own grid is the chain from previousInterval(
+   * start_ms) to previousInterval(end_ms) (FillingDownsampler.java:113-135):
+   * previousInterval(end_ms) must then be the largest anchor <= end_ms too.
+   * A point past its chain's last edge is OTSDB_E_UNSUPPORTED only when a
+   * query reads it (rate queries; the first bucket past the window).  The
+   * multi-GPU partial / selection entry points -> OTSDB_E_UNSUPPORTED.
+   * HOST memory.                                                          */
   const int64_t* cal_anchors;
   const int64_t* cal_anchor_edge;
   int64_t n_cal_anchors;
@@ -299,7 +304,8 @@ otsdb_status otsdb_agg_finalize_device(otsdb_ctx* ctx,
  *
  * otsdb_sel_hist_device returns without waiting for its kernels: the
  * caller's collective must be ordered after them on hip_stream (an RCCL
- * all-reduce enqueued there is; a host-staged one must synchronise first).
+ * all-reduce enqueued there is); a binding that reads `hist` from the host
+ * or from another stream calls otsdb_sel_hist_wait(ctx, hip_stream) first.
  * 8-bit digits rather than §8e's 11-bit ones: 2 x 256 bins per (group,
  * bucket) keep each all-reduce at 2 KB per bucket (C5: 2.9 MB a pass, against
  * 23.6 MB at 11 bits), at two more passes over the local keys.
@@ -320,6 +326,9 @@ otsdb_status otsdb_sel_hist_device(otsdb_ctx* ctx, int32_t pass,
                                    void* hip_stream);
 otsdb_status otsdb_sel_finish_device(otsdb_ctx* ctx, uint32_t* hist_last,
                                      otsdb_result* out, void* hip_stream);
+/* Blocks until the kernels otsdb_sel_hist_device enqueued on hip_stream (NULL:
+ * the context's stream) are done, so `hist` is readable from anywhere.      */
+otsdb_status otsdb_sel_hist_wait(otsdb_ctx* ctx, void* hip_stream);
 
 /* ---- compacted-cell decode (RowSeq) ------------------- */
 /* The storage rows of a query as the scanner hands them to Span.addRow

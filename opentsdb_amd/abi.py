@@ -139,7 +139,7 @@ EXPORTS = [
     "otsdb_agg_finalize_device", "otsdb_gen_counts_device",
     "otsdb_gen_fill_device", "otsdb_prof_enable", "otsdb_prof_read",
     "otsdb_decode_cells_device", "otsdb_sel_prepare_device",
-    "otsdb_sel_hist_device", "otsdb_sel_finish_device",
+    "otsdb_sel_hist_device", "otsdb_sel_hist_wait", "otsdb_sel_finish_device",
     "otsdb_encode_cells_device", "otsdb_agg_run_cells_device",
     "otsdb_compact_rows_device", "otsdb_span_assemble_device",
     "otsdb_agg_run_raw_device", "otsdb_agg_run_raw", "otsdb_agg_run_cells",
@@ -204,6 +204,8 @@ def load(path=None):
     lib.otsdb_sel_prepare_device.restype = C.c_int
     lib.otsdb_sel_hist_device.argtypes = [vp, i32, vp, vp, vp, vp, vp]
     lib.otsdb_sel_hist_device.restype = C.c_int
+    lib.otsdb_sel_hist_wait.argtypes = [vp, vp]
+    lib.otsdb_sel_hist_wait.restype = C.c_int
     lib.otsdb_sel_finish_device.argtypes = [vp, vp, PR, vp]
     lib.otsdb_sel_finish_device.restype = C.c_int
     lib.otsdb_encode_cells_device.argtypes = [vp, PB, vp, vp, vp,

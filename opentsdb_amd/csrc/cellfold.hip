@@ -125,6 +125,7 @@ __global__ __launch_bounds__(256) void k_cells_prep(Params P, CellsFold CF,
   };
   const int64_t t_first = ts_at(0, r0), t_last = ts_at(Ns - 1, r1 - 1);
   if (!(t_first <= P.end_ms && t_last >= P.start_ms)) {
+    if (P.check_order) atomicOr(err_word, ERR_SPEC_MISS);
     store(false, 0, 0, r0, C.val_off[r0], qw, 8, 0, 0, 0.0);
     return;
   }
@@ -205,6 +206,9 @@ __global__ __launch_bounds__(256) void k_cells_prep(Params P, CellsFold CF,
       of_has = 1;
     }
   }
+  // verbatim storage rows: every point of the series must be streamed (and
+  // so checked for order) by the fold
+  if (P.check_order && (lo != 0 || hi != Ns)) atomicOr(err_word, ERR_SPEC_MISS);
   store(true, lo, hi, rlo, vlo, qw, vl0, of_has, of_ts, of_val);
 }
 
@@ -344,18 +348,31 @@ __global__ __launch_bounds__(256) void k_cells_fold_prep(
   c.bnd = p;
   int err = 0;
   if (p > lo) {
-    // the bucket of point p - 1 and its points [q, p), scanning back
+    // the bucket of point p - 1 and its points [q, p): galloping back from
+    // p - 1 brackets the bucket's first point, a binary search finds it
+    // (a bucket of millisecond points holds millions: no point-by-point
+    // walk), each probe's row by row_of
     int64_t rq = (p - 1 >= first_pt(r) || r == r0) ? r : r - 1;
     if (p - 1 < first_pt(rq)) rq = row_of(p - 1);
     const int64_t bt = bucket_ts(P, bucket_of(P, ts_in(p - 1, rq)));
-    int64_t q = p - 1;
-    while (q > lo) {
-      int64_t rr = rq;
-      if (q - 1 < first_pt(rq)) rr = rq - 1;
-      if (ts_in(q - 1, rr) < bt) break;
-      --q;
-      rq = rr;
+    auto ts_of = [&](int64_t m) { return ts_in(m, row_of(m)); };
+    int64_t hi_q = p - 1, lo_q = lo - 1;  // ts(hi_q) >= bt; ts(lo_q) < bt
+    for (int64_t step = 1;; step <<= 1) {
+      const int64_t m = hi_q - step;
+      if (m <= lo_q) break;
+      if (ts_of(m) < bt) {
+        lo_q = m;
+        break;
+      }
+      hi_q = m;
     }
+    while (hi_q - lo_q > 1) {
+      const int64_t m = lo_q + ((hi_q - lo_q) >> 1);
+      if (ts_of(m) < bt) lo_q = m;
+      else hi_q = m;
+    }
+    const int64_t q = hi_q;
+    rq = row_of(q);
     c.prev_ts = bt;
     c.prev_val = fold_run(q, rq, voff_of(q, rq), p, INT64_MAX, &err);
   }
@@ -546,6 +563,8 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
     }
   };
   int32_t p = (int32_t)uni(mc->pa);
+  const int32_t pa0 = p;
+  uint32_t t_last_prev = 0;  // check_order: the previous step's last time
   L2Touch pq_, pv_;
   const int32_t n_guard = pe - p + 64;  // every step consumes >= 1 point
   int dbg_n = 0;
@@ -696,6 +715,20 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
       fault |= ERR_CELLS_GENERIC;
       break;
     }
+    if (P.check_order) {
+      // verbatim storage rows: each point strictly after its predecessor
+      // (the lane before it; lane 0: the previous step's last point)
+      const uint32_t tp = (uint32_t)dpp32<0x138, 0xF>((int32_t)t_last_prev,
+                                                      (int32_t)t[K - 1]);
+      int ob = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        if (j < nv) ob |= (j == 0 ? (p0 > pa0 && t[0] <= tp) : t[j] <= t[j - 1]);
+      if (__ballot(ob)) {
+        fault |= ERR_NOT_SORTED;
+        break;
+      }
+    }
     const int32_t vo1 = __builtin_amdgcn_readlane(w_vo, j0 + 1);
     const int32_t vo2 = __builtin_amdgcn_readlane(w_vo, j0 + 2);
     const int32_t vo3 = __builtin_amdgcn_readlane(w_vo, j0 + 3);
@@ -798,6 +831,7 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
     }
     const int32_t k_last =
         hs == sb ? k_hi : bucket_rel(P, cells_pick<K>(t, hs - 1 - p));
+    if (P.check_order) t_last_prev = cells_pick<K>(t, hs - 1 - p);
     // a step cut at a row rule (not at a bucket edge) leaves the bucket of
     // its last point open: it carries into the next step (keep_open)
 #if defined(OTSDB_CELLS_ABL) && OTSDB_CELLS_ABL == 1  // timing: no reduction

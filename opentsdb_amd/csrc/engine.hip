@@ -93,6 +93,7 @@ inline int64_t jmod(int64_t a, int64_t b) { return a % b; }
 inline int64_t align_down(int64_t t, int64_t iv) { return t - jmod(t, iv); }
 
 constexpr int64_t kChunk = 256;  // series per cross-series chunk
+
 // members per tile of the ordered fold: one tile is one workgroup that
 // streams all its members' points, so big groups (C3's 7.8k-series
 // datacenters per GPU) are cut finer than kChunk — 256-member tiles of one
@@ -113,6 +114,10 @@ constexpr int64_t kOrderedChunk = 16384;
 // down to kFoldMinWindow buckets
 constexpr int64_t kFoldMinBlocks = 2048;
 constexpr int64_t kFoldMinWindow = 128;
+
+// the storage rows cannot be taken verbatim (run_raw_verbatim): flagged on
+// the context, never returned through the C-ABI
+otsdb_status spec_miss(otsdb_ctx* c);
 
 struct Carve {
   char* base;
@@ -167,6 +172,8 @@ struct otsdb_ctx {
   bool tiles_sel_all = false;
   int64_t tiles_chunk = 0;
   int64_t tiles_whole = 0;
+  bool verbatim = false;  // run_raw_verbatim: the cells query's rows as stored
+  bool spec_miss = false;  // ... and they cannot be: the caller compacts
   std::mutex mu;  // one query at a time per context
   // stage timing (otsdb_prof_*)
   bool prof = false;
@@ -803,6 +810,9 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
     }
   }
   const bool cfold = cells && fold;
+  // verbatim storage rows: the single-window cells fold only (it checks
+  // what compaction would change; window boundaries it does not see)
+  if (c->verbatim && (!cfold || NW > 1)) return spec_miss(c);
   otsdb_status rc = build_tiles(
       c, goff, mode == 2, fold ? kFoldChunk : kChunk,
       ordered ? (fold ? kOrderedFoldChunk : kOrderedChunk) : 0);
@@ -812,7 +822,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   // few tiles (small queries, e.g. C1's 100 groups of 10 series): narrower
   // fold windows give the grid more workgroups — each window's workgroup
   // streams only that window's points (k_fold_prep hands it the context)
-  if (fold && T.T > 0 && NB > kFoldMinWindow &&
+  if (fold && !c->verbatim && T.T > 0 && NB > kFoldMinWindow &&
       T.T * NW < kFoldMinBlocks) {
     const int64_t want = (kFoldMinBlocks + T.T - 1) / T.T;  // windows
     int64_t wb = (NB + want - 1) / want;
@@ -1653,6 +1663,7 @@ otsdb_status run_cells_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
                        0, st, R, S, cells->row_series, series_row);
     BatchDev B{S, nullptr, nullptr, nullptr, nullptr, nullptr};
     Work W;
+    P.check_order = c->verbatim ? 1 : 0;
     rc = run_pipeline(c, spec, B, b->group_members, goff, P, W, 0, nullptr,
                       nullptr, &C, series_row);
     if (rc) return rc;
@@ -1662,6 +1673,9 @@ otsdb_status run_cells_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
                            hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const int e = (int)(c->h_small[0] & 0xFFFFFFFF);
+    if (c->verbatim && (e & (ERR_CORRUPT_CELL | ERR_CELLS_GENERIC |
+                             ERR_NOT_SORTED | ERR_SPEC_MISS)))
+      return spec_miss(c);
     if (e & ERR_CORRUPT_CELL)
       return fail(OTSDB_E_ILLEGAL_DATA,
                   "Corrupted value: couldn't break down into individual values");
@@ -1672,6 +1686,8 @@ otsdb_status run_cells_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
       return finish(c, G, out);
     }
   }
+  // (verbatim storage rows take only the cells fold)
+  if (c->verbatim) return spec_miss(c);
   // decode to a columnar batch in the context's own buffer, then the
   // columnar pipeline (raw group-by, median/percentile or "all" downsampling,
   // mixed-width columns)
@@ -2105,6 +2121,48 @@ otsdb_status cells_buffer(otsdb_ctx* c, int which, int64_t R, int64_t qb,
   return OTSDB_OK;
 }
 
+// The storage rows taken verbatim, when they can be: every row one
+// compacted column (k_rows_shape), the rows of each series in base-time
+// order, every series in one group — the rows ARE the compacted, assembled
+// spans, viewed in place (qual_off / val_off point into the column offsets).
+// The cells fold checks the rest as it streams (Params.check_order).
+// Flags spec_miss when the view does not hold or the query would not
+// stream every point through the cells fold; the caller then compacts.
+otsdb_status spec_miss(otsdb_ctx* c) {
+  c->spec_miss = true;
+  return OTSDB_E_UNSUPPORTED;
+}
+
+otsdb_status run_raw_verbatim(otsdb_ctx* c, const otsdb_query_spec* spec,
+                              const otsdb_raw_rows* raw, const otsdb_batch* b,
+                              otsdb_result* out, std::vector<int64_t>& goff) {
+  hipStream_t st = c->stream;
+  const int64_t R = raw->n_rows;
+  if (R <= 0 || goff.empty() || goff.back() != b->n_series ||
+      !(spec->ds_interval_ms > 0) || spec->run_all || anchored(spec))
+    return spec_miss(c);
+  RawDev D{R, raw->row_col_off, raw->col_qual_off, raw->qual, raw->col_val_off,
+           raw->val, raw->col_ts};
+  int* bad = (int*)c->d_mm;
+  HIP_TRY(hipMemsetAsync(bad, 0, sizeof(int), st));
+  hipLaunchKernelGGL(k_rows_shape, dim3(blocks_for(R, 256)), dim3(256), 0, st,
+                     D, raw->row_series, raw->row_base_s, bad);
+  HIP_TRY(hipGetLastError());
+  int h[3] = {0, 0, 0};
+  int64_t c0 = 0;
+  HIP_TRY(hipMemcpyAsync(h, bad, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&c0, raw->row_col_off, 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (h[0]) return spec_miss(c);
+  const otsdb_cells cc{R, raw->row_series, raw->row_base_s,
+                       raw->col_qual_off + c0, raw->qual,
+                       raw->col_val_off + c0, raw->val};
+  c->verbatim = true;
+  const otsdb_status rc = run_cells_impl(c, spec, &cc, b, out, goff);
+  c->verbatim = false;
+  return rc;
+}
+
 // The query from storage rows: compaction -> span assembly -> the cells
 // query (DEVICE pointers).
 otsdb_status run_raw_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
@@ -2113,6 +2171,15 @@ otsdb_status run_raw_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
                           std::vector<int64_t>& goff) {
   hipStream_t st = c->stream;
   if (!raw->row_series) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null row_series");
+  if (!raw->row_base_s || !raw->row_col_off || !raw->col_qual_off ||
+      !raw->col_val_off || (raw->n_rows > 0 && (!raw->qual || !raw->val)))
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null raw row array");
+  {
+    c->spec_miss = false;
+    const otsdb_status v = run_raw_verbatim(c, spec, raw, b, out, goff);
+    if (!c->spec_miss) return v;
+    c->spec_miss = false;
+  }
   int64_t nk = 0, tq = 0, tv = 0;
   otsdb_cells_out co;
   otsdb_status rc;
@@ -2543,6 +2610,13 @@ otsdb_status otsdb_sel_hist_device(otsdb_ctx* c, int32_t pass,
   // no host sync: the caller's collective on the same stream consumes
   // hist_out (RCCL enqueues behind it; a gloo staging copy waits for it)
   HIP_TRY(hipGetLastError());
+  return OTSDB_OK;
+}
+
+otsdb_status otsdb_sel_hist_wait(otsdb_ctx* c, void* hip_stream) {
+  if (!c) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(hip_stream ? (hipStream_t)hip_stream : c->stream));
   return OTSDB_OK;
 }
 

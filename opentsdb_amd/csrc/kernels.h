@@ -42,6 +42,11 @@ enum : int {
   ERR_RAW_DUP = 32,     // timestamps not increasing inside a raw span
   ERR_CAL_RANGE = 64,   // a point past the window outside the calendar table
   ERR_INTERNAL = 128,   // engine invariant broken          -> E_DEVICE
+  // the storage-row query's verbatim speculation (Params.check_order) does
+  // not hold: a series' points do not strictly increase, or a series is not
+  // streamed whole -> the full compaction path runs instead
+  ERR_NOT_SORTED = 1 << 22,
+  ERR_SPEC_MISS = 1 << 23,
 };
 
 struct Params {
@@ -85,6 +90,11 @@ struct Params {
   // buckets per window of the ordered fold (k_fold / k_fold_prep); 0: the
   // largest the aggregator state allows (fold_wb)
   int32_t fold_wb;
+  // the cells query runs on storage rows taken verbatim (no compaction):
+  // k_cells_prep flags a series not streamed whole, the cells fold a point
+  // that does not follow its predecessor strictly (ERR_SPEC_MISS /
+  // ERR_NOT_SORTED: the caller compacts and re-runs)
+  int32_t check_order;
 };
 
 // value bits of an absent bucket in sentinel rows: a signalling NaN, which

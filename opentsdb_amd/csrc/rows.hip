@@ -1470,6 +1470,37 @@ __global__ __launch_bounds__(256) void k_rows_alias(
 }
 
 // The per-row arrays of an aliased output (thread per row; no bytes move).
+// k_rows_shape: the storage rows' shapes only (no qualifier byte read) —
+// can the query take every row verbatim?  Each row one column (no append /
+// annotation column beside it) of an even qualifier length, with value
+// bytes; rows of a series with strictly increasing base
+// times (Span.addRow then keeps them as they are, Span.java:177-220) and
+// series in order.  What compaction would still change inside such a
+// column (offsets out of order or repeated, a second qualifier width,
+// value lengths that do not add up) the cells fold checks as it streams
+// the points (Params.check_order); any miss re-runs the full path.
+__global__ __launch_bounds__(256) void k_rows_shape(
+    RawDev D, const int64_t* __restrict__ row_series,
+    const int64_t* __restrict__ row_base_s, int* __restrict__ bad) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int b = 0;
+  if (r < D.R) {
+    const int64_t c = D.row_col_off[r];
+    const int64_t ql = D.col_qoff[c + 1] - D.col_qoff[c];
+    const int64_t vl = D.col_voff[c + 1] - D.col_voff[c];
+    b |= D.row_col_off[r + 1] - c != 1;
+    // (a single 2-byte cell is verbatim unless checkForFixup changes it:
+    // then its value bytes do not add up to its qualifier's length, which
+    // the fold checks)
+    b |= ql < 2 || (ql & 1) || vl < 1;
+    if (r > 0) {
+      const int64_t s0 = row_series[r - 1], s1 = row_series[r];
+      b |= s1 < s0 || (s1 == s0 && row_base_s[r] <= row_base_s[r - 1]);
+    }
+  }
+  if (__ballot(b) && LANE == 0) atomicOr(bad, 1);
+}
+
 __global__ __launch_bounds__(256) void k_rows_meta(
     int64_t R, const int64_t* __restrict__ row_series,
     const int64_t* __restrict__ row_base_s, const uint8_t* __restrict__ kind,

@@ -290,6 +290,13 @@ class ShardedSelect:
             self._stream()))
         return self.hist
 
+    def wait(self):
+        """The histogram kernels are done (otsdb_sel_hist_wait): for a
+        host-staged collective that does not read through torch's current
+        stream."""
+        self.engine._check(self.engine.lib.otsdb_sel_hist_wait(
+            self.engine.ctx, self._stream()))
+
     def set_prev(self, global_hist):
         self.prev.copy_(global_hist)
 
@@ -313,6 +320,8 @@ def run_sharded_select(engine, spec, dbatch, n_groups_global, group=None):
     all_reduce(emit, "max", group)
     for p in range(8):
         h = sel.hist_pass(p)
+        if _staged(group):
+            sel.wait()  # the host copy below reads h
         all_reduce(h, "sum", group)
         sel.set_prev(h)
     return sel.finish()

@@ -80,3 +80,25 @@ def encode_batch(batch, rng=None, float4_frac=0.0, ms_frac=0.0):
                 qual=np.frombuffer(bytes(qb) + b"\0", np.uint8),
                 val_off=np.array(vo, np.int64),
                 val=np.frombuffer(bytes(vb) + b"\0", np.uint8))
+
+
+def batch_from_rows(rows, like):
+    """A HostBatch of the points in compacted rows [(series, base_s, qual,
+    val)] (rows of a series in base-time order; RowSeq decode by the
+    oracle), with `like`'s series count and groups."""
+    from oracle import pyoracle
+    from opentsdb_amd.batch import HostBatch
+    per = [[] for _ in range(like.n_series)]
+    for s, base, q, v in rows:
+        per[s].append(pyoracle.decode_row(q, v, base))
+    offs, ts, bits, isf = [0], [], [], []
+    for s in range(like.n_series):
+        pts = (np.concatenate(per[s]) if per[s]
+               else np.zeros(0, pyoracle.POINT))
+        ts.append(pts["ts"])
+        bits.append(pts["bits"])
+        isf.append(1 - pts["is_int"].astype(np.uint8))
+        offs.append(offs[-1] + len(pts))
+    return HostBatch(np.array(offs, np.int64), np.concatenate(ts),
+                     np.concatenate(bits), np.concatenate(isf), None,
+                     like.group_offsets, like.group_members)

@@ -229,6 +229,92 @@ def test_query_from_storage_rows_aliasing(engine, breaker):
             where="alias/%s" % breaker)
 
 
+def _stage_calls(engine):
+    """How many times each engine stage ran since the last read
+    (otsdb_prof_read; stage 5 = query-time compaction)."""
+    import ctypes as C
+    ms = (C.c_double * 8)()
+    n = (C.c_int64 * 8)()
+    engine.lib.otsdb_prof_read(engine.ctx, ms, n, 8, 1)
+    return list(n)
+
+
+@pytest.mark.parametrize("breaker", [None, "unsorted", "repeat", "repeat-nofix",
+                                     "length", "ms-row", "window"])
+def test_query_from_storage_rows_verbatim(engine, breaker):
+    """Storage rows of single compacted columns over a whole-range window:
+    the query takes the rows as stored (no compaction pass: k_rows_shape,
+    then the cells fold checks every point's order as it streams).  A column
+    compaction would change — offsets out of order or repeated, value bytes
+    that do not add up, an ms row in a seconds series — or a window that
+    does not stream every point sends the query through the full path:
+    either way the result (or the error) is the oracle's."""
+    import torch
+    from opentsdb_amd.engine import DeviceResult
+    from tests.test_gpu_parity import compare
+    from tests.test_gpu_decode import _device_batch, _result_points
+    from tests import cells as C
+    hb = datasets.random_batch(48, n_series=24, n_groups=4, span_ms=5 * 3600000,
+                               cadence_ms=10000, outside=False)
+    hb.ts[:] = hb.ts - hb.ts % 1000
+    hb.is_float = np.ones(len(hb.ts), np.uint8)
+    rows = []
+    for s in range(hb.n_series):
+        a, b = hb.offsets[s], hb.offsets[s + 1]
+        for base, q, v in C.encode_series(hb.ts[a:b], hb.val[a:b],
+                                          hb.is_float[a:b]):
+            rows.append((s, base, [(q, v, 0)]))
+    fix = breaker != "repeat-nofix"
+    k = 30
+    s_k, base_k, cols = rows[k]
+    pts = rows_fuzz.split_points(cols[0][0], cols[0][1])
+    if breaker == "unsorted":
+        pts[3], pts[4] = pts[4], pts[3]
+        rows[k] = (s_k, base_k, [rows_fuzz.compacted(pts) + (0,)])
+    elif breaker in ("repeat", "repeat-nofix"):
+        pts.insert(5, (pts[5][0], pts[4][1]))  # offset 5 again, other bytes
+        rows[k] = (s_k, base_k, [rows_fuzz.compacted(pts) + (0,)])
+    elif breaker == "length":
+        q, v = cols[0][0], cols[0][1]
+        rows[k] = (s_k, base_k, [(q, v[:-2] + v[-1:], 0)])  # a byte short
+    elif breaker == "ms-row":
+        ms = [(rows_fuzz.ms_qual(((qq[0] << 8 | qq[1]) >> 4) * 1000,
+                                 qq[1] & 0xF), vv) for qq, vv in pts]
+        rows[k] = (s_k, base_k, [rows_fuzz.compacted(ms) + (0,)])
+    raw = storage.HostRawRows(rows, with_ts=True).to_device()
+    raw.n_series = hb.n_series
+    db = _device_batch(hb, "float")
+    lo, hi = int(hb.ts.min()), int(hb.ts.max())
+    if breaker == "window":
+        lo += 600000
+    spec = core.make_spec(lo, hi, core.Aggregators.get("sum"),
+                          core.DownsamplingSpecification("1m-avg"), lo, hi)
+    # the oracle over the points the full path compacts from the rows
+    try:
+        crow = _oracle_rows(rows, fix)
+        ref_err = None
+    except pyoracle.OracleError as e:
+        ref_err = e.status
+    res = DeviceResult(torch, db.n_groups, 4 * len(hb.ts) + 64, "cuda")
+    engine.lib.otsdb_prof_enable(engine.ctx, 1)
+    _stage_calls(engine)
+    try:
+        if ref_err is not None:
+            with pytest.raises(core.OpenTSDBException):
+                storage.run_raw_device(engine, spec, raw, db, res,
+                                       fix_duplicates=fix)
+            return
+        storage.run_raw_device(engine, spec, raw, db, res, fix_duplicates=fix)
+        calls = _stage_calls(engine)
+    finally:
+        engine.lib.otsdb_prof_enable(engine.ctx, 0)
+    assert (calls[5] == 0) == (breaker is None), calls  # compaction ran?
+    from tests.cells import batch_from_rows
+    ref = pyoracle.group_by(spec, batch_from_rows(crow, hb))
+    compare(_result_points(res, db.n_groups), ref, False,
+            where="verbatim/%s" % breaker)
+
+
 def test_compaction_first_failing_row_decides(engine):
     """The first failing row in row order decides the exception (the
     scanner compacts rows in order)."""
