@@ -196,8 +196,13 @@ DEV void fold_fill_gap(const Params& P, FoldSink<A>& F, int32_t a, int32_t e,
 }
 
 // Turns the ring's buckets [flushed, limit) (all final) into contributions.
+#ifdef OTSDB_FLUSH_NOINLINE  // tuning builds: the flush as a real call
+#define FLUSH_FN __device__ __attribute__((noinline))
+#else
+#define FLUSH_FN DEV
+#endif
 template <class A>
-DEV void fold_flush(const Params& P, FoldSink<A>& F, int32_t limit) {
+FLUSH_FN void fold_flush(const Params& P, FoldSink<A>& F, int32_t limit) {
   if (limit <= F.flushed) return;
 #ifdef OTSDB_FOLD_ABL_NOFLUSH  // timing ablation: no contributions
   F.flushed = limit;
@@ -384,7 +389,9 @@ DEV void fold_member(const Params& P, const BatchDev& B, FoldSink<A>& F,
     // step's loads are in flight (nothing below reads t[] / v[])
     const bool carry_ok = carry_key >= 0 && carry_key < P.nb;
     int32_t limit = carry_ok ? carry_key : prev_hi + 1;
+#ifndef OTSDB_FOLD_FLUSH_LATE
     if (limit - F.flushed >= FOLD_FL) fold_flush(P, F, limit);
+#endif
     const bool full = base >= lo_eff && base + PTS <= pb;
     const int64_t last_i = (base + PTS < pb ? base + PTS : pb) - 1;
     // the step's last bucket: lane 63's last point when the step is full
@@ -433,6 +440,13 @@ DEV void fold_member(const Params& P, const BatchDev& B, FoldSink<A>& F,
       prev_hi = k_hi;
       base += PTS;
     }
+#ifdef OTSDB_FOLD_FLUSH_LATE
+    {
+      const int32_t lim = (carry_key >= 0 && carry_key < P.nb) ? carry_key
+                                                                 : prev_hi + 1;
+      if (lim - F.flushed >= FOLD_FL) fold_flush(P, F, lim);
+    }
+#endif
   }
   if (carry_key >= 0 && carry_key < P.nb && lane == 0)
     S.put(carry_key, carry.finish(&err));
