@@ -1788,7 +1788,7 @@ otsdb_status compact_large(otsdb_ctx* c, const RawDev& D, int fix,
   HIP_TRY(rocprim::segmented_radix_sort_keys(
       nullptr, t_keys, (const uint64_t*)nullptr, (uint64_t*)nullptr,
       (unsigned)ncell, (unsigned)n_large, (const int64_t*)nullptr,
-      (const int64_t*)nullptr, 0, 54, st));
+      (const int64_t*)nullptr, 0, kLargeKeyBits, st));
   const size_t t_scan = scan_tmp_bytes(NC, st);
   const size_t t_sort = std::max(std::max(t_pairs, t_keys), t_scan);
   uint64_t *ckey, *ckey2, *rkey, *rkey2;
@@ -1837,12 +1837,14 @@ otsdb_status compact_large(otsdb_ctx* c, const RawDev& D, int fix,
   t = t_sort;
   HIP_TRY(rocprim::segmented_radix_sort_keys(
       tmp, t, (const uint64_t*)rkey, rkey2, (unsigned)ncell,
-      (unsigned)n_large, (const int64_t*)segb, (const int64_t*)sege, 0, 54,
-      st));
+      (unsigned)n_large, (const int64_t*)segb, (const int64_t*)sege, 0,
+      kLargeKeyBits, st));
+  // (rkey, free after the sort, holds the heap order of rows with unsorted
+  // columns)
   hipLaunchKernelGGL(k_large_merge, dim3((unsigned)n_large), dim3(64), 0, st,
                      D, fix, LS, gen_base, gen_n, (const CellRec*)rec,
-                     (const uint64_t*)rkey2, (const int*)bad, stq, stv, out_q,
-                     out_v, first_err);
+                     (const uint64_t*)rkey2, (const int*)bad, rkey, stq, stv,
+                     out_q, out_v, first_err);
   HIP_TRY(hipGetLastError());
   return OTSDB_OK;
 }

@@ -1174,7 +1174,18 @@ __global__ __launch_bounds__(64) void k_rows_general(
 //   segmented radix sort of the keys = the heap order;
 //   k_large_merge   merge_sorted + finish_row, one wavefront per row.
 // A LARGE row holding a column whose cells go back in time (never written by
-// the write path or compaction) is OTSDB_E_UNSUPPORTED.
+// the write path or compaction): that column's cells are keyed past every
+// offset (kLargeUnsorted), so the sort leaves the in-order columns' cells
+// merged in heap order and the unsorted columns' cells after them, column by
+// column in rank order; k_large_merge then replays the heap over those
+// streams (the merged in-order cells are one stream — popping the least head
+// among in-order columns IS their merged order — and each unsorted column
+// one more), up to 63 unsorted columns per row.
+// sort key offset of a cell of an unsorted column (past every 22-bit ms
+// offset; the segmented key sort runs over bits [0, kLargeKeyBits))
+constexpr uint32_t kLargeUnsorted = 1u << 22;
+constexpr int kLargeKeyBits = 55;
+
 struct LargeWs {
   LargeSlots LS;
   uint64_t* ckey;     // [NC] rank keys
@@ -1355,7 +1366,13 @@ __global__ __launch_bounds__(256) void k_large_recs(
       n += __popcll(w.mask);
     }
     if (!mode && lane == 0) ccount[p0 + b] = n;
-    if (mode && unsorted && lane == 0) atomicOr(&bad[bsl], 1);
+    if (mode && unsorted) {
+      // its cells sort after every in-order cell, in column order
+      for (int64_t i = lane; i < n; i += 64)
+        rkey[rb + bir + i] =
+            ((uint64_t)kLargeUnsorted << 32) | (uint64_t)(uint32_t)(bir + i);
+      if (lane == 0) atomicOr(&bad[bsl], 1);
+    }
   }
 }
 
@@ -1371,28 +1388,91 @@ __global__ void k_large_segs(LargeSlots LS, int64_t n_slots,
   sege[sl] = gen_base[r] + gen_n[r];
 }
 
+// The heap order of a row with unsorted columns (CompactionQueue.
+// defaultMergeDataPoints pops the least (offset, rank) head,
+// CompactionQueue.java:549-584): lane 0 holds the in-order stream's head,
+// lane u the u-th unsorted column's; each step the wave's least head pops
+// into perm (keys in merge_sorted's form).  Returns false past 63 unsorted
+// columns.
+DEV bool large_heap_order(const CellRec* R, const uint64_t* keys, int64_t n,
+                          uint64_t* perm) {
+  const int lane = LANE;
+  // the unsorted tail [m, n): its cells carry the kLargeUnsorted offset
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = lo + ((hi - lo) >> 1);
+    if ((uint32_t)(keys[mid] >> 32) >= kLargeUnsorted) hi = mid;
+    else lo = mid + 1;
+  }
+  const int64_t m = lo;
+  // stream u >= 1: the tail's u-th run of one column (rank)
+  int64_t head = lane == 0 ? 0 : -1, end = lane == 0 ? m : -1;
+  {
+    int64_t u = 1, a = m;
+    while (a < n) {
+      const int32_t col = R[(uint32_t)keys[a]].col;
+      int64_t e = a + 1;
+      while (e < n && R[(uint32_t)keys[e]].col == col) ++e;  // (lane-uniform)
+      if (u >= 64) return false;
+      if (lane == u) {
+        head = a;
+        end = e;
+      }
+      ++u;
+      a = e;
+    }
+  }
+  for (int64_t o = 0; o < n; ++o) {
+    uint64_t k = ~0ULL;
+    if (head >= 0 && head < end) {
+      const CellRec& x = R[(uint32_t)keys[head]];
+      k = ((uint64_t)(uint32_t)x.off << 32) | ((uint64_t)(uint32_t)x.col << 6) |
+          (uint64_t)lane;
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      const uint64_t y = __shfl_xor(k, d);
+      k = y < k ? y : k;
+    }
+    const int w = (int)(k & 63);
+    if (lane == w) {
+      const uint32_t idx = (uint32_t)keys[head];
+      perm[o] = ((uint64_t)(uint32_t)R[idx].off << 32) | idx;
+      ++head;
+    }
+  }
+  return true;
+}
+
 __global__ __launch_bounds__(64) void k_large_merge(
     RawDev D, int fix, LargeSlots LS, const int64_t* __restrict__ gen_base,
     const int64_t* __restrict__ gen_n, const CellRec* __restrict__ rec,
     const uint64_t* __restrict__ rkey, const int* __restrict__ bad_in,
-    uint8_t* __restrict__ stq, uint8_t* __restrict__ stv,
-    int64_t* __restrict__ out_q, int64_t* __restrict__ out_v,
-    unsigned long long* first_err) {
+    uint64_t* __restrict__ perm, uint8_t* __restrict__ stq,
+    uint8_t* __restrict__ stv, int64_t* __restrict__ out_q,
+    int64_t* __restrict__ out_v, unsigned long long* first_err) {
   const int lane = LANE;
   const int64_t sl = blockIdx.x;
   const int64_t r = LS.row[sl];
   const int64_t gb = gen_base[r], n = gen_n[r];
+  const uint64_t* order = rkey + gb;
   if (bad_in[sl]) {
-    if (lane == 0) {
-      row_error(first_err, r, RS_UNSUPPORTED);
-      out_q[r] = 0;
-      out_v[r] = 0;
+    if (!large_heap_order(rec + gb, rkey + gb, n, perm + gb)) {
+      if (lane == 0) {
+        row_error(first_err, r, RS_UNSUPPORTED);
+        out_q[r] = 0;
+        out_v[r] = 0;
+      }
+      return;
     }
-    return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    order = perm + gb;
   }
   int64_t nq = 0, nv = 0, nk = 0;
   int ms_in = 0, s_in = 0, bad = 0;
-  merge_sorted(D, fix, rec + gb, n, rkey + gb, stq + 4 * gb, stv + 9 * gb, nq,
+  merge_sorted(D, fix, rec + gb, n, order, stq + 4 * gb, stv + 9 * gb, nq,
                nv, nk, ms_in, s_in, bad);
   finish_row(r, bad, nq, nv, nk, ms_in, s_in, stv + 9 * gb, out_q, out_v,
              first_err);

@@ -410,18 +410,41 @@ def test_compaction_large_merged_columns(engine):
             _gpu_compact(engine, [(0, rows_fuzz.BASE, cols2)], fix=False)
 
 
-def test_compaction_large_row_out_of_order_is_unsupported(engine):
-    """A large row holding a compacted column whose offsets go back in time
-    (never written by the write path or compaction): UnsupportedOperation,
-    the caller keeps the reference's compaction for that row."""
+@pytest.mark.parametrize("fix", [True, False])
+def test_compaction_large_row_out_of_order(engine, fix):
+    """Large rows (past the LDS caps) holding compacted columns whose offsets
+    go back in time (never written by the write path or compaction): the
+    heap's pop order is replayed over the in-order columns' merged cells and
+    each unsorted column (CompactionQueue.java:549-584) — the bytes equal
+    the oracle's heap merge, or both raise."""
     rng = np.random.default_rng(7)
     offs = list(range(0, 20000, 2))
     offs[10], offs[11] = offs[11], offs[10]
     a = rows_fuzz.compacted([rows_fuzz.cell(rng, o, True) for o in offs])
     b = rows_fuzz.compacted([rows_fuzz.cell(rng, o + 1, True)
                              for o in range(0, 20000, 2)])
-    with pytest.raises(core.UnsupportedOperationException):
-        _gpu_compact(engine, [(0, rows_fuzz.BASE, [a + (0,), b + (1,)])])
+    # a second unsorted column (a stretch reversed, repeating offsets of a)
+    c_offs = list(range(500, 1500, 4))
+    c_offs[20:40] = c_offs[20:40][::-1]
+    c = rows_fuzz.compacted([rows_fuzz.cell(rng, o, True) for o in c_offs])
+    singles = [rows_fuzz.cell(rng, 1000 * k, False) for k in range(3, 9)]
+    rows = [(0, rows_fuzz.BASE, [a + (0,), b + (1,)]),
+            (1, rows_fuzz.BASE, [c + (5,), a + (3,)] +
+             [(q, v, 9) for q, v in singles]),
+            (2, rows_fuzz.BASE, [b + (0,)])]
+    for r in rows:
+        try:
+            ref = _oracle_rows([r], fix)
+            err = None
+        except pyoracle.OracleError as e:
+            err = e.status
+        if err is None:
+            assert _gpu_compact(engine, [r], fix) == ref
+        else:
+            with pytest.raises(STATUS_EXC[err]):
+                _gpu_compact(engine, [r], fix)
+    if fix:
+        assert _gpu_compact(engine, rows, fix) == _oracle_rows(rows, fix)
 
 
 def test_row_seq_kats(engine):
