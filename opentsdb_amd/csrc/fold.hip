@@ -139,28 +139,11 @@ struct FoldSink {
 // Waits until every member before this one has pushed all its contributions
 // to buckets < need.
 template <class A>
-DEV void fold_wait_spin(FoldSink<A>& F, int32_t need);
-#ifdef OTSDB_FLUSH_SPLIT
-template <class A>
-__device__ __attribute__((noinline)) void fold_wait_call(FoldSink<A>& F,
-                                                         int32_t need) {
-  fold_wait_spin(F, need);
-}
-#endif
-template <class A>
 DEV void fold_wait(FoldSink<A>& F, int32_t need) {
 #ifdef OTSDB_FOLD_NOWAIT  // debug build: no ordering
   return;
 #endif
   if (F.eff >= need) return;
-#ifdef OTSDB_FLUSH_SPLIT
-  fold_wait_call(F, need);
-#else
-  fold_wait_spin(F, need);
-#endif
-}
-template <class A>
-DEV void fold_wait_spin(FoldSink<A>& F, int32_t need) {
   const int lane = LANE;
   for (uint32_t spin = 0;; ++spin) {
     int32_t e = INT32_MAX;  // no unfinished predecessor
@@ -218,19 +201,6 @@ DEV void fold_fill_gap(const Params& P, FoldSink<A>& F, int32_t a, int32_t e,
 #else
 #define FLUSH_FN DEV
 #endif
-// one chunk of a flush with gaps (interpolation inside / before it)
-template <class A>
-DEV void fold_flush_gaps(const Params& P, FoldSink<A>& F, int32_t f,
-                         double v, bool inb, bool real, uint64_t rm);
-#ifdef OTSDB_FLUSH_SPLIT
-template <class A>
-__device__ __attribute__((noinline)) void fold_flush_gaps_call(
-    const Params& P, FoldSink<A>& F, int32_t f, double v, bool inb, bool real,
-    uint64_t rm) {
-  fold_flush_gaps(P, F, f, v, inb, real, rm);
-}
-#endif
-
 template <class A>
 FLUSH_FN void fold_flush(const Params& P, FoldSink<A>& F, int32_t limit) {
   if (limit <= F.flushed) return;
@@ -262,33 +232,6 @@ FLUSH_FN void fold_flush(const Params& P, FoldSink<A>& F, int32_t limit) {
     }
     const uint64_t rm = __ballot(real);
     if (!rm) continue;  // pending gap goes on (or absent before any real)
-#ifdef OTSDB_FLUSH_SPLIT
-    // every bucket of the chunk real and none pending before it (the common
-    // case): the values themselves; gaps take the out-of-line path
-    if (rm == __ballot(inb) && (F.pend < 0 || F.pend == f)) {
-      if (real) {
-        F.st[b - F.W0].push(v);
-        F.emit[b - F.W0] = 1;
-      }
-      const int lr = 63 - __builtin_clzll(rm);
-      F.x0 = bucket_ts(P, f + lr);
-      F.y0 = readlane_d(v, lr);
-      F.pend = f + lr + 1;
-    } else {
-      fold_flush_gaps_call(P, F, f, v, inb, real, rm);
-    }
-  }
-  F.flushed = limit;
-  fold_publish(F, (fill || F.pend < 0) ? limit : F.pend);
-}
-
-template <class A>
-DEV void fold_flush_gaps(const Params& P, FoldSink<A>& F, int32_t f,
-                         double v, bool inb, bool real, uint64_t rm) {
-  const int lane = LANE;
-  const int32_t b = f + lane;
-  {
-#endif
     const int fr = __builtin_ctzll(rm);
     const double vfr = readlane_d(v, fr);
     if (F.pend >= 0) fold_fill_gap(P, F, F.pend, f + fr, bucket_ts(P, f + fr), vfr);
@@ -311,10 +254,8 @@ DEV void fold_flush_gaps(const Params& P, FoldSink<A>& F, int32_t f,
     F.y0 = readlane_d(v, lr);
     F.pend = f + lr + 1;
   }
-#ifndef OTSDB_FLUSH_SPLIT
   F.flushed = limit;
   fold_publish(F, (fill || F.pend < 0) ? limit : F.pend);
-#endif
 }
 
 // wave-uniform copies (SGPRs): the member loop and the stream loop branch on

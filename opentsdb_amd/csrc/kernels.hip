@@ -439,64 +439,6 @@ DEV void rate_flush(const Params& P, RowSink& S, RateState& R, int64_t f,
     S.rv[i] = absent_value();
   }
   const bool p = inb && __double_as_longlong(v) != kAbsentBits;
-  {
-    // every bucket of the run present (the common case): each rate's
-    // previous point is the lane before it (lane 0: the carry), a DPP shift
-    // instead of the general path's lane shuffles; kept unless a counter
-    // reset is dropped (then the general path below)
-    const uint64_t inm = __ballot(inb);
-    if (__ballot(p) == inm) {
-      const double vp = dppd<0x138, 0xF>(v);  // wave_shr:1
-      const int64_t t = bucket_ts(P, b);
-      const int64_t tprev = lane == 0 ? R.carry_pts : bucket_ts(P, b - 1);
-      const double vprev = lane == 0 ? R.carry_pv : vp;
-      bool kept = false, bad = false;
-      double rate = 0.0;
-      if (inb) {
-        if (t <= tprev) bad = true;
-        const double dt = (double)(t - tprev) / 1000.0;
-        double diff = v - vprev;
-        if (P.counter && diff < 0) {
-          if (!P.drop_resets) {
-            kept = true;
-            diff = (double)P.counter_max - vprev + v;
-            const double r = diff / dt;
-            rate = (P.reset_value > 0 && r > (double)P.reset_value) ? 0.0 : r;
-          }
-        } else {
-          kept = true;
-          rate = diff / dt;
-        }
-      }
-      const uint64_t km = __ballot(kept);
-      if (km == inm) {
-        if (__ballot(bad)) R.bad = 1;
-        if (R.r0_idx < 0) {
-          R.r0_idx = f;
-          R.r0_val = readlane_d(rate, 0);
-        }
-        R.kept_count += __popcll(km);
-        if (R.kept_count > 2) R.kept_count = 2;
-        const int l = 63 - __builtin_clzll(km);
-        R.last_kept = f + l;
-        R.carry_pts = bucket_ts(P, f + l);
-        R.carry_pv = readlane_d(v, l);
-        if (inb) {
-          const uint8_t st = b != R.r0_idx ? ST_REAL : ST_INTERP;
-          if (S.nt) {
-            __builtin_nontemporal_store(rate, &S.rowv[b]);
-            __builtin_nontemporal_store(st, &S.rows[b]);
-          } else {
-            S.rowv[b] = rate;
-            S.rows[b] = st;
-          }
-        }
-        R.carry_k = f + l;
-        R.carry_kv = readlane_d(rate, l);
-        return;
-      }
-    }
-  }
   const int64_t t = inb ? bucket_ts(P, b) : 0;
   const uint64_t pm = __ballot(p);
   const uint64_t below = pm & ((1ULL << lane) - 1);
