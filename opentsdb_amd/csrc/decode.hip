@@ -1041,6 +1041,168 @@ __global__ void k_series_offsets(int64_t R, int64_t S,
   const int64_t cur = r == R ? S : row_series[r];
   for (int64_t s = prev + 1; s <= cur && s <= S; ++s) offsets[s] = row_out[r];
 }
+
+// ------------------------------------------------------------------------
+// k_requal: columns whose qualifier widths mix (MS_MIXED_COMPACT rows, or
+// second rows and millisecond rows in one series) rewritten with one width,
+// so the cells fold streams them: every qualifier becomes the 4-byte
+// millisecond qualifier of the same point (Internal.buildQualifier,
+// Internal.java:848-863: 0xF << 28 | offset_ms << 6 | flags; a 2-byte
+// qualifier's offset_s * 1000 < 2^22), the value pool stays as it is (same
+// points, same value bytes, same meta byte).  One wavefront per row, 16
+// two-byte units per lane (1,024 a pass: a 360-point row in one); MODE 0
+// counts the row's points, MODE 1 writes its qualifiers at 4 * row_out[r]
+// (qoff_out[r]), compacted through LDS into coalesced stores.
+//
+// Qualifier starts without a scan.  start(u+1) = !(start(u) && ms(u)): a
+// unit that does not look like a millisecond qualifier's first (high nibble
+// 0xF) makes the next unit a start, so inside a run of ms-looking units that
+// begins on a start, starts and non-starts alternate; with the run's first
+// unit at position a, the non-starts are a+1, a+3, ... (up to the unit just
+// past the run).  Runs are labelled by the parity of a with one add (the
+// carry of `m + even run starts` clears exactly the runs that begin on even
+// positions).  Across a lane whose units all look like ms ones the start
+// state flips 16 times (returns unchanged), so a lane's entry state is the
+// exit state of the nearest lane below holding a non-ms unit (one ballot),
+// or the pass's carry; the lane's starts for entry state 1 and 0 differ
+// exactly on its units up to and including its first non-ms unit.  (Holding
+// one unit per lane instead — ms-looking units as a 64-bit wave mask, the
+// same logic on scalar registers — measured 2.5x slower for the count: a
+// dependent chain of ~20 scalar ops per 64 units.)
+DEV void requal_lane(uint32_t m, int nu, uint32_t& S1, uint32_t& flip, int& d,
+                     int& fixed_out) {
+  const uint32_t vm = nu >= 16 ? 0xFFFFu : ((1u << nu) - 1);
+  const uint32_t edges = m & ~(m << 1);             // run starts
+  const uint32_t x = m + (edges & 0x55555555u);      // even-start runs carry out
+  const uint32_t ns = (((m & ~x) << 1) & 0xAAAAAAAAu) | (((m & x) << 1) & 0x55555555u);
+  S1 = ~ns & vm;
+  const uint32_t nz = ~m & vm;
+  d = nz != 0;
+  fixed_out = !((ns >> nu) & 1u);
+  flip = d ? ((2u << __builtin_ctz(nz)) - 1) : vm;
+}
+
+// The lane's 32 bytes at a (units past the row are masked off later) and,
+// for a 4-byte qualifier at its last unit, the 4 after them.
+template <int MODE>
+DEV void requal_words(const CellsDev& C, int64_t a, int64_t pool_end,
+                      uint32_t* w) {
+#pragma unroll
+  for (int k = 0; k < 9; ++k) w[k] = 0;
+  if (a + 36 <= pool_end) {
+    const uint4 x0 = *reinterpret_cast<const uint4*>(C.qual + a);
+    const uint4 x1 = *reinterpret_cast<const uint4*>(C.qual + a + 16);
+    w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w;
+    w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
+    if (MODE == 1) w[8] = *reinterpret_cast<const uint32_t*>(C.qual + a + 32);
+  } else if (a < pool_end) {  // the pool's last bytes
+#pragma unroll
+    for (int i = 0; i < 36; ++i)
+      if (a + i < pool_end) w[i >> 2] |= (uint32_t)C.qual[a + i] << (8 * (i & 3));
+  }
+}
+
+// rows per wavefront: the next row's first pass is loaded while this one
+// is processed (rows are contiguous in the pool: it starts where this ends)
+#ifndef OTSDB_RQ_RPW
+#define OTSDB_RQ_RPW 8
+#endif
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_requal(
+    CellsDev C, int64_t* __restrict__ row_count,
+    const int64_t* __restrict__ row_out, int64_t* __restrict__ qoff_out,
+    uint8_t* __restrict__ qual_out, int* err_word) {
+  constexpr int RPW = OTSDB_RQ_RPW;
+  __shared__ uint32_t lds[MODE ? 4 : 1][MODE ? 1024 + 64 : 1];
+  const int lane = LANE, wv = threadIdx.x >> 6;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wv) * RPW;
+  if (r0 >= C.R) return;
+  if (MODE == 1 && r0 == 0 && lane == 0) qoff_out[C.R] = 4 * row_out[C.R];
+  const int64_t pool_end = C.qual_off[C.R];
+  // the wave's row offsets (and output offsets), one per lane
+  const int64_t off_l = (lane <= RPW && r0 + lane <= C.R) ? C.qual_off[r0 + lane] : 0;
+  const int64_t out_l = (MODE == 1 && lane < RPW && r0 + lane < C.R) ? row_out[r0 + lane] : 0;
+  const uint64_t below_me = (1ULL << lane) - 1;
+  int bad = 0;
+  uint32_t wn[9];
+  requal_words<MODE>(C, readlane_l(off_l, 0) + 32 * lane, pool_end, wn);
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const int64_t r = r0 + k;
+    if (r >= C.R) break;
+    const int64_t qa = readlane_l(off_l, k), qe = readlane_l(off_l, k + 1);
+    uint32_t w[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) w[i] = wn[i];
+    if (k + 1 < RPW && r + 1 < C.R) requal_words<MODE>(C, qe + 32 * lane, pool_end, wn);
+    const int64_t qlen = qe - qa;
+    const int64_t out0 = MODE ? readlane_l(out_l, k) : 0;
+    if (MODE == 1 && lane == 0) qoff_out[r] = 4 * out0;
+    if (qlen & 1) {  // not a data-point column (Internal.java:262-264)
+      if (MODE == 0 && lane == 0) row_count[r] = 0;
+      continue;
+    }
+    const int64_t units = qlen >> 1;
+    int cs = 1;
+    int64_t n_acc = 0;  // MODE 0: the lane's points; MODE 1: the row's so far
+    for (int64_t u0 = 0; u0 < units; u0 += 1024) {
+      if (u0 > 0) requal_words<MODE>(C, qa + 2 * u0 + 32 * lane, pool_end, w);
+      const int64_t ub = u0 + 16 * lane;
+      const int nu = ub >= units ? 0 : (int)(units - ub < 16 ? units - ub : 16);
+      uint32_t m = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        m |= (uint32_t)((w[i] & 0xF0u) == 0xF0u) << (2 * i);
+        m |= (uint32_t)((w[i] & 0xF00000u) == 0xF00000u) << (2 * i + 1);
+      }
+      m &= nu >= 16 ? 0xFFFFu : ((1u << nu) - 1);
+      uint32_t S1, flip;
+      int d, fixed_out;
+      requal_lane(m, nu, S1, flip, d, fixed_out);
+      const uint64_t below = __ballot(d) & below_me;
+      const int fo_src = __shfl(fixed_out, below ? 63 - __builtin_clzll(below) : 0);
+      const int cin = below ? fo_src : cs;
+      const uint32_t S = cin ? S1 : (S1 ^ flip);
+      // a 4-byte qualifier cut by the column end
+      if (nu > 0 && ub + nu == units) bad |= (int)(((S & m) >> (nu - 1)) & 1u);
+      cs = __shfl(d ? fixed_out : cin, 63);
+      const int np = __builtin_popcount(S);
+      if (MODE == 0) {
+        n_acc += np;
+        continue;
+      }
+      int tot;
+      const int k0 = wave_excl_scan(np, tot);
+      // branch free: every unit's 4-byte form goes to LDS, a non-start's to
+      // the lane's scratch slot
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        // the unit's 4 bytes B0 B1 B2 B3 as stored (little-endian word)
+        const uint32_t u = (i & 1) ? __builtin_amdgcn_alignbyte(w[(i >> 1) + 1], w[i >> 1], 2)
+                                   : w[i >> 1];
+        const uint32_t q2 = __builtin_amdgcn_perm(0u, u, 0x0c0c0001u);  // B0 B1
+        const uint32_t ms4 = 0xF0000000u | ((q2 >> 4) * 64000u) | (q2 & 0xFu);
+        // a 4-byte qualifier is kept byte for byte
+        const uint32_t o = ((m >> i) & 1u) ? u : __builtin_amdgcn_perm(0u, ms4, 0x00010203u);
+        const int slot = ((S >> i) & 1u) ? k0 + __builtin_popcount(S & ((1u << i) - 1))
+                                         : 1024 + lane;
+        lds[MODE ? wv : 0][slot] = o;
+      }
+      wave_lds_fence();
+      uint32_t* dst = reinterpret_cast<uint32_t*>(qual_out) + out0 + n_acc;
+      for (int j = lane; j < tot; j += 64) dst[j] = lds[MODE ? wv : 0][j];
+      n_acc += tot;
+      wave_lds_fence();
+    }
+    if (MODE == 0) {
+      int tot;
+      wave_excl_scan((int)n_acc, tot);
+      if (lane == 0) row_count[r] = tot;
+    }
+  }
+  if (__ballot(bad) && lane == 0) atomicOr(err_word, ERR_CORRUPT_CELL);
+}
 #endif  // OTSDB_DS_TU
 
 }  // namespace otsdb

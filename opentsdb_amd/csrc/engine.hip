@@ -1635,6 +1635,59 @@ otsdb_status decode_impl(otsdb_ctx* c, const otsdb_cells* cells,
   return write_pass();
 }
 
+// Columns of mixed qualifier widths rewritten with one (k_requal, decode.hip)
+// into the context's cells_col buffer: *out views the rewritten qualifier
+// pool with the original rows and value pool.  A count pass, a scan of the
+// row counts, a write pass.
+otsdb_status requal_impl(otsdb_ctx* c, const CellsDev& C, CellsDev* out,
+                         hipStream_t st) {
+  const int64_t R = C.R;
+  size_t scan_tmp = 0;
+  HIP_TRY(rocprim::exclusive_scan(nullptr, scan_tmp, (const int64_t*)nullptr,
+                                  (int64_t*)nullptr, (int64_t)0,
+                                  (size_t)(R + 1), rocprim::plus<int64_t>(),
+                                  st));
+  otsdb_status rc = ensure(&c->dec_ws, &c->dec_ws_cap,
+                           (size_t)(2 * R + 2) * 8 + 128 + scan_tmp);
+  if (rc) return rc;
+  int64_t* row_count = (int64_t*)c->dec_ws;
+  int64_t* row_out = row_count + (R + 1);
+  void* tmp = (void*)(((uintptr_t)(row_out + R + 1) + 63) & ~(uintptr_t)63);
+  HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), st));
+  HIP_TRY(hipMemsetAsync(row_count + R, 0, 8, st));
+  if (R > 0)
+    hipLaunchKernelGGL(k_requal<0>, dim3(blocks_for(R, 4 * OTSDB_RQ_RPW)), dim3(256), 0, st,
+                       C, row_count, (const int64_t*)nullptr, (int64_t*)nullptr,
+                       (uint8_t*)nullptr, c->d_err);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(rocprim::exclusive_scan(tmp, scan_tmp, (const int64_t*)row_count,
+                                  row_out, (int64_t)0, (size_t)(R + 1),
+                                  rocprim::plus<int64_t>(), st));
+  HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
+                         hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(&c->h_small[1], row_out + R, 8, hipMemcpyDeviceToHost,
+                         st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (c->h_small[0] & ERR_CORRUPT_CELL)
+    return fail(OTSDB_E_ILLEGAL_DATA,
+                "Corrupted value: couldn't break down into individual values");
+  const int64_t N = c->h_small[1];
+  const size_t qo = ((size_t)(R + 1) * 8 + 255) & ~(size_t)255;
+  rc = ensure(&c->cells_col, &c->cells_col_cap, qo + 4 * (size_t)N + 64);
+  if (rc) return rc;
+  int64_t* qoff = (int64_t*)c->cells_col;
+  uint8_t* qual = (uint8_t*)c->cells_col + qo;
+  if (R > 0)
+    hipLaunchKernelGGL(k_requal<1>, dim3(blocks_for(R, 4 * OTSDB_RQ_RPW)), dim3(256), 0, st,
+                       C, row_count, (const int64_t*)row_out, qoff, qual,
+                       c->d_err);
+  else
+    HIP_TRY(hipMemsetAsync(qoff, 0, 8, st));
+  HIP_TRY(hipGetLastError());
+  *out = CellsDev{R, C.row_series, C.row_base_s, qoff, qual, C.val_off, C.val};
+  return OTSDB_OK;
+}
+
 // Query straight from compacted columns: the fused decode + downsample when
 // the query and the columns allow it, else decode -> columnar -> pipeline.
 otsdb_status run_cells_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
@@ -1662,28 +1715,38 @@ otsdb_status run_cells_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
     hipLaunchKernelGGL(k_series_rows, dim3(blocks_for(R + 1, 256)), dim3(256),
                        0, st, R, S, cells->row_series, series_row);
     BatchDev B{S, nullptr, nullptr, nullptr, nullptr, nullptr};
-    Work W;
     P.check_order = c->verbatim ? 1 : 0;
-    rc = run_pipeline(c, spec, B, b->group_members, goff, P, W, 0, nullptr,
-                      nullptr, &C, series_row);
-    if (rc) return rc;
-    // a column the fused path does not take (ERR_CELLS_GENERIC): re-run
-    // through the decode below
-    HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
-                           hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    const int e = (int)(c->h_small[0] & 0xFFFFFFFF);
-    if (c->verbatim && (e & (ERR_CORRUPT_CELL | ERR_CELLS_GENERIC |
-                             ERR_NOT_SORTED | ERR_SPEC_MISS)))
-      return spec_miss(c);
-    if (e & ERR_CORRUPT_CELL)
-      return fail(OTSDB_E_ILLEGAL_DATA,
-                  "Corrupted value: couldn't break down into individual values");
-    if (!(e & ERR_CELLS_GENERIC)) {
-      const int64_t G = (int64_t)goff.size() - 1;
-      rc = compact(c, P, G, W.out_val, W.out_emit, W.counts, out);
+    // a column the fused path does not take (ERR_CELLS_GENERIC) — widths
+    // mixed inside a row or across a series' rows — is rewritten with
+    // 4-byte qualifiers (k_requal) and the fused path runs again; what it
+    // still does not take re-runs through the decode below
+    CellsDev CQ = C;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      Work W;
+      rc = run_pipeline(c, spec, B, b->group_members, goff, P, W, 0, nullptr,
+                        nullptr, &CQ, series_row);
       if (rc) return rc;
-      return finish(c, G, out);
+      HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
+                             hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      const int e = (int)(c->h_small[0] & 0xFFFFFFFF);
+      if (c->verbatim && (e & (ERR_CORRUPT_CELL | ERR_CELLS_GENERIC |
+                               ERR_NOT_SORTED | ERR_SPEC_MISS)))
+        return spec_miss(c);
+      if (e & ERR_CORRUPT_CELL)
+        return fail(OTSDB_E_ILLEGAL_DATA,
+                    "Corrupted value: couldn't break down into individual values");
+      if (!(e & ERR_CELLS_GENERIC)) {
+        const int64_t G = (int64_t)goff.size() - 1;
+        rc = compact(c, P, G, W.out_val, W.out_emit, W.counts, out);
+        if (rc) return rc;
+        return finish(c, G, out);
+      }
+      if (attempt == 0) {
+        std::unique_ptr<StageTimer> rq_tm(new StageTimer(c, 7));
+        rc = requal_impl(c, C, &CQ, st);
+        if (rc) return rc;
+      }
     }
   }
   // (verbatim storage rows take only the cells fold)

@@ -232,6 +232,20 @@ FLUSH_FN void fold_flush(const Params& P, FoldSink<A>& F, int32_t limit) {
     }
     const uint64_t rm = __ballot(real);
     if (!rm) continue;  // pending gap goes on (or absent before any real)
+    if (rm == __ballot(inb)) {
+      // every bucket of the run is real (dense series): no gap inside it
+      if (F.pend >= 0 && F.pend < f)
+        fold_fill_gap(P, F, F.pend, f, bucket_ts(P, f), readlane_d(v, 0));
+      if (inb) {
+        F.st[b - F.W0].push(v);
+        F.emit[b - F.W0] = 1;
+      }
+      const int lr = 63 - __builtin_clzll(rm);
+      F.x0 = bucket_ts(P, f + lr);
+      F.y0 = readlane_d(v, lr);
+      F.pend = f + lr + 1;
+      continue;
+    }
     const int fr = __builtin_ctzll(rm);
     const double vfr = readlane_d(v, fr);
     if (F.pend >= 0) fold_fill_gap(P, F, F.pend, f + fr, bucket_ts(P, f + fr), vfr);
@@ -537,7 +551,11 @@ __global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
       kc.out_val = out_val;
       kc.out_emit = out_emit;
       kc.fin = tile_single[t] && !always_partial;
-      s_next = 0;
+      // a cells fold whose prep already sent the batch to the generic path
+      // (mixed qualifier widths: the engine rewrites them and runs again)
+      s_next = (CELLS && (__hip_atomic_load(err_word, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT) &
+                          ERR_CELLS_GENERIC)) ? -1 : 0;
     }
   }
   const int nw = W1 - W0;
@@ -548,6 +566,7 @@ __global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
   prog[tid] = 0;
   for (int i = lane; i < FOLD_WIN; i += 64) ring[w][i] = absent_value();
   __syncthreads();
+  if (CELLS && s_next < 0) return;  // (block-uniform)
   int dbg_n = 0;
   FoldSink<A> F{st, emit, ring[w], prog, err_word, 0, 0, W0, W1, W0, -1, 0, 0.0};
   for (;;) {

@@ -829,7 +829,20 @@ DEV void reduce_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
   int pkey, next_head;
   M pst;
   if (DPP) {
-    seg_scan_dpp(key, st);
+    // A tail run spans its own lane and the following lanes that hold no
+    // bucket boundary (nseg <= 1), so the scan needs only the row steps
+    // reaching the longest such stretch (the row broadcasts carry it across
+    // rows): 1 m buckets of 10 s points (a boundary in every lane) skip it
+    int L = 0;
+    for (uint64_t y = __ballot(nseg <= 1); y; y &= y << 1) ++L;
+    if (L > 0) {
+      seg_step_dpp<0x111, 0xF>(key, st);               // row_shr:1
+      if (L > 1) seg_step_dpp<0x112, 0xF>(key, st);    // row_shr:2
+      if (L > 3) seg_step_dpp<0x114, 0xF>(key, st);    // row_shr:4
+      if (L > 7) seg_step_dpp<0x118, 0xF>(key, st);    // row_shr:8
+      seg_step_dpp<0x142, 0xA>(key, st);  // row_bcast:15 -> rows 1, 3
+      seg_step_dpp<0x143, 0xC>(key, st);  // row_bcast:31 -> rows 2, 3
+    }
     pkey = dpp32<0x138, 0xF>(INT32_MIN, key);  // wave_shr:1
     pst = st;
     pst.template dpp<0x138, 0xF>();

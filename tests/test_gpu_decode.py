@@ -432,3 +432,109 @@ def test_fused_cells_ragged_rows(engine, kind, agg, ds, window):
     fl = cancel_floor(hb, 400) if kind == "int" else 0.0  # mixed signs
     compare(got, ref, exact, where="ragged/%s/%s/%s" % (kind, agg, ds),
             floor=fl)
+
+
+@pytest.mark.parametrize("layout", ["in-row", "by-row", "sparse"])
+@pytest.mark.parametrize("agg,ds,rate,days", [
+    ("sum", "1m-avg", False, 0), ("dev", "5m-dev", False, 0),
+    ("max", "1m-max-nan", False, 0), ("sum", "5m-sum", True, 0),
+    ("zimsum", "7m-count", False, 0), ("avg", "1m-avg-zero", False, 2)])
+def test_fused_cells_mixed_widths(engine, layout, agg, ds, rate, days):
+    """Columns mixing 2-byte second and 4-byte millisecond qualifiers
+    (MS_MIXED_COMPACT inside rows, RowSeq.java:338-356), or series whose
+    rows alternate between the two widths, or sparse rows of both: k_requal
+    rewrites them with 4-byte qualifiers and the cells fold streams them
+    (one window and, over two days of 1 m buckets, several) — against the
+    oracle on the points RowSeq decodes from the original columns."""
+    import torch
+    from opentsdb_amd import workload
+    from opentsdb_amd.batch import HostBatch
+    from opentsdb_amd.engine import DeviceResult
+    from tests.test_gpu_parity import compare, cancel_floor
+    rng = np.random.default_rng(23 + days)
+    span = (days or 4) * (86400000 if days else 3600000)
+    if layout == "sparse":
+        b = _ragged_rows_batch(9, 36, span // 3600000, "int")
+        b.ts = b.ts + rng.integers(0, 999, len(b.ts)) * (rng.random(len(b.ts)) < 0.5)
+    else:
+        b = datasets.random_batch(41 + days, n_series=30, n_groups=3,
+                                  span_ms=span, value_kind="int", counter=rate,
+                                  cadence_ms=20000 if days else 7000)
+        b.ts = b.ts - b.ts % 1000
+        ms = rng.integers(1, 999, len(b.ts))
+        if layout == "in-row":  # about half the points on milliseconds
+            b.ts = b.ts + ms * (rng.random(len(b.ts)) < 0.5)
+        else:  # odd hours on milliseconds, even hours on whole seconds
+            b.ts = b.ts + ms * (((b.ts - datasets.T0) // 3600000) % 2)
+    for s in range(b.n_series):
+        a, z = b.offsets[s], b.offsets[s + 1]
+        b.ts[a:z] = np.sort(b.ts[a:z])
+        assert (np.diff(b.ts[a:z]) > 0).all()
+    b.is_float = np.zeros(len(b.ts), np.uint8)
+    enc = cells.encode_batch(b)
+    widths = set()
+    for r in range(len(enc["row_series"])):
+        q = enc["qual"][enc["qual_off"][r]:enc["qual_off"][r + 1]]
+        if len(q):
+            widths.add(4 if q[0] >> 4 == 0xF else 2)
+    assert widths == {2, 4}
+    ts, bits, isint = [], [], []
+    for r in range(len(enc["row_series"])):
+        q = enc["qual"][enc["qual_off"][r]:enc["qual_off"][r + 1]]
+        v = enc["val"][enc["val_off"][r]:enc["val_off"][r + 1]]
+        p = pyoracle.decode_row(q.tobytes(), v.tobytes(), enc["row_base_s"][r])
+        ts.append(p["ts"])
+        bits.append(p["bits"])
+        isint.append(p["is_int"])
+    rts = np.concatenate(ts).astype(np.int64)
+    assert np.array_equal(rts, b.ts)
+    hb = HostBatch(b.offsets, rts, np.concatenate(bits).astype(np.int64),
+                   (np.concatenate(isint) == 0).astype(np.uint8), None,
+                   b.group_offsets, b.group_members)
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda()
+         for k, v in enc.items()}
+    dc = workload.DeviceCells(d, b.n_series)
+    db = _device_batch(hb, "int")
+    t0, t1 = datasets.T0 + 600000, datasets.T0 + span - 300000
+    ro = core.RateOptions(True, core.LONG_MAX, 0) if rate else None
+    spec = core.make_spec(t0, t1, core.Aggregators.get(agg),
+                          core.DownsamplingSpecification(ds), t0, t1, rate, ro)
+    ref = pyoracle.group_by(spec, hb)
+    res = DeviceResult(torch, db.n_groups, 4 * len(hb.ts) + 64, "cuda")
+    workload.run_cells_device(engine, spec, dc, db, res)
+    got = _result_points(res, db.n_groups)
+    exact = ds.split("-")[1] in ("max", "count", "dev") and agg in (
+        "max", "zimsum", "dev")
+    fl = 0.0 if rate else cancel_floor(hb, 400)
+    compare(got, ref, exact, floor=fl,
+            where="mixedw/%s/%s/%s" % (layout, agg, ds))
+
+
+def test_fused_cells_mixed_cut_qualifier(engine):
+    """A mixed-width column whose last qualifier is a 4-byte one cut after
+    two bytes: IllegalDataException, as RowSeq's walk."""
+    import torch
+    from opentsdb_amd import workload
+    from opentsdb_amd.engine import DeviceResult
+    b = datasets.random_batch(43, n_series=4, n_groups=1, span_ms=3600000,
+                              value_kind="int", cadence_ms=7000)
+    b.ts = b.ts - b.ts % 1000
+    b.ts[1::2] += 500  # every other point on milliseconds
+    b.is_float = np.zeros(len(b.ts), np.uint8)
+    enc = cells.encode_batch(b)
+    # row 0: append the first half of a 4-byte qualifier
+    qo, q = enc["qual_off"].copy(), enc["qual"]
+    z = int(qo[1])
+    enc["qual"] = np.concatenate([q[:z], np.array([0xF0, 0x00], np.uint8), q[z:]])
+    qo[1:] += 2
+    enc["qual_off"] = qo
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda()
+         for k, v in enc.items()}
+    dc = workload.DeviceCells(d, b.n_series)
+    db = _device_batch(b, "int")
+    spec = core.make_spec(datasets.T0, datasets.T0 + 3600000,
+                          core.Aggregators.SUM,
+                          core.DownsamplingSpecification("1m-avg"))
+    res = DeviceResult(torch, db.n_groups, 4096, "cuda")
+    with pytest.raises(core.IllegalDataException):
+        workload.run_cells_device(engine, spec, dc, db, res)
