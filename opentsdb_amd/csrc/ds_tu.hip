@@ -16,6 +16,32 @@
 #ifndef OTSDB_DS_PART
 #define OTSDB_DS_PART 0  // 0: launch_ds kernels, 1: the cells fold
 #endif
+// k_bucketize_k ring shape (tuning builds override)
+#ifndef OTSDB_RING_WAVES
+#define OTSDB_RING_WAVES 1
+#endif
+#ifndef OTSDB_RING_WIN
+#define OTSDB_RING_WIN 256
+#endif
+#ifndef OTSDB_RING_FL
+#define OTSDB_RING_FL 64
+#endif
+// rate-fused k_bucketize_k shape (tuning builds override)
+#ifndef OTSDB_RATE_K
+#define OTSDB_RATE_K 8
+#endif
+#ifndef OTSDB_RATE_WAVES
+#define OTSDB_RATE_WAVES 4
+#endif
+#ifndef OTSDB_RATE_WIN
+#define OTSDB_RATE_WIN 1024
+#endif
+#ifndef OTSDB_RATE_FL
+#define OTSDB_RATE_FL 512
+#endif
+#ifndef OTSDB_RATE_PF
+#define OTSDB_RATE_PF 0
+#endif
 #include "kernels.hip"
 #include "decode.hip"
 #include "fold.hip"
@@ -79,14 +105,17 @@ bool launch_ds(DsKernel k, const DsLaunch& a) {
       OTSDB_DBG(a.st, "k_prep");
       return true;
     case DS_RING:  // production: LDS ring sink, sentinel rows, DPP scan
-      hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, OTSDB_RING_NT, 1, 0, 1, 256>),
+      hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, OTSDB_RING_NT, OTSDB_RING_WAVES, 0, 1,
+                                        OTSDB_RING_WIN, OTSDB_RING_FL>),
                          dim3(ds_blocks(S, 4)), dim3(256), 0, a.st, a.P, a.B,
                          a.SM, a.R);
       return true;
     case DS_RATE:
       // launch-bounded to 128 VGPRs (4 waves / SIMD instead of the 3 its 140
       // VGPRs allow; 8 cold spills): C4 bucketize 14.1 -> 13.3 ms
-      hipLaunchKernelGGL((k_bucketize_k<M, 8, 0, OTSDB_RING_NT, 4, 0, 1, 1024, 512, 1>),
+      hipLaunchKernelGGL((k_bucketize_k<M, OTSDB_RATE_K, OTSDB_RATE_PF, OTSDB_RING_NT,
+                                        OTSDB_RATE_WAVES, 0, 1, OTSDB_RATE_WIN,
+                                        OTSDB_RATE_FL, 1>),
                          dim3(ds_blocks(S, 4)), dim3(256), 0, a.st, a.P, a.B,
                          a.SM, a.R);
       return true;

@@ -1742,7 +1742,9 @@ __global__ __launch_bounds__(SEL_THREADS) void k_group_select(
 
 // ------------------------------------------------------------------------
 // k_compact: dense (group, bucket) results -> per-group (ts, value) arrays.
-// One wavefront per group.  mode 0 counts, mode 1 scatters.
+// One wavefront per group.  mode 0 counts (16 emit flags a lane per load:
+// 1,024 buckets a pass), mode 1 scatters (4 runs of 64 buckets a pass, their
+// loads issued together: the loop is latency-bound, not byte-bound).
 // ------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_compact(
     Params P, int64_t G, const double* __restrict__ out_val,
@@ -1753,22 +1755,53 @@ __global__ __launch_bounds__(256) void k_compact(
   const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (g >= G) return;
   const int64_t nb = P.nb;
-  int64_t pos = mode ? offsets[g] : 0;
-  for (int64_t c0 = 0; c0 < nb; c0 += 64) {
-    const int64_t b = c0 + lane;
-    const bool e = b < nb && out_emit[g * nb + b];
-    const uint64_t m = __ballot(e);
-    if (mode && e) {
-      const int64_t p = pos + __popcll(m & ((1ULL << lane) - 1));
-      if (p < cap) {
-        r_ts[p] = bucket_ts(P, b);
-        r_val[p] = __double_as_longlong(out_val[g * nb + b]);
-        r_isint[p] = 0;
+  const uint8_t* em = out_emit + g * nb;
+  if (!mode) {
+    int64_t n = 0;
+    for (int64_t c0 = 0; c0 < nb; c0 += 1024) {
+      const int64_t b = c0 + 16 * lane;
+      if (b + 16 <= nb) {
+        const uint4 x = *reinterpret_cast<const uint4*>(em + b);
+        // non-zero bytes: the high bit of ((byte & 0x7F) + 0x7F) | byte
+        auto nz = [](uint32_t w) {
+          return __builtin_popcount((((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u);
+        };
+        n += nz(x.x) + nz(x.y) + nz(x.z) + nz(x.w);
+      } else {
+        for (int64_t i = b; i < nb && i < b + 16; ++i) n += em[i] ? 1 : 0;
       }
     }
-    pos += __popcll(m);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) n += __shfl_xor(n, d);
+    if (lane == 0) counts[g] = n;
+    return;
   }
-  if (!mode && lane == 0) counts[g] = pos;
+  constexpr int U = 4;
+  int64_t pos = offsets[g];
+  for (int64_t c0 = 0; c0 < nb; c0 += 64 * U) {
+    bool e[U];
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t b = c0 + 64 * u + lane;
+      e[u] = b < nb && em[b];
+      v[u] = b < nb ? out_val[g * nb + b] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t b = c0 + 64 * u + lane;
+      const uint64_t m = __ballot(e[u]);
+      if (e[u]) {
+        const int64_t p = pos + __popcll(m & ((1ULL << lane) - 1));
+        if (p < cap) {
+          r_ts[p] = bucket_ts(P, b);
+          r_val[p] = __double_as_longlong(v[u]);
+          r_isint[p] = 0;
+        }
+      }
+      pos += __popcll(m);
+    }
+  }
 }
 
 // exclusive scan of counts[G] -> offsets[G+1] (single workgroup; G is the

@@ -41,7 +41,8 @@ def main(tag):
             done.append(dst)
     for name, src in (("pmc_C2.json", "pmc_C2/summary.json"),
                       ("pmc_C4.json", "pmc_C4/summary.json"),
-                      ("pmc_cells_C2.json", "pmc_cells/summary.json")):
+                      ("pmc_cells_C2.json", "pmc_cells/summary.json"),
+                      ("pmc_C2_named.json", "pmc_C2_named/summary.json")):
         p = os.path.join(OUT, src)
         if os.path.exists(p):
             shutil.copy(p, os.path.join(PROF, name))

@@ -14,6 +14,7 @@ if [ "${PART:-bench}" = pmc ]; then
   PMC_CFG=C2 PMC_PASSES="sq fetch write" bash scripts/gpu_pmc.sh > gpurun_out/pmc_c2.log 2>&1 || { tail -5 gpurun_out/pmc_c2.log; exit 1; }
   PMC_CFG=C4 PMC_PASSES="sq fetch write" bash scripts/gpu_pmc.sh > gpurun_out/pmc_c4.log 2>&1 || { tail -5 gpurun_out/pmc_c4.log; exit 1; }
   bash scripts/gpu_pmc_cells.sh > gpurun_out/pmc_cells.log 2>&1 || { tail -5 gpurun_out/pmc_cells.log; exit 1; }
+  PMC_CFG=C2 PMC_TAG=_named PMC_BENCH_ARGS=--named-query PMC_PASSES="sq fetch write lds" bash scripts/gpu_pmc.sh > gpurun_out/pmc_named.log 2>&1 || { tail -5 gpurun_out/pmc_named.log; exit 1; }
   echo "pmc ok"
   exit 0
 fi
