@@ -147,10 +147,18 @@ def named_spec(config):
 
 def pmc_traffic(name):
     """HBM bytes per launch of the dominant kernel measured by
-    scripts/gpu_pmc.sh for this workload (profiles/pmc_<name>.json)."""
-    pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % name)
-    if not os.path.exists(pmc):
+    scripts/gpu_pmc.sh for this workload (the latest round's
+    profiles/r<N>_pmc_<name>.json)."""
+    import glob
+    import re
+    found = []
+    for p in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_%s.json" % name)):
+        m = re.match(r"r(\d+)_pmc_", os.path.basename(p))
+        if m:
+            found.append((int(m.group(1)), p))
+    if not found:
         return None
+    pmc = max(found)[1]
     with open(pmc) as f:
         d = json.load(f)
     return d.get("hbm_bytes_per_launch",

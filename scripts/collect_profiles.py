@@ -45,7 +45,7 @@ def main(tag):
                       ("pmc_C2_named.json", "pmc_C2_named/summary.json")):
         p = os.path.join(OUT, src)
         if os.path.exists(p):
-            shutil.copy(p, os.path.join(PROF, name))
+            shutil.copy(p, os.path.join(PROF, "%s_%s" % (tag, name)))
             done.append(name)
     for what in ("rows", "mixed"):
         ks = first("ks_%s/**/*kernel_stats.csv" % what)
