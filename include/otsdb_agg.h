@@ -56,7 +56,10 @@ typedef enum {
   OTSDB_E_UNSUPPORTED = 5,
   /* HIP runtime failure / out of device memory.                            */
   OTSDB_E_DEVICE = 6,
-  /* Caller-provided output capacity too small (otsdb_result.capacity).      */
+  /* Caller-provided output capacity too small (otsdb_result.capacity).  The
+   * host entries (otsdb_agg_run, otsdb_agg_run_cells, otsdb_agg_run_raw)
+   * still fill result.offsets with the whole result's offsets, so
+   * offsets[n_groups] is the capacity a retry needs; nothing else written. */
   OTSDB_E_CAPACITY = 7
 } otsdb_status;
 

@@ -274,7 +274,8 @@ public final class GpuAggregation {
           row_base, qual_off, qual, val_off, val, group_offsets,
           group_members, out_offsets, out_ts, out_val, out_is_int);
       if (st == CAPACITY) {
-        cap *= 2;
+        // the offsets carry the whole result's size (include/otsdb_agg.h)
+        cap = Math.max(cap + 1, out_offsets[groups.length]);
         continue;
       }
       if (st == UNSUPPORTED) {

@@ -174,6 +174,7 @@ struct otsdb_ctx {
   int64_t tiles_whole = 0;
   bool verbatim = false;  // run_raw_verbatim: the cells query's rows as stored
   bool spec_miss = false;  // ... and they cannot be: the caller compacts
+  bool result_short = false;  // the last E_CAPACITY was the result's (finish)
   std::mutex mu;  // one query at a time per context
   // stage timing (otsdb_prof_*)
   bool prof = false;
@@ -1184,10 +1185,23 @@ otsdb_status finish(otsdb_ctx* c, int64_t G, otsdb_result* out) {
                 "a point past the window lies outside the calendar table");
   if (err & ERR_INTERNAL)
     return fail(OTSDB_E_DEVICE, "internal: bucket outside the group row");
-  if (total > out->capacity)
+  if (total > out->capacity) {
+    c->result_short = true;  // the offsets are whole: the host entries return them
     return fail(OTSDB_E_CAPACITY, "result capacity %lld < %lld points",
                 (long long)out->capacity, (long long)total);
+  }
   return OTSDB_OK;
+}
+
+// a host entry's result too small: the caller still gets the offsets the
+// whole result needs (offsets[G] = its point count), then the status
+otsdb_status copy_offsets_back(otsdb_ctx* c, otsdb_result* out,
+                               const int64_t* d_offsets, int64_t G,
+                               otsdb_status rc) {
+  HIP_TRY(hipMemcpyAsync(out->offsets, d_offsets, 8 * (G + 1),
+                         hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return rc;
 }
 
 otsdb_status read_goff(otsdb_ctx* c, const otsdb_batch* b, bool device,
@@ -2470,7 +2484,10 @@ otsdb_status otsdb_agg_run(otsdb_ctx* c, const otsdb_query_spec* spec,
   dr.ts = (int64_t*)pp[8];
   dr.val = (int64_t*)pp[9];
   dr.is_int = (uint8_t*)pp[10];
+  c->result_short = false;
   rc = run_device_impl(c, spec, &db, &dr, goff);
+  if (rc == OTSDB_E_CAPACITY && c->result_short)
+    return copy_offsets_back(c, out, dr.offsets, G, rc);
   if (rc) return rc;
   const int64_t total = c->h_small[1];
   HIP_TRY(hipMemcpyAsync(out->offsets, dr.offsets, 8 * (G + 1),
@@ -2889,7 +2906,10 @@ otsdb_status otsdb_agg_run_raw(otsdb_ctx* c, const otsdb_query_spec* spec,
   dres.ts = (int64_t*)pp[11];
   dres.val = (int64_t*)pp[12];
   dres.is_int = (uint8_t*)pp[13];
+  c->result_short = false;
   rc = run_raw_impl(c, spec, &dr, fix_duplicates != 0, &db, &dres, goff);
+  if (rc == OTSDB_E_CAPACITY && c->result_short)
+    return copy_offsets_back(c, out, dres.offsets, G, rc);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(out->offsets, dres.offsets, 8 * (G + 1),
                          hipMemcpyDeviceToHost, st));
@@ -2997,7 +3017,10 @@ otsdb_status otsdb_agg_run_cells(otsdb_ctx* c, const otsdb_query_spec* spec,
   dres.ts = (int64_t*)pp[9];
   dres.val = (int64_t*)pp[9] + (cap + 1);
   dres.is_int = (uint8_t*)pp[10];
+  c->result_short = false;
   rc = run_cells_impl(c, spec, &dc, &db, &dres, goff);
+  if (rc == OTSDB_E_CAPACITY && c->result_short)
+    return copy_offsets_back(c, out, dres.offsets, G, rc);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(out->offsets, dres.offsets, 8 * (G + 1),
                          hipMemcpyDeviceToHost, st));

@@ -27,6 +27,12 @@ def build():
 def load():
     if not os.path.exists(LIB):
         build()
+    # the engine first, through abi.load(): it imports torch so that
+    # libotsdb_agg.so (the shim's dependency) binds to torch's HIP runtime —
+    # the shim pulling in the system one first would start a second runtime
+    # in the process and leave torch without devices
+    from opentsdb_amd import abi
+    abi.load()
     lib = C.CDLL(LIB)
     lib.fj_exception_class.restype = C.c_char_p
     lib.fj_exception_message.restype = C.c_char_p
