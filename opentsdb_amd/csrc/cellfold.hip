@@ -209,6 +209,7 @@ __global__ __launch_bounds__(256) void k_cells_prep(Params P, CellsFold CF,
   // verbatim storage rows: every point of the series must be streamed (and
   // so checked for order) by the fold
   if (P.check_order && (lo != 0 || hi != Ns)) atomicOr(err_word, ERR_SPEC_MISS);
+  if (CF.wide) atomicOr(CF.wide, qw == 4 ? 1 : 2);
   store(true, lo, hi, rlo, vlo, qw, vl0, of_has, of_ts, of_val);
 }
 
@@ -504,7 +505,9 @@ DEV uint32_t cells_pick(const uint32_t* t, int32_t rel) {
 // pools exceed 2^30 bytes to the generic decode): loads address a uniform
 // base pointer plus a per-lane 32-bit offset, and no runtime multiply is
 // left (qualifier width and value length are powers of two: shifts).
-template <class M, class A, int K>
+// QW: the series' qualifier width when the launch fixes it (every kept
+// series of the batch has QW-byte qualifiers), 0: read from the member
+template <class M, class A, int K, int QW>
 DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
                            const FoldMember* mc, const CellsMember* cm) {
   constexpr int PTS = 64 * K;
@@ -516,7 +519,7 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
   if (!kept) return;
   const int32_t pe = (int32_t)uni(mc->pb);
   const int64_t r1 = uni(cm->r1);
-  const int qw = uni(cm->qw);
+  const int qw = QW ? QW : uni(cm->qw);
   const int qsh = qw == 4 ? 2 : 1;
   const int64_t qb = uni(cm->qb), vb0 = uni(cm->vb0);
   const uint8_t* qp = C.qual + qb;  // the series' qualifier stream

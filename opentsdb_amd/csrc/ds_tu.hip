@@ -76,6 +76,30 @@ bool launch_cells(DsKernel k, const DsLaunch& a) {
                            a.st, a.P, a.cf, S, a.SM, a.NW, a.WB, a.wc, a.err);
       OTSDB_DBG(a.st, "k_cells_fold_prep");
       return true;
+    case DS_CELLS_FOLD4:
+      return with_monoid(a.agg_id, [&](auto tag) {
+        using A = decltype(tag);
+        hipLaunchKernelGGL((k_fold<M, A, 8, 4>),
+                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(256),
+                           (unsigned)fold_lds_bytes<A>(a.P),
+                           a.st, a.P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
+                           a.tm1, a.single, a.members, a.wc, a.NW, a.partial,
+                           a.tile_emit, a.out_val, a.out_emit, a.err,
+                           a.always_partial, a.cf);
+        OTSDB_DBG(a.st, "k_fold<cells, qw 4>");
+      });
+    case DS_CELLS_FOLD2:
+      return with_monoid(a.agg_id, [&](auto tag) {
+        using A = decltype(tag);
+        hipLaunchKernelGGL((k_fold<M, A, 8, 2>),
+                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(256),
+                           (unsigned)fold_lds_bytes<A>(a.P),
+                           a.st, a.P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
+                           a.tm1, a.single, a.members, a.wc, a.NW, a.partial,
+                           a.tile_emit, a.out_val, a.out_emit, a.err,
+                           a.always_partial, a.cf);
+        OTSDB_DBG(a.st, "k_fold<cells, qw 2>");
+      });
     case DS_CELLS_FOLD:
       return with_monoid(a.agg_id, [&](auto tag) {
         using A = decltype(tag);

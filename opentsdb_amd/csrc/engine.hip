@@ -851,6 +851,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   if (cfold) {
     CF.C = *cells;
     CF.series_row = series_row;
+    CF.wide = c->d_err + 1;
   }
   auto carve = [&](char* base) {
     Carve cv{base};
@@ -902,7 +903,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   if (rc) return rc;
   carve((char*)c->ws);
 
-  HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), st));
+  HIP_TRY(hipMemsetAsync(c->d_err, 0, 2 * sizeof(int), st));  // + cells "wide"
   if (G * NB > 0 && mode != 1)
     HIP_TRY(hipMemsetAsync(W.out_emit, 0, (size_t)G * NB, st));
   // the ring-sink k_bucketize leaves sentinel rows whose states k_transform
@@ -965,7 +966,19 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       a.always_partial = mode == 1;
       a.agg_id = spec->agg_id;
       if (T.T > 0) {
-        if (cfold) launch_cells<M>(DS_CELLS_FOLD, a);
+        if (cfold) {
+          // every kept series on one qualifier width (k_cells_prep's bits
+          // 0 / 1: 4- / 2-byte series seen): the fold with that width fixed
+          // at compile time (14 % faster on C2's cells), else the generic one
+          int widths = 3;
+          if (hipMemcpyAsync(&c->h_small[2], c->d_err + 1, sizeof(int),
+                             hipMemcpyDeviceToHost, st) == hipSuccess &&
+              hipStreamSynchronize(st) == hipSuccess)
+            widths = (int)(c->h_small[2] & 3);
+          launch_cells<M>(widths == 3 ? DS_CELLS_FOLD
+                                      : (widths == 1 ? DS_CELLS_FOLD4 : DS_CELLS_FOLD2),
+                          a);
+        }
         else launch_ds<M>(DS_FOLD, a);
       }
     });

@@ -498,7 +498,7 @@ struct CellsMember {
   int32_t qw, vl0;
 };
 
-template <class M, class A, int K>
+template <class M, class A, int K, int QW>
 DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
                            const FoldMember* mc, const CellsMember* cm);
 
@@ -637,7 +637,7 @@ __global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
       }
     }
     if constexpr (CELLS != 0)
-      fold_member_cells<M, A, K>(P, CF.C, F, &mc[w], &cm[w]);
+      fold_member_cells<M, A, K, CELLS == 1 ? 0 : CELLS>(P, CF.C, F, &mc[w], &cm[w]);
     else
       fold_member<M, A, K>(P, B, F, &mc[w]);
     fold_publish(F, kProgDone);

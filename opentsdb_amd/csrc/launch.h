@@ -49,6 +49,9 @@ struct CellsFold {
   int64_t* wrlo;
   int64_t* wvlo;
   uint8_t* wvl0;
+  int* wide;                  // k_cells_prep: bit 0 / 1 = some kept series
+                              // has 4- / 2-byte qualifiers (one width: the
+                              // fold with that width fixed runs)
 };
 
 // buckets per fold window: the aggregator states of a window live in LDS
@@ -94,7 +97,10 @@ enum DsKernel {
   DS_FOLD,       // k_fold: downsample + contribution + ordered aggregator
   DS_CELLS_PREP, // k_cells_prep: bounds / cursors of a cells fold
   DS_CELLS_FOLD, // k_fold fed straight from compacted columns
-  DS_CELLS_FOLD_PREP  // k_cells_fold_prep: window boundaries of a cells fold
+  DS_CELLS_FOLD_PREP, // k_cells_fold_prep: window boundaries of a cells fold
+  DS_CELLS_FOLD2, // the cells fold of a batch whose kept series all have
+                  // 2-byte qualifiers (the width a compile-time constant)
+  DS_CELLS_FOLD4  // ... all 4-byte ones
 };
 
 struct DsLaunch {
