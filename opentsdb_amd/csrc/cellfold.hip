@@ -847,8 +847,8 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
       if (x == 42) F.emit[0] = 1;
     }
 #else
-    reduce_step<M, K, 1>(P, Bd, 1, p, hs, p, p0, t, v, S, err, carry_key,
-                         carry, hs < pe);
+    reduce_step<M, K, 1, uint32_t, 1>(P, Bd, 1, p, hs, p, p0, t, v, S, err,
+                                      carry_key, carry, hs < pe);
 #endif
     vcur += used + (ps1 <= hs ? m0 : 0) + (ps2 <= hs ? m1 : 0) +
             (ps3 <= hs ? m2 : 0);

@@ -741,7 +741,10 @@ DEV void ordered_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
 // of every lane (points i0 .. i0+K-1 of the series, step base `base`):
 // lane-local fold, the previous step's open bucket, the segmented wave scan
 // over the lanes' tail runs, the row writes and the new carry.
-template <class M, int K, int DPP, class TT = int64_t>
+// FO = 1: the caller guarantees doubles only (the cells fold decodes every
+// value to its double bits): the per-point type tests and their registers
+// are not compiled in
+template <class M, int K, int DPP, class TT = int64_t, int FO = 0>
 DEV void reduce_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
                      int64_t hi, int64_t base, int64_t i0, const TT* t,
                      const int64_t* v, RowSink& S, int& err,
@@ -757,7 +760,7 @@ DEV void reduce_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
   // applies, each lane to its in-range prefix
   const bool tail = !full && base >= lo && P.narrow;
   if (full || tail) {
-    const bool fonly = !B.is_float && sf;
+    const bool fonly = FO || (!B.is_float && sf);
     bool done = false;
     const int64_t nr = hi - i0;
     const int nv = full ? K : (int)(nr < 0 ? 0 : (nr > K ? K : nr));
@@ -779,13 +782,13 @@ DEV void reduce_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
                                           err, nseg, cur_key, head_key, cur,
                                           head);
       else
-        fold_lane<M, K, false, true, TT>(P, B, sf, i0, lo, hi, t, v, S,
-                                         err, nseg, cur_key, head_key, cur,
-                                         head);
+        fold_lane<M, K, FO != 0, true, TT>(P, B, sf, i0, lo, hi, t, v, S,
+                                           err, nseg, cur_key, head_key, cur,
+                                           head);
     }
   } else {
-    fold_lane<M, K, false, true, TT>(P, B, sf, i0, lo, hi, t, v, S,
-                                     err, nseg, cur_key, head_key, cur, head);
+    fold_lane<M, K, FO != 0, true, TT>(P, B, sf, i0, lo, hi, t, v, S,
+                                       err, nseg, cur_key, head_key, cur, head);
   }
   if (nseg == 0) {  // lane wholly before lo (first step) or past hi
     cur_key = (i0 < lo) ? -1 : INT32_MAX;
