@@ -100,18 +100,6 @@ bool launch_cells(DsKernel k, const DsLaunch& a) {
                            a.always_partial, a.cf);
         OTSDB_DBG(a.st, "k_fold<cells, qw 2>");
       });
-    case DS_CELLS_FOLD:
-      return with_monoid(a.agg_id, [&](auto tag) {
-        using A = decltype(tag);
-        hipLaunchKernelGGL((k_fold<M, A, 8, 1>),
-                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(256),
-                           (unsigned)fold_lds_bytes<A>(a.P),
-                           a.st, a.P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
-                           a.tm1, a.single, a.members, a.wc, a.NW, a.partial,
-                           a.tile_emit, a.out_val, a.out_emit, a.err,
-                           a.always_partial, a.cf);
-        OTSDB_DBG(a.st, "k_fold<cells>");
-      });
     default:
       return false;
   }

@@ -967,17 +967,24 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       a.agg_id = spec->agg_id;
       if (T.T > 0) {
         if (cfold) {
-          // every kept series on one qualifier width (k_cells_prep's bits
-          // 0 / 1: 4- / 2-byte series seen): the fold with that width fixed
-          // at compile time (14 % faster on C2's cells), else the generic one
+          // the fold with the qualifier width fixed at compile time (one
+          // copy of the member loop per kernel: 14 % faster on C2's cells
+          // than a width read per member).  k_cells_prep's bits 0 / 1: 4- /
+          // 2-byte series kept; both -> ERR_CELLS_GENERIC, and the engine
+          // rewrites the batch with one width (k_requal) and runs again
           int widths = 3;
-          if (hipMemcpyAsync(&c->h_small[2], c->d_err + 1, sizeof(int),
+          if (hipMemcpyAsync(&c->h_small[2], c->d_err, 2 * sizeof(int),
                              hipMemcpyDeviceToHost, st) == hipSuccess &&
               hipStreamSynchronize(st) == hipSuccess)
-            widths = (int)(c->h_small[2] & 3);
-          launch_cells<M>(widths == 3 ? DS_CELLS_FOLD
-                                      : (widths == 1 ? DS_CELLS_FOLD4 : DS_CELLS_FOLD2),
-                          a);
+            widths = (int)((c->h_small[2] >> 32) & 3);
+          if (widths == 3) {
+            const int e = (int)(c->h_small[2] & 0xFFFFFFFF) | ERR_CELLS_GENERIC;
+            c->h_small[3] = e;
+            hipMemcpyAsync(c->d_err, &c->h_small[3], sizeof(int),
+                           hipMemcpyHostToDevice, st);
+          } else {
+            launch_cells<M>(widths == 1 ? DS_CELLS_FOLD4 : DS_CELLS_FOLD2, a);
+          }
         }
         else launch_ds<M>(DS_FOLD, a);
       }

@@ -96,7 +96,8 @@ enum DsKernel {
   DS_FOLD_PREP,  // k_fold_prep: window boundaries of the ordered fold
   DS_FOLD,       // k_fold: downsample + contribution + ordered aggregator
   DS_CELLS_PREP, // k_cells_prep: bounds / cursors of a cells fold
-  DS_CELLS_FOLD, // k_fold fed straight from compacted columns
+  DS_CELLS_FOLD, // (unused: a batch whose kept series mix qualifier widths
+                 // is rewritten with one width, k_requal)
   DS_CELLS_FOLD_PREP, // k_cells_fold_prep: window boundaries of a cells fold
   DS_CELLS_FOLD2, // the cells fold of a batch whose kept series all have
                   // 2-byte qualifiers (the width a compile-time constant)

@@ -434,7 +434,7 @@ def test_fused_cells_ragged_rows(engine, kind, agg, ds, window):
             floor=fl)
 
 
-@pytest.mark.parametrize("layout", ["in-row", "by-row", "sparse"])
+@pytest.mark.parametrize("layout", ["in-row", "by-row", "by-series", "sparse"])
 @pytest.mark.parametrize("agg,ds,rate,days", [
     ("sum", "1m-avg", False, 0), ("dev", "5m-dev", False, 0),
     ("max", "1m-max-nan", False, 0), ("sum", "5m-sum", True, 0),
@@ -442,7 +442,8 @@ def test_fused_cells_ragged_rows(engine, kind, agg, ds, window):
 def test_fused_cells_mixed_widths(engine, layout, agg, ds, rate, days):
     """Columns mixing 2-byte second and 4-byte millisecond qualifiers
     (MS_MIXED_COMPACT inside rows, RowSeq.java:338-356), or series whose
-    rows alternate between the two widths, or sparse rows of both: k_requal
+    rows alternate between the two widths, or a batch whose series each
+    keep one width but not the same one, or sparse rows of both: k_requal
     rewrites them with 4-byte qualifiers and the cells fold streams them
     (one window and, over two days of 1 m buckets, several) — against the
     oracle on the points RowSeq decodes from the original columns."""
@@ -464,8 +465,11 @@ def test_fused_cells_mixed_widths(engine, layout, agg, ds, rate, days):
         ms = rng.integers(1, 999, len(b.ts))
         if layout == "in-row":  # about half the points on milliseconds
             b.ts = b.ts + ms * (rng.random(len(b.ts)) < 0.5)
-        else:  # odd hours on milliseconds, even hours on whole seconds
+        elif layout == "by-row":  # odd hours on ms, even hours on seconds
             b.ts = b.ts + ms * (((b.ts - datasets.T0) // 3600000) % 2)
+        else:  # odd series on ms (4-byte rows), even ones on seconds
+            sid = np.repeat(np.arange(b.n_series), np.diff(b.offsets))
+            b.ts = b.ts + ms * (sid % 2)
     for s in range(b.n_series):
         a, z = b.offsets[s], b.offsets[s + 1]
         b.ts[a:z] = np.sort(b.ts[a:z])
