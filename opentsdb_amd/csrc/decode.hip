@@ -60,15 +60,18 @@ DEV int64_t value_bits(uint64_t x, int vl, int fl) {
   }
 }
 
-// exclusive wave prefix sum of x; total = the wave's sum
+// exclusive wave prefix sum of x; total = the wave's sum.  DPP row shifts
+// and row broadcasts (VALU only, no LDS round trips); lanes without a
+// source add 0
 DEV int wave_excl_scan(int x, int& total) {
   int incl = x;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(incl, d);
-    if (LANE >= d) incl += y;
-  }
-  total = __shfl(incl, 63);
+  incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xF, 0xF, false);  // row_shr:1
+  incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xF, 0xF, false);  // row_shr:2
+  incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xF, 0xF, false);  // row_shr:4
+  incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xF, 0xF, false);  // row_shr:8
+  incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  total = __builtin_amdgcn_readlane(incl, 63);
   return incl - x;
 }
 
