@@ -1169,7 +1169,7 @@ __global__ __launch_bounds__(256) void k_requal(
       const uint32_t S = cin ? S1 : (S1 ^ flip);
       // a 4-byte qualifier cut by the column end
       if (nu > 0 && ub + nu == units) bad |= (int)(((S & m) >> (nu - 1)) & 1u);
-      cs = __shfl(d ? fixed_out : cin, 63);
+      cs = __builtin_amdgcn_readlane(d ? fixed_out : cin, 63);
       const int np = __builtin_popcount(S);
       if (MODE == 0) {
         n_acc += np;
