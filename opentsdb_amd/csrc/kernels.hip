@@ -441,9 +441,17 @@ DEV void rate_flush(const Params& P, RowSink& S, RateState& R, int64_t f,
   const bool p = inb && __double_as_longlong(v) != kAbsentBits;
   const int64_t t = inb ? bucket_ts(P, b) : 0;
   const uint64_t pm = __ballot(p);
+  const uint64_t im = __ballot(inb);
   const uint64_t below = pm & ((1ULL << lane) - 1);
   const int pl = below ? 63 - __builtin_clzll(below) : -1;
-  const double vp = __shfl(v, pl >= 0 ? pl : 0);
+  // every bucket of the run present (dense series): the previous point is
+  // the lane before (a DPP shift, not a lane shuffle)
+  double vp;
+#ifndef OTSDB_RATE_SHFL  // tuning builds: lane shuffles only
+  if (pm == im) vp = dppd<0x138, 0xF>(v);
+  else
+#endif
+    vp = __shfl(v, pl >= 0 ? pl : 0);
   const int64_t tprev = pl >= 0 ? bucket_ts(P, f + pl) : R.carry_pts;
   const double vprev = pl >= 0 ? vp : R.carry_pv;
   bool kept = false;
@@ -468,7 +476,7 @@ DEV void rate_flush(const Params& P, RowSink& S, RateState& R, int64_t f,
   const uint64_t km = __ballot(k);
   if (km) {
     const int f0 = __builtin_ctzll(km);
-    const double rf = __shfl(rate, f0);
+    const double rf = readlane_d(rate, f0);
     if (R.r0_idx < 0) {
       R.r0_idx = f + f0;
       R.r0_val = rf;
@@ -486,7 +494,13 @@ DEV void rate_flush(const Params& P, RowSink& S, RateState& R, int64_t f,
   const double kv = k ? rate : 0.0;
   const uint64_t upto = km & ((2ULL << lane) - 1);
   const int il = upto ? 63 - __builtin_clzll(upto) : -1;
-  const double lv = __shfl(kv, il >= 0 ? il : 0);
+  // every bucket of the run kept: its own rate
+  double lv;
+#ifndef OTSDB_RATE_SHFL
+  if (km == im) lv = kv;
+  else
+#endif
+    lv = __shfl(kv, il >= 0 ? il : 0);
   const double held = il >= 0 ? lv : (R.carry_k >= 0 ? R.carry_kv : R.r0_val);
   if (inb) {
     const bool real = k && b != R.r0_idx;
