@@ -36,8 +36,11 @@
 // (the cursor lands on the next row's val_off); illegal value lengths are
 // corrupt (ERR_CORRUPT_CELL).  A row whose qualifier width differs from the
 // series' (MS_MIXED_COMPACT columns, or second and ms rows in one series)
-// raises ERR_CELLS_GENERIC: the engine then decodes the batch and runs the
-// columnar pipeline, as the row-per-step kernel does.
+// raises ERR_CELLS_GENERIC: the engine then rewrites the batch's qualifiers
+// with one width (k_requal, decode.hip) and runs the fold again; what still
+// does not fit (a series pool past 2^30 bytes) is decoded into columns and
+// takes the columnar pipeline.  The fold itself is compiled once per
+// qualifier width (QW) and launched with the width k_cells_prep saw.
 #pragma once
 #include "fold.hip"
 
@@ -220,7 +223,7 @@ __global__ __launch_bounds__(256) void k_cells_prep(Params P, CellsFold CF,
 // the points like the Downsampler does) plus the cells stream's cursor there
 // (row, value byte offset, value length), from the series' qualifier stream.
 // A row whose qualifier width is not the series' raises ERR_CELLS_GENERIC
-// (the generic decode takes the batch, as in k_cells_prep).
+// (the batch is rewritten with one width, as in k_cells_prep).
 template <class M>
 __global__ __launch_bounds__(256) void k_cells_fold_prep(
     Params P, CellsFold CF, int64_t S, SeriesMeta SM, int64_t NW, int64_t WB,
