@@ -1164,10 +1164,6 @@ otsdb_status compact(otsdb_ctx* c, const Params& P, int64_t G,
                      (uint8_t*)nullptr, 0);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, G,
                      (const int64_t*)counts, out->offsets);
-  // downsampled results are doubles: is_int is 0 for every point (at most
-  // one per (group, bucket))
-  const int64_t n_isint = std::min<int64_t>(out->capacity, G * P.nb);
-  if (n_isint > 0) HIP_TRY(hipMemsetAsync(out->is_int, 0, (size_t)n_isint, st));
   hipLaunchKernelGGL(k_compact, dim3(blocks_for(G, 4)), dim3(256), 0, st, P,
                      G, out_val, out_emit, counts,
                      (const int64_t*)out->offsets, out->capacity, out->ts,

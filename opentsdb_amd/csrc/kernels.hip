@@ -1810,9 +1810,10 @@ __global__ __launch_bounds__(256) void k_compact(
       const uint64_t m = __ballot(e[u]);
       if (e[u]) {
         const int64_t p = pos + __popcll(m & ((1ULL << lane) - 1));
-        if (p < cap) {  // (is_int: 0 throughout, one memset by the engine)
+        if (p < cap) {
           r_ts[p] = bucket_ts(P, b);
           r_val[p] = __double_as_longlong(v[u]);
+          r_isint[p] = 0;  // downsampled values are doubles
         }
       }
       pos += __popcll(m);
