@@ -112,8 +112,14 @@ constexpr int64_t kOrderedFoldChunk = 256;
 constexpr int64_t kOrderedChunk = 16384;
 // below this many (tile, window) workgroups the fold narrows its windows,
 // down to kFoldMinWindow buckets
-constexpr int64_t kFoldMinBlocks = 2048;
-constexpr int64_t kFoldMinWindow = 128;
+#ifndef OTSDB_FOLD_MIN_BLOCKS  // tuning builds override
+#define OTSDB_FOLD_MIN_BLOCKS 1024
+#endif
+#ifndef OTSDB_FOLD_MIN_WINDOW
+#define OTSDB_FOLD_MIN_WINDOW 128
+#endif
+constexpr int64_t kFoldMinBlocks = OTSDB_FOLD_MIN_BLOCKS;
+constexpr int64_t kFoldMinWindow = OTSDB_FOLD_MIN_WINDOW;
 
 // the storage rows cannot be taken verbatim (run_raw_verbatim): flagged on
 // the context, never returned through the C-ABI
