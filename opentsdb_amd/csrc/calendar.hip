@@ -154,15 +154,22 @@ __global__ __launch_bounds__(256) void k_cal_fill_count(
     bool k_on = false;
     int64_t v = start_ms - 1;
     if (i >= lo) {
-      // (a point past its chain's last edge lies past every FD edge: its
-      // bucket is never emitted, and nothing else reads it)
       const int64_t k = last_le(A.edges, pos, cend, B.ts[i]);
       if (k < pos) {
         bad = 1;
       } else if (k + 1 < cend) {
         v = A.edges[k];
         k_on = on_grid(fd, nfd, v);
+      } else if (A.edges[cend - 1] <= fd[nfd - 1]) {
+        // past its chain's last edge, and that edge is not past the filling
+        // grid: the point's bucket starts at that edge or at some later one
+        // the table does not hold — it may be an FD edge (emitted) or not
+        // (dropped), so the engine cannot tell (the caller's chains end too
+        // early: E_UNSUPPORTED, as for a global table's)
+        bad = 1;
       }
+      // (otherwise the point's bucket starts past every FD edge: it is never
+      // emitted, and nothing else reads it)
     }
     vts[i] = v;
     on[i] = k_on;

@@ -158,3 +158,60 @@ def test_comparator_rejects_a_reordered_welford():
     assert any((m["bits"] != r["bits"]).any() for m, r in zip(mut, ref))
     with pytest.raises(AssertionError):
         compare([_Res(p) for p in mut], ref, False, "reordered-dev", fl)
+
+
+def _sweep_cases():
+    """The general sweep's first 120 seeds and sweep_many.py's 5000-5399 (the
+    seeds whose MAX / MIN fill-ins gave round 4's comparator floors of
+    ~1e296 or infinity: 5007, 5184, 5255, 5397)."""
+    for seed in list(range(120)) + list(range(5000, 5400)):
+        b, spec, exact, where = _case(seed)
+        try:
+            ref = pyoracle.group_by(spec, b)
+        except pyoracle.OracleError:
+            continue
+        yield b, spec, exact, where, ref
+
+
+def test_contribution_floors_are_finite_and_bounded():
+    """No floor of the sweep comparator is infinite or lets a MAX_VALUE
+    fill-in in: every floor is at most 2e-12 x the sum over the group's
+    members of the largest scale of the member's own view stream — a bound
+    computed from the real contributions only, whatever the interpolation
+    (AggregationIterator.java:711-719, :781-787)."""
+    from tests.test_gpu_parity import _member_scales
+    n_fill = 0
+    for b, spec, exact, where, ref in _sweep_cases():
+        views = _member_scales(spec, b)
+        fl = contribution_floor(spec, b, ref, views)
+        n_fill += spec.interp in (2, 3)
+        for g, (f, gv) in enumerate(zip(fl, views)):
+            assert np.isfinite(f).all(), where
+            bound = 2e-12 * sum(float(sc.max()) for _, _, sc in gv if len(sc))
+            assert (f <= bound).all(), "%s/g%d: floor %g > %g" % (
+                where, g, f.max(), bound)
+    assert n_fill >= 40, n_fill  # the generator's MAX / MIN overrides
+
+
+def test_comparator_sees_perturbed_fill_in_results():
+    """Every sweep query with a MAX / MIN fill-in (mimmin / mimmax, whose
+    default interpolation it is, and the i2 / i3 overrides): a 1e-9 relative
+    change of any nonzero output point is outside the comparator's bound at
+    all but a handful of points (where the result is a near-cancellation of
+    real contributions).  Round 4's floors took the fill-ins' MAX_VALUE as a
+    scale and were blind at 910 of these 26,302 points; now 4."""
+    from tests.test_gpu_parity import _vals
+    n = blind = 0
+    for b, spec, exact, where, ref in _sweep_cases():
+        agg = where.split(":")[1]
+        if spec.rate or not (spec.interp in (2, 3) or
+                             agg in ("mimmin", "mimmax")):
+            continue
+        for r, f in zip(ref, contribution_floor(spec, b, ref)):
+            v = _vals(r["bits"], r["is_int"])
+            sel = np.isfinite(v) & (v != 0) & (np.abs(v) < 1e300)
+            tol = 1e-12 * np.abs(v[sel]) + np.asarray(f)[sel]
+            n += int(sel.sum())
+            blind += int((1e-9 * np.abs(v[sel]) <= tol).sum())
+    assert n > 20000, n
+    assert blind <= n // 1000, (blind, n)

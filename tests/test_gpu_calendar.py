@@ -209,3 +209,45 @@ def test_per_series_grids_from_cells(engine, ds):  # noqa: F811
     res = DeviceResult(torch, db.n_groups, 4 * len(hb.ts) + 64, "cuda")
     workload.run_cells_device(engine, spec, cells_d, db, res)
     compare(_result_points(res, db.n_groups), ref, False, where="cells/" + ds)
+
+
+def test_per_series_grids_with_fill_chain_ends_inside_the_window(engine):  # noqa: F811
+    """FillingDownsampler over per-series grids whose caller-supplied chains
+    end inside the window (every chain but the filling grid's own is cut at
+    the window's middle): a point past its chain's last edge may lie in a
+    bucket that starts on the filling grid, and the table cannot say which
+    — the engine must not drop it (and fill its bucket) silently:
+    E_UNSUPPORTED, the Java path's query (advisor, round 4)."""
+    import numpy as np
+    b = datasets.random_batch(197, n_series=24, n_groups=3, span_ms=3 * DAY,
+                              cadence_ms=60000, t0=T_SPRING)
+    start, end = T_SPRING + 3600000, T_SPRING + 2 * DAY
+    spec = _cal_spec("sum", "7mc-avg-nan", None, start, end, batch=b)
+    assert spec.n_cal_anchors > 0
+    edges = spec._cal_edges_ref.copy()
+    anchors, aedge = (np.array(x) for x in spec._cal_anchor_refs)
+    big = np.iinfo(np.int64).max
+    terms = np.nonzero(edges == big)[0]
+    j = int(np.searchsorted(anchors, start, "right")) - 1
+    fd_term = int(terms[np.searchsorted(terms, aedge[j])])
+    mid = (start + end) // 2
+    a, cut_any = 0, False
+    for t in terms:
+        if t != fd_term:
+            seg = np.arange(a, t)
+            past = seg[edges[seg] > mid]
+            if len(past) > 1:
+                edges[past[0]] = big
+                cut_any = True
+        a = t + 1
+    assert cut_any
+    keep = edges[aedge] == anchors
+    anchors, aedge = anchors[keep], aedge[keep]
+    spec._cal_edges_ref, spec._cal_anchor_refs = edges, (anchors, aedge)
+    spec.cal_edges = edges.ctypes.data
+    spec.n_cal_edges = len(edges)
+    spec.cal_anchors = anchors.ctypes.data
+    spec.cal_anchor_edge = aedge.ctypes.data
+    spec.n_cal_anchors = len(anchors)
+    with pytest.raises(core.UnsupportedOperationException):
+        engine.run(spec, b)

@@ -28,6 +28,14 @@ pytestmark = pytest.mark.gpu
 
 ORDER_FREE = {"min", "max", "mimmin", "mimmax", "first", "last", "count",
               "diff"}
+# cross-series aggregators whose result moves by at most the largest error
+# of one contribution: selections, percentiles (between two selections),
+# population sigma, last - first
+LIPSCHITZ_AGG = ({"dev", "diff", "min", "max", "mimmin", "mimmax", "first",
+                  "last", "median"} |
+                 {"p%s" % q for q in ("999", "99", "95", "90", "75", "50")} |
+                 {"ep%sr%d" % (q, k) for q in ("999", "99", "95", "90", "75",
+                                              "50") for k in (3, 7)})
 
 
 @pytest.fixture(scope="module")
@@ -158,7 +166,7 @@ def _member_scales(spec, batch):
     return out
 
 
-def contribution_floor(spec, batch, ref):
+def contribution_floor(spec, batch, ref, views=None):
     """Per emitted point, the absolute floor 1e-12 x sum of the scales of
     the values the cross-series aggregator is fed at that timestamp
     (AggregationIterator.java:682-797) — each member's real value, or its
@@ -170,21 +178,34 @@ def contribution_floor(spec, batch, ref):
     a contribution's own computation does (rates; sums over raw values of
     both signs).  Elsewhere the comparator is the
     pure 1e-12 relative bound (a sum of same-signed terms keeps its relative
-    error)."""
+    error).
+
+    A member filled in with Long/Double MAX_VALUE or -MAX_VALUE (MAX / MIN
+    interpolation, AggregationIterator.java:711-719, :781-787) contributes
+    an exact constant: it carries no rounding and takes no part in the floor
+    (scale 0, no sign), so every floor is at most 1e-12 x the sum of the
+    real contributions' scales (tests/test_comparator_cpu.py checks that
+    over the sweep generator).  Aggregators whose result moves by at most
+    one contribution's error (LIPSCHITZ_AGG: selections, percentiles, dev,
+    diff) take 2e-12 x the largest scale instead of the sum, avg the sum's
+    floor / the number of contributions."""
     interp = spec.interp
     if interp < 0:
         interp = core.Aggregators.by_id(spec.agg_id).interpolationMethod()
     interp = int(interp)
     agg = core.Aggregators.by_id(spec.agg_id).registry_name
-    big = np.finfo(np.float64).max
     floors = []
-    for views, r in zip(_member_scales(spec, batch), ref):
+    if views is None:
+        views = _member_scales(spec, batch)
+    for gviews, r in zip(views, ref):
         x = np.asarray(r["ts"], np.int64)
         mag = np.zeros(len(x))
+        mag_max = np.zeros(len(x))
+        n_live = np.zeros(len(x), np.int64)
         pos = np.zeros(len(x), bool)
         neg = np.zeros(len(x), bool)
         amp = np.zeros(len(x), bool)  # a contribution's own subtraction
-        for vts, vv, sc in views:
+        for vts, vv, sc in gviews:
             if len(vts) == 0:
                 continue
             v = np.nan_to_num(vv, nan=0.0)
@@ -208,11 +229,9 @@ def contribution_floor(spec, batch, ref):
                     lo, hi, m = y0, y1, np.maximum(s0, s1)
                 elif interp == 1:  # ZIM
                     lo = hi = m = np.zeros(len(x))
-                elif interp == 2:  # MAX
-                    lo = hi = m = np.full(len(x), big)
-                elif interp == 3:  # MIN
-                    lo = hi = np.full(len(x), -big)
-                    m = np.full(len(x), big)
+                elif interp in (2, 3):  # MAX / MIN: an exact constant
+                    live = live & exact_pt
+                    lo = hi = m = np.zeros(len(x))
                 else:              # PREV
                     lo = hi = y0
                     m = s0
@@ -220,11 +239,23 @@ def contribution_floor(spec, batch, ref):
                 hi = np.where(exact_pt, y1, hi)
                 m = np.where(exact_pt, s1, m)
             mag += np.where(live, m, 0.0)
+            mag_max = np.maximum(mag_max, np.where(live, m, 0.0))
+            n_live += live
             pos |= live & ((lo > 0) | (hi > 0))
             neg |= live & ((lo < 0) | (hi < 0))
             amp |= live & (m > np.maximum(np.abs(lo), np.abs(hi)))
         need = (pos & neg) | amp | (agg in ("dev", "diff"))
-        floors.append(np.where(need, 1e-12 * mag, 0.0))
+        if agg in LIPSCHITZ_AGG:
+            # |f(x + d) - f(x)| <= max|d_i| (population sigma, last - first,
+            # a selection or an interpolation between two selections): the
+            # largest contribution error bounds the result's, whatever the
+            # group size
+            fl = 2e-12 * mag_max
+        elif agg == "avg":
+            fl = 1e-12 * mag / np.maximum(n_live, 1)
+        else:
+            fl = 1e-12 * mag
+        floors.append(np.where(need, fl, 0.0))
     return floors
 
 

@@ -32,8 +32,10 @@ INTERVALS = ["30s", "1m", "2m", "5m", "7m", "13m", "1h"]
 # and dev (one sequential Welford pass per bucket, in point order)
 EXACT_DS = ("min", "max", "count", "first", "last", "mimmax", "median", "p90",
             "dev")
+# cross-series: order-free ones, and dev (one sequential chain per (group,
+# bucket) in SpanCmp order) and diff (last - first) over exact inputs
 EXACT_AGG = ("min", "max", "mimmin", "mimmax", "count", "first", "last",
-             "median", "p50", "p95", "p99", "ep90r3", "ep99r7")
+             "median", "p50", "p95", "p99", "ep90r3", "ep99r7", "dev", "diff")
 
 
 def _case(seed):
