@@ -278,6 +278,24 @@ otsdb_status otsdb_agg_partials_device(otsdb_ctx* ctx,
                                        const otsdb_batch* batch,
                                        otsdb_partial* partials,
                                        uint8_t* emit, void* hip_stream);
+/* The same, each (group, bucket) continuing from `init`/`init_emit` (DEVICE,
+ * [G*n_buckets]): the state of the group's members on the ranks before this
+ * one.  Handed from rank to rank in series order, the last rank's output is
+ * the state ONE pass over every member in SpanCmp order reaches — for `dev`
+ * the reference's single Welford loop (StdDev.runDouble,
+ * src/core/Aggregators.java:547-568, fed by AggregationIterator.java:735-797)
+ * bit for bit while each rank's share of a group is one chain
+ * (<= 65,536 members), where merging per-rank partials (Chan's formula)
+ * lands ~1e-11 from it on offset data.  Groups with no member on this rank
+ * pass their state on unchanged; init may alias partials.  Finalise the last
+ * rank's output with otsdb_agg_finalize_device(n_ranks = 1).              */
+otsdb_status otsdb_agg_partials_chained_device(otsdb_ctx* ctx,
+                                               const otsdb_query_spec* spec,
+                                               const otsdb_batch* batch,
+                                               const otsdb_partial* init,
+                                               const uint8_t* init_emit,
+                                               otsdb_partial* partials,
+                                               uint8_t* emit, void* hip_stream);
 /* Combines `n_ranks` partial sets laid out rank-major in DEVICE memory
  * ([n_ranks][G*n_buckets], combined in rank order = series order) and
  * writes the final result (DEVICE pointers).                                */

@@ -136,7 +136,8 @@ EXPORTS = [
     "otsdb_last_error", "otsdb_agg_lookup", "otsdb_agg_name",
     "otsdb_agg_interpolation", "otsdb_agg_plan", "otsdb_agg_run",
     "otsdb_agg_run_device", "otsdb_agg_partials_device",
-    "otsdb_agg_finalize_device", "otsdb_gen_counts_device",
+    "otsdb_agg_partials_chained_device", "otsdb_agg_finalize_device",
+    "otsdb_gen_counts_device",
     "otsdb_gen_fill_device", "otsdb_prof_enable", "otsdb_prof_read",
     "otsdb_decode_cells_device", "otsdb_sel_prepare_device",
     "otsdb_sel_hist_device", "otsdb_sel_hist_wait", "otsdb_sel_finish_device",
@@ -189,6 +190,9 @@ def load(path=None):
     lib.otsdb_agg_run_device.restype = C.c_int
     lib.otsdb_agg_partials_device.argtypes = [vp, PS, PB, vp, vp, vp]
     lib.otsdb_agg_partials_device.restype = C.c_int
+    lib.otsdb_agg_partials_chained_device.argtypes = [vp, PS, PB, vp, vp, vp,
+                                                      vp, vp]
+    lib.otsdb_agg_partials_chained_device.restype = C.c_int
     lib.otsdb_agg_finalize_device.argtypes = [vp, PS, i64, i64, i32, vp, vp,
                                               PR, vp]
     lib.otsdb_agg_finalize_device.restype = C.c_int

@@ -105,11 +105,14 @@ constexpr int64_t kFoldChunk = 32;
 // ~1e-11 from the reference's one sequential pass, Aggregators.java:547-568)
 // reduce a group's members in ONE sequential chain per (group, bucket) while
 // the group fits: fold tiles of up to kOrderedFoldChunk members (the LDS
-// progress marks of one workgroup), then the row path's k_group with chunks
-// of up to kOrderedChunk members (one thread walks them in SpanCmp order).
-// Larger groups, and groups spanning ranks, merge ordered chunk partials.
+// progress marks of one workgroup), then the row path's k_group with one
+// chain of up to kOrderedChunk members (one thread walks them in SpanCmp
+// order; ~100 ns a member: tools/chain_probe.hip, 69 ns with no memory at
+// all, so a 500k-member chain — C4 — would cost ~50 ms).  Larger groups
+// merge 256-member chunk partials in order (Chan); across ranks the chain is
+// handed on (otsdb_agg_partials_chained_device).
 constexpr int64_t kOrderedFoldChunk = 256;
-constexpr int64_t kOrderedChunk = 16384;
+constexpr int64_t kOrderedChunk = 65536;
 // below this many (tile, window) workgroups the fold narrows its windows,
 // down to kFoldMinWindow buckets
 #ifndef OTSDB_FOLD_MIN_BLOCKS  // tuning builds override
@@ -699,13 +702,13 @@ template <class M>
 void launch_combine(otsdb_ctx* c, const Work& W, int64_t NB, int64_t n,
                     const int64_t* g, const int64_t* t0, const int64_t* t1,
                     double* out_val, uint8_t* out_emit, Packed* out_partial,
-                    bool two_level) {
+                    bool two_level, int keep_empty = 0) {
   hipStream_t st = c->stream;
   if (!two_level) {
     hipLaunchKernelGGL(k_combine<M>, dim3(blocks_for(n * NB, 256)), dim3(256),
                        0, st, NB, n, g, t0, t1, (const Packed*)W.partial,
                        (const uint8_t*)W.tile_emit, out_val, out_emit,
-                       out_partial, c->d_err, (int64_t)0);
+                       out_partial, c->d_err, (int64_t)0, keep_empty);
     return;
   }
   hipLaunchKernelGGL(k_combine_l1<M>,
@@ -716,7 +719,7 @@ void launch_combine(otsdb_ctx* c, const Work& W, int64_t NB, int64_t n,
   hipLaunchKernelGGL(k_combine<M>, dim3(blocks_for(n * NB, 256)), dim3(256), 0,
                      st, NB, n, g, t0, t1, (const Packed*)W.comb,
                      (const uint8_t*)W.comb_emit, out_val, out_emit,
-                     out_partial, c->d_err, kCombineSlices);
+                     out_partial, c->d_err, kCombineSlices, keep_empty);
 }
 
 // The per-downsampler kernels live in one translation unit per downsampling
@@ -753,12 +756,15 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
                           std::vector<int64_t>& goff, Params& P, Work& W,
                           int mode, Packed* gpart, uint8_t* gemit,
                           const CellsDev* cells = nullptr,
-                          const int64_t* series_row = nullptr) {
+                          const int64_t* series_row = nullptr,
+                          const Packed* ginit = nullptr,
+                          const uint8_t* ginit_emit = nullptr) {
   hipStream_t st = c->stream;
   const int64_t S = B.S;
   const int64_t G = (int64_t)goff.size() - 1;
   const int64_t nb = P.nb;
-  bool fold = fold_path(spec, P, mode);
+  // chained partials continue each group's state in k_group (the row path)
+  bool fold = fold_path(spec, P, mode) && !ginit;
 
   // grid trimming for very wide windows (NONE fill only): the rows span only
   // the buckets that hold data
@@ -807,11 +813,17 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   });
   if (ordered && fold) {
     // a group past one fold tile takes the row path (one chain per bucket)
-    // when its bucket matrix fits
+    // when its bucket matrix (8-byte value + state byte per series and
+    // bucket) fits in what the device has free; otherwise the fold's tiles
+    // stay, merged in order (Chan) like a group past the exact-chain bound
     int64_t kmax = 0;
     for (size_t g = 0; g + 1 < goff.size(); ++g)
       kmax = std::max(kmax, goff[g + 1] - goff[g]);
-    if (kmax > kOrderedFoldChunk && (double)S * (double)NB <= 2.0e10) {
+    size_t free_b = 0, total_b = 0;
+    if (kmax > kOrderedFoldChunk &&
+        hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+        (double)S * (double)NB * 9.0 + (double)c->ws_cap <=
+            0.8 * ((double)free_b + (double)c->ws_cap)) {
       fold = false;
       WB = NW = 0;
     }
@@ -1085,7 +1097,8 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         hipLaunchKernelGGL(k_group<MC>, dim3(blocks_for(T.T * NB, 256)),
                            dim3(256), 0, st, NB, T.T, T.tg, T.tm0, T.tm1,
                            T.single, d_members, W.R, W.partial, W.tile_emit,
-                           W.out_val, W.out_emit, c->d_err, 0);
+                           W.out_val, W.out_emit, c->d_err, 0,
+                           (const Packed*)nullptr, (const uint8_t*)nullptr);
       if (T.MG > 0)
         launch_combine<MC>(c, W, NB, T.MG, T.mg, T.mt0, T.mt1, W.out_val,
                            W.out_emit, nullptr, two_level);
@@ -1134,14 +1147,15 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
           hipLaunchKernelGGL(k_group<M>, dim3(blocks_for(T.T * NB, 256)),
                              dim3(256), 0, st, NB, T.T, T.tg, T.tm0, T.tm1,
                              T.single, d_members, W.R, W.partial, W.tile_emit,
-                             W.out_val, W.out_emit, c->d_err, mode);
+                             W.out_val, W.out_emit, c->d_err, mode, ginit,
+                             ginit_emit);
         if (mode == 0) {
           if (T.MG > 0)
             launch_combine<M>(c, W, NB, T.MG, T.mg, T.mt0, T.mt1, W.out_val,
                               W.out_emit, nullptr, two_level);
         } else {
           launch_combine<M>(c, W, NB, G, T.ag, T.at0, T.at1, W.out_val, gemit,
-                            gpart, two_level);
+                            gpart, two_level, ginit ? 1 : 0);
         }
       });
       if (!ok) return fail(OTSDB_E_NO_SUCH_ELEMENT, "aggregator %d", spec->agg_id);
@@ -2527,12 +2541,14 @@ otsdb_status otsdb_agg_run(otsdb_ctx* c, const otsdb_query_spec* spec,
   return OTSDB_OK;
 }
 
-otsdb_status otsdb_agg_partials_device(otsdb_ctx* c,
-                                       const otsdb_query_spec* spec,
-                                       const otsdb_batch* b,
-                                       otsdb_partial* partials, uint8_t* emit,
-                                       void* hip_stream) {
-  if (!c || !spec || !b || !partials || !emit)
+}  // extern "C"
+
+namespace {
+otsdb_status partials_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
+                           const otsdb_batch* b, const otsdb_partial* init,
+                           const uint8_t* init_emit, otsdb_partial* partials,
+                           uint8_t* emit, void* hip_stream) {
+  if (!c || !spec || !b || !partials || !emit || (!init != !init_emit))
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(hipSetDevice(c->device));
@@ -2552,13 +2568,23 @@ otsdb_status otsdb_agg_partials_device(otsdb_ctx* c,
                b->series_float};
     Work W;
     const int64_t G = (int64_t)goff.size() - 1;
-    if (G * P.nb > 0) {
+    if (G * P.nb > 0 && init) {
+      // groups with no member here pass their state on unchanged
+      if (init != partials)
+        HIP_TRY(hipMemcpyAsync(partials, init,
+                               sizeof(otsdb_partial) * (size_t)G * P.nb,
+                               hipMemcpyDeviceToDevice, c->stream));
+      if (init_emit != emit)
+        HIP_TRY(hipMemcpyAsync(emit, init_emit, (size_t)G * P.nb,
+                               hipMemcpyDeviceToDevice, c->stream));
+    } else if (G * P.nb > 0) {
       hipMemsetAsync(emit, 0, (size_t)G * P.nb, c->stream);
       hipMemsetAsync(partials, 0, sizeof(otsdb_partial) * (size_t)G * P.nb,
                      c->stream);
     }
     rc = run_pipeline(c, spec, B, b->group_members, goff, P, W, 1,
-                      (Packed*)partials, emit);
+                      (Packed*)partials, emit, nullptr, nullptr,
+                      (const Packed*)init, init_emit);
     if (!rc) {
       HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
                              hipMemcpyDeviceToHost, c->stream));
@@ -2570,6 +2596,27 @@ otsdb_status otsdb_agg_partials_device(otsdb_ctx* c,
     }
   }
   return rc;
+}
+}  // namespace
+
+extern "C" {
+
+otsdb_status otsdb_agg_partials_device(otsdb_ctx* c,
+                                       const otsdb_query_spec* spec,
+                                       const otsdb_batch* b,
+                                       otsdb_partial* partials, uint8_t* emit,
+                                       void* hip_stream) {
+  return partials_impl(c, spec, b, nullptr, nullptr, partials, emit,
+                       hip_stream);
+}
+
+otsdb_status otsdb_agg_partials_chained_device(
+    otsdb_ctx* c, const otsdb_query_spec* spec, const otsdb_batch* b,
+    const otsdb_partial* init, const uint8_t* init_emit,
+    otsdb_partial* partials, uint8_t* emit, void* hip_stream) {
+  if (!init || !init_emit) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null init");
+  return partials_impl(c, spec, b, init, init_emit, partials, emit,
+                       hip_stream);
 }
 
 otsdb_status otsdb_agg_finalize_device(otsdb_ctx* c,

@@ -1502,6 +1502,10 @@ DEV void transform_rate(const Params& P, const SeriesMeta& SM, int64_t s,
 // (chunk of a group's members, bucket); the members of a chunk are pushed in
 // SpanCmp order, so a group of <= CHUNK series reproduces the Java sum
 // bit for bit.  Single-chunk groups finish here; others leave partials.
+// init (chained partials, otsdb_agg_partials_chained_device): the state of
+// the group's members on earlier ranks; a group's first chunk continues it,
+// so a dev chain runs on across ranks exactly as StdDev.runDouble's one
+// loop (Aggregators.java:547-568).
 // ------------------------------------------------------------------------
 template <class M>
 __global__ __launch_bounds__(256) void k_group(
@@ -1510,7 +1514,8 @@ __global__ __launch_bounds__(256) void k_group(
     const uint8_t* __restrict__ tile_single, const int64_t* __restrict__ members,
     Rows R, Packed* __restrict__ partial, uint8_t* __restrict__ tile_emit,
     double* __restrict__ out_val, uint8_t* __restrict__ out_emit,
-    int* err_word, int always_partial) {
+    int* err_word, int always_partial, const Packed* __restrict__ init = nullptr,
+    const uint8_t* __restrict__ init_emit = nullptr) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t t = idx / nb;
   if (t >= n_tiles) return;
@@ -1518,6 +1523,11 @@ __global__ __launch_bounds__(256) void k_group(
   const int64_t m0 = tile_m0[t], m1 = tile_m1[t];
   M st = M::init();
   int emit = 0;
+  if (init && (t == 0 || tile_g[t - 1] != tile_g[t])) {
+    const int64_t o = tile_g[t] * nb + b;
+    st = M::unpack(init[o]);
+    emit = init_emit[o];
+  }
   int64_t m = m0;
   // (the chain is latency-bound on the gathers: 8 members' loads in flight;
   // chunks of dev groups run up to kOrderedChunk members)
@@ -1624,12 +1634,16 @@ __global__ __launch_bounds__(256) void k_combine(
     const int64_t* __restrict__ grp_t0, const int64_t* __restrict__ grp_t1,
     const Packed* __restrict__ partial, const uint8_t* __restrict__ tile_emit,
     double* __restrict__ out_val, uint8_t* __restrict__ out_emit,
-    Packed* __restrict__ out_partial, int* err_word, int64_t ns) {
+    Packed* __restrict__ out_partial, int* err_word, int64_t ns,
+    int keep_empty = 0) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t i = idx / nb;
   if (i >= n_groups) return;
   const int64_t b = idx - i * nb;
   const int64_t g = grp_g[i];
+  // chained partials: a group with no local member keeps the state it came
+  // with (copied to out_partial before the pipeline)
+  if (keep_empty && grp_t0[i] == grp_t1[i]) return;
   M st = M::init();
   int emit = 0;
   if (ns > 0)

@@ -8,7 +8,13 @@ all-gathered over RCCL (torch.distributed, backend "nccl"; "gloo" in CPU
 tests) and merged in rank order, which is series order, by
 otsdb_agg_finalize_device.  Median / percentiles across ranks run the
 otsdb_sel_* protocol instead: all-reduced contribution counts, then eight
-radix-select passes whose 256-bin histograms are all-reduced (exact).  Raw
+radix-select passes whose 256-bin histograms are all-reduced (exact).
+Order-sensitive aggregators (`dev`: StdDev.runDouble is one sequential
+Welford loop, Aggregators.java:547-568, whose result on offset data depends
+on its order at ~1e-11) hand their states on instead of merging them: rank 0
+reduces its members, each later rank continues from its predecessor's states
+(otsdb_agg_partials_chained_device, point-to-point in rank = series order),
+and the last rank's states are broadcast (hand_on_partials).  Raw
 (non-downsampled) queries, whose union-timestamp merge needs every member's
 points, run the groups spanning ranks as replicas over all-gathered member
 series (gather_shared_series).
@@ -16,6 +22,9 @@ series (gather_shared_series).
 import numpy as np
 
 PARTIAL_WORDS = 4  # otsdb_partial = 3 doubles + int64
+# aggregators whose partial states are handed on across ranks, not merged
+# (monoids.h kOrdered)
+ORDERED_AGGS = ("dev",)
 
 
 def shard_range(n_series, world, rank, offsets=None):
@@ -93,6 +102,55 @@ def all_gather_partials(partials, emit, group=None):
     dist.all_gather(gp, partials.contiguous(), group=group)
     dist.all_gather(ge, emit.contiguous(), group=group)
     return torch.stack(gp).to(dev), torch.stack(ge).to(dev)
+
+
+def hand_on_partials(local_step, partials, emit, group=None):
+    """The chained exchange of an order-sensitive aggregator's states.
+
+    local_step(init_p, init_e) fills `partials` [GB, 4] / `emit` [GB] with
+    this rank's states: from empty states on rank 0 (init None), from the
+    previous rank's output on every later one.  Rank r waits for rank r - 1
+    (a point-to-point send / recv in rank = series order), so the last
+    rank's states are those of ONE pass over every member; they are
+    broadcast and returned (the tensors passed in, overwritten) on every
+    rank.  The ranks run their downsampling in parallel; only the hand-offs
+    are sequential."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    staged = partials.device.type != "cpu" and _staged(group)
+
+    def peer(r):
+        return dist.get_global_rank(group, r) if group is not None else r
+
+    def xfer(op, t, r):
+        if staged:
+            h = t.cpu() if op is dist.send else t.new_empty(t.shape,
+                                                             device="cpu")
+            op(h, peer(r), group=group)
+            if op is dist.recv:
+                t.copy_(h)
+        else:
+            op(t.contiguous(), peer(r), group=group)
+
+    if rank == 0:
+        local_step(None, None)
+    else:
+        init_p, init_e = partials.clone(), emit.clone()
+        xfer(dist.recv, init_p, rank - 1)
+        xfer(dist.recv, init_e, rank - 1)
+        local_step(init_p, init_e)
+    if rank + 1 < world:
+        xfer(dist.send, partials, rank + 1)
+        xfer(dist.send, emit, rank + 1)
+    for t in (partials, emit):
+        if staged:
+            h = t.cpu()
+            dist.broadcast(h, peer(world - 1), group=group)
+            t.copy_(h)
+        else:
+            dist.broadcast(t, peer(world - 1), group=group)
+    return partials, emit
 
 
 def classify_groups(group_offsets, group=None, device=None):
@@ -191,6 +249,11 @@ def _host_slices(ids, res):
                      ii[offs[k]:offs[k + 1]]) for k, g in enumerate(ids)}
 
 
+def _agg_name(spec):
+    from . import core
+    return core.Aggregators.by_id(spec.agg_id).registry_name
+
+
 def run_sharded(engine, spec, dbatch, n_groups_global, torch_mod=None,
                 group=None, plan=None):
     """Runs one query over a rank's DeviceBatch whose group_offsets span all
@@ -228,14 +291,29 @@ def run_sharded(engine, spec, dbatch, n_groups_global, torch_mod=None,
         emit = torch.zeros(max(GB, 1), dtype=torch.uint8, device=dev)
         b = plan.shared_batch.as_abi()
         stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-        engine._check(engine.lib.otsdb_agg_partials_device(
-            engine.ctx, C.byref(spec), C.byref(b), parts.data_ptr(),
-            emit.data_ptr(), stream))
-        gp, ge = all_gather_partials(parts[:GB], emit[:GB], group)
+        if _agg_name(spec) in ORDERED_AGGS:
+            def step(init_p, init_e):
+                if init_p is None:
+                    engine._check(engine.lib.otsdb_agg_partials_device(
+                        engine.ctx, C.byref(spec), C.byref(b),
+                        parts.data_ptr(), emit.data_ptr(), stream))
+                else:
+                    engine._check(engine.lib.otsdb_agg_partials_chained_device(
+                        engine.ctx, C.byref(spec), C.byref(b),
+                        init_p.data_ptr(), init_e.data_ptr(),
+                        parts.data_ptr(), emit.data_ptr(), stream))
+            hand_on_partials(step, parts, emit, group)
+            gp, ge, n_ranks = parts[:GB], emit[:GB], 1
+        else:
+            engine._check(engine.lib.otsdb_agg_partials_device(
+                engine.ctx, C.byref(spec), C.byref(b), parts.data_ptr(),
+                emit.data_ptr(), stream))
+            gp, ge = all_gather_partials(parts[:GB], emit[:GB], group)
+            n_ranks = plan.world
         shared_res = DeviceResult(torch, n_sh, GB, dev)
         r = shared_res.as_abi()
         engine._check(engine.lib.otsdb_agg_finalize_device(
-            engine.ctx, C.byref(spec), n_sh, nb, plan.world,
+            engine.ctx, C.byref(spec), n_sh, nb, n_ranks,
             gp.contiguous().data_ptr(), ge.contiguous().data_ptr(),
             C.byref(r), stream))
     return ShardedResult(plan.local, plan.local_res, plan.shared, shared_res)

@@ -236,3 +236,79 @@ def test_raw_replica_gather_gloo_world2():
             assert np.array_equal(ts[offs[sg]:offs[sg + 1]], hb.ts[a:b])
             assert np.array_equal(val[offs[sg]:offs[sg + 1]], hb.val[a:b])
             assert np.array_equal(isf[offs[sg]:offs[sg + 1]], hb.is_float[a:b])
+
+
+def _welford_push(state, x):
+    """StdDev.runDouble's loop body (Aggregators.java:553-560) on an
+    (n, mean, M2) state."""
+    n, mean, m2 = state
+    if n == 0:
+        return (1, x, 0.0)
+    n += 1
+    nm = mean + (x - mean) / n
+    return (n, nm, m2 + (x - mean) * (x - nm))
+
+
+def _hand_on_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    GB = 5
+    # this rank's members' values per slot: offset data (~3e9 +- 1e4), where
+    # merging per-rank Welford states lands ~1e-11 from one pass
+    rng = np.random.default_rng(500 + rank)
+    vals = 3.0e9 + rng.random((GB, 40 + 7 * rank)) * 1e4
+    parts = torch.zeros((GB, 4), dtype=torch.int64)
+    emit = torch.zeros(GB, dtype=torch.uint8)
+
+    def step(init_p, init_e):
+        for k in range(GB):
+            if init_p is None:
+                st = (0, 0.0, 0.0)
+            else:
+                w = init_p[k].numpy()
+                st = (int(w[3]), float(w[0:1].view(np.float64)[0]),
+                      float(w[1:2].view(np.float64)[0]))
+            for x in vals[k]:
+                st = _welford_push(st, float(x))
+            parts[k, 0] = int(np.float64(st[1]).view(np.int64))
+            parts[k, 1] = int(np.float64(st[2]).view(np.int64))
+            parts[k, 3] = st[0]
+            emit[k] = 1
+    odist.hand_on_partials(step, parts, emit)
+    q.put((rank, parts.numpy().copy(), emit.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_hand_on_partials_gloo_world3():
+    """The chained exchange of dev states (dist.hand_on_partials): rank r
+    continues rank r - 1's Welford states, so every rank ends with exactly
+    the state of ONE sequential pass over all ranks' members in rank order —
+    bit for bit, where a merge of per-rank states misses it."""
+    world = 3
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_hand_on_worker, args=(r, world, port, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict((r, (pp, ee)) for r, pp, ee in (q.get(timeout=120)
+                                              for _ in range(world)))
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for r in range(1, world):  # broadcast: every rank holds the last's states
+        assert np.array_equal(got[r][0], got[0][0])
+    vals = [3.0e9 + np.random.default_rng(500 + r).random((5, 40 + 7 * r)) * 1e4
+            for r in range(world)]
+    for k in range(5):
+        st = (0, 0.0, 0.0)
+        for r in range(world):
+            for x in vals[r][k]:
+                st = _welford_push(st, float(x))
+        w = got[0][0][k]
+        assert int(w[3]) == st[0]
+        assert w[0] == np.float64(st[1]).view(np.int64)
+        assert w[1] == np.float64(st[2]).view(np.int64)

@@ -1,0 +1,148 @@
+"""Cross-series `dev` over large groups and across ranks (Needs an MI355X).
+
+StdDev.runDouble (src/core/Aggregators.java:547-568) is ONE sequential
+Welford loop over a group's members at each timestamp, in SpanCmp order
+(AggregationIterator.java:735-797).  The engine reproduces that loop bit for
+bit while a group is one chain — fold tiles of 256 members, the row path's
+k_group up to 65,536 members — and across ranks by handing the chain's
+states on (otsdb_agg_partials_chained_device, dist.hand_on_partials).  A
+group past 65,536 members on one GPU (C4: 500k counters) merges 256-member
+chunk states in order with Chan's formula: a 500k-step chain costs ~50 ms
+(tools/chain_probe.hip: 69 ns a step with no memory traffic at all), and on
+well-conditioned contributions — C4's rates, |mean| / sigma of a few — that
+merge stays far inside 1e-12 of the one loop.  Everything here is compared
+at the pure 1e-12 relative bound or bit for bit, with NO absolute floor.
+"""
+import numpy as np
+import pytest
+
+from opentsdb_amd import abi, core, dist as odist, workload
+from oracle import pyoracle
+from tests import datasets
+from tests.test_gpu_parity import _spec, compare
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from opentsdb_amd.engine import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def test_c4_query_over_all_500k_series(engine):
+    """C4's own query and shape — `dev:1m-sum:rate{counter,LONG_MAX,1e6}`
+    over ONE group of all 500,000 generator series (the bench's generator,
+    on the device) — with the window cut to 1 h so the oracle finishes: 60
+    buckets, each the merge of 1,953 chunk states (two-level combine), at
+    the pure 1e-12 bound (the rates are exact: sums of longs, one division)."""
+    import torch
+    from opentsdb_amd.engine import DeviceResult, run_device
+    from opentsdb_amd.batch import HostBatch
+    from tests.test_gpu_fullsize import _result_groups
+    n = workload.default_series_per_gpu("C4")
+    assert n == 500000
+    g = abi.GenSpec(42, workload.T0_S * 1000, 3600 * 1000, 10000, 2, 0)
+    db = workload.generate_device(engine, g, 0, n, config="C4")
+    assert db.n_groups == 1
+    c = workload.CONFIGS["C4"]
+    t0 = workload.T0_S * 1000
+    spec = core.make_spec(t0, t0 + 3600 * 1000 - 1000,
+                          core.Aggregators.get("dev"),
+                          core.DownsamplingSpecification(c["ds"]), t0,
+                          t0 + 3600 * 1000 - 1000, True,
+                          core.RateOptions(*c["rate"]))
+    sz = engine.plan(spec, db)
+    res = DeviceResult(torch, 1, int(sz.max_out_points), "cuda")
+    run_device(engine, spec, db, res)
+    torch.cuda.synchronize()
+    got = _result_groups(res, [0])
+    hb = HostBatch(db.offsets.cpu().numpy(), db.ts.cpu().numpy(),
+                   db.val.cpu().numpy(), None, db.series_float.cpu().numpy(),
+                   np.array([0, n], np.int64), np.arange(n, dtype=np.int64))
+    del db
+    ref = pyoracle.group_by(spec, hb)
+    assert len(ref[0]) >= 55
+    compare(got, ref, False, where="C4-500k-dev", floor=0.0)
+
+
+@pytest.mark.parametrize("ds", ["max", "first", "min"])
+def test_dev_offset_gauge_20000_members(engine, ds):
+    """20,000 gauges of ~3e9 +- 1e4 in one group: the reference's own loop
+    lies ~1e-11 from the exact sigma here (tests/test_dev_conditioning_cpu.py),
+    so only its order meets 1e-12 — one row-path chain per bucket, compared
+    bit for bit."""
+    b = datasets.random_batch(20000, n_series=20000, big_group=True,
+                              span_ms=3600 * 1000, cadence_ms=30000,
+                              value_kind="offset")
+    for fill in ("none", "nan"):
+        spec = _spec("dev", ds, fill, end=datasets.T0 + 3600 * 1000)
+        ref = pyoracle.group_by(spec, b)
+        got = engine.run(spec, b)
+        compare(got, ref, True, where="dev20k/%s/%s" % (ds, fill))
+
+
+def _chained_emulated(engines, spec, hb, world):
+    """dist.hand_on_partials with the ranks run one after another in this
+    process: rank 0's partials, each later rank's continued from the
+    previous output, the last one finalised."""
+    import ctypes as C
+    import torch
+    from opentsdb_amd.engine import DeviceResult
+    from tests.test_gpu_sharded import _host
+    G = hb.n_groups
+    e = engines[0]
+    prev = None
+    for r in range(world):
+        db = odist.to_device(odist.shard_host_batch(hb, world, r))
+        nb = int(e.plan(spec, db).n_buckets)
+        GB = max(G * nb, 1)
+        p = torch.zeros((GB, 4), dtype=torch.int64, device="cuda")
+        m = torch.zeros(GB, dtype=torch.uint8, device="cuda")
+        b = db.as_abi()
+        if prev is None:
+            e._check(e.lib.otsdb_agg_partials_device(
+                e.ctx, C.byref(spec), C.byref(b), p.data_ptr(), m.data_ptr(),
+                None))
+        else:
+            e._check(e.lib.otsdb_agg_partials_chained_device(
+                e.ctx, C.byref(spec), C.byref(b), prev[0].data_ptr(),
+                prev[1].data_ptr(), p.data_ptr(), m.data_ptr(), None))
+        prev = (p, m)
+    res = DeviceResult(torch, G, max(G * nb, 1), "cuda")
+    r = res.as_abi()
+    e._check(e.lib.otsdb_agg_finalize_device(
+        e.ctx, C.byref(spec), G, nb, 1, prev[0].data_ptr(), prev[1].data_ptr(),
+        C.byref(r), None))
+    torch.cuda.synchronize()
+    return _host(res, G)
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_dev_offset_across_ranks_chained(engine, world):
+    """Offset gauges (~3e9 +- 1e4) sharded over 2, 3 and 5 ranks: a 3,000-
+    series group cut by every shard boundary, and six 10-series groups on
+    rank 0 only; the chained partials continue each group's loop across
+    the ranks — bit-exact, where the rank-merged partials
+    (_partials_emulated, Chan's formula) land ~1e-11 away."""
+    from tests.test_gpu_sharded import _partials_emulated
+    hb = datasets.random_batch(7100 + world, n_series=3000, n_groups=7,
+                               span_ms=3600 * 1000, cadence_ms=30000,
+                               value_kind="offset")
+    gid = np.minimum(np.arange(3000) // 10, 6)  # groups 0-5: 10 series each
+    from opentsdb_amd.batch import groups_from_ids
+    hb.group_offsets, hb.group_members = groups_from_ids(gid, 7)
+    for ds, fill in (("max", "none"), ("first", "nan")):
+        spec = _spec("dev", ds, fill, end=datasets.T0 + 3600 * 1000)
+        ref = pyoracle.group_by(spec, hb)
+        got = _chained_emulated([engine], spec, hb, world)
+        compare(got, ref, True, where="chain-w%d/%s/%s" % (world, ds, fill))
+    # the merge of per-rank states misses the one loop on this data (why the
+    # states are handed on)
+    spec = _spec("dev", "max", "none", end=datasets.T0 + 3600 * 1000)
+    ref = pyoracle.group_by(spec, hb)
+    merged = _partials_emulated([engine], spec, hb, world)
+    with pytest.raises(AssertionError):
+        compare(merged[6:], ref[6:], False, where="merged", floor=0.0)
