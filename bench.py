@@ -196,6 +196,8 @@ def named_query_figure(eng, db, config, warm=3, reps=10):
            # scripts/gpu_pmc.sh with bench.py --named-query
            "traffic": pmc_traffic(config + "_named")}
     out["frac"] = out["achieved_GBs"] / HBM_PEAK_GBS if kf else None
+    # over the whole query (median step), like the headline's frac
+    out["step_frac"] = BYTES_PER_POINT * n / med / 1e9 / HBM_PEAK_GBS
     del res
     return out
 
@@ -562,10 +564,10 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    read = stage_reader(eng)
-    eng.lib.otsdb_prof_enable(eng.ctx, 1)
-    read()  # reset
 
+    # the timed steps run with stage timing OFF (no HIP events in the
+    # pipeline); the per-stage kernel times come from a separate profiled
+    # pass over the same steps afterwards
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -579,6 +581,13 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+
+    read = stage_reader(eng)
+    eng.lib.otsdb_prof_enable(eng.ctx, 1)
+    read()  # reset
+    for _ in range(max(1, min(args.steps, 10))):
+        step()
+    torch.cuda.synchronize()
     stage_ms = read()
     eng.lib.otsdb_prof_enable(eng.ctx, 0)
 
@@ -605,7 +614,12 @@ def main():
     # compact), with the downsample stage alone beside it
     row_path = bool(cfg["rate"]) or cfg["agg"] in ("p99", "p999", "median")
     kb_s = (sum(stage_ms[:5]) if row_path else stage_ms[0]) / 1e3
-    achieved = BYTES_PER_POINT * n_points / kb_s / 1e9 if kb_s > 0 else None
+    kernel_achieved = (BYTES_PER_POINT * n_points / kb_s / 1e9
+                       if kb_s > 0 else None)
+    # the headline fraction: algorithmic bytes over the driver-timed step
+    # (the whole query: every kernel, launch gaps and the read-back); the
+    # dominant kernel's own HIP-event time is the secondary figure
+    achieved = BYTES_PER_POINT * n_points / step_s / 1e9
     kernel = ("k_fold" if not row_path else
               "pipeline: k_prep + k_bucketize_k (rate-fused) + k_transform + "
               "k_group<MDev> + k_compact"
@@ -681,8 +695,13 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                "timed_over": "ms_per_step (the whole query, per GPU)",
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": BYTES_PER_POINT * n_points,
+                "kernel_ms": kb_s * 1e3,
+                "kernel_achieved": kernel_achieved,
+                "kernel_frac": (kernel_achieved / HBM_PEAK_GBS
+                                if kernel_achieved else None),
             },
             "cpu_baseline": extra.get("cpu_baseline"),
         }

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OTSDB_ABI_VERSION 3
+#define OTSDB_ABI_VERSION 4
 
 /* ------------------------------------------------------------------------ */
 /* Status codes — 1:1 with the exceptions of the reference path.             */
@@ -209,6 +209,11 @@ typedef struct {
   int64_t n_groups;             /* G                                       */
   const int64_t* group_offsets; /* [G+1] CSR into group_members            */
   const int64_t* group_members; /* [M] series indices, SpanCmp order       */
+  /* Optional HOST copy of group_offsets (the same G+1 values) for the
+   * device entries: the engine plans its tiles from it instead of reading
+   * group_offsets back from the device (one copy + stream sync per call).
+   * NULL = read it back.  Ignored by the host entries.                    */
+  const int64_t* group_offsets_host;
 } otsdb_batch;
 
 /* ------------------------------------------------------------------------ */

@@ -62,6 +62,7 @@ class Batch(C.Structure):
         ("n_groups", C.c_int64),
         ("group_offsets", C.c_void_p),
         ("group_members", C.c_void_p),
+        ("group_offsets_host", C.c_void_p),
     ]
 
 

@@ -217,6 +217,17 @@ struct otsdb_ctx {
   size_t raw_cells_cap[2] = {0, 0};          // then the assembled spans
   void* raw_stage = nullptr;  // otsdb_agg_run_raw: host rows staged in HBM
   size_t raw_stage_cap = 0;
+  // single-pass compaction (k_compact1): per-group look-back granules and
+  // the call's epoch; {error word, total} read back in one copy
+  void* cmp_flags = nullptr;
+  size_t cmp_flags_cap = 0;
+  uint32_t cmp_epoch = 0;
+  // the device error word is known to be zero (the last call ended with the
+  // one-pass compaction, which zeroes it): the next pipeline skips its
+  // memset.  clean_entry: that mark as the current call found it (CtxLock)
+  bool err_clean = false;
+  bool clean_entry = false;
+  bool small_ready = false;  // k_compact1 wrote {error word, total}
   // cross-rank selection session (otsdb_sel_*): lives in `ws` between calls
   struct {
     bool active = false;
@@ -242,6 +253,18 @@ otsdb_status ensure(void** p, size_t* cap, size_t need) {
   *cap = n;
   return OTSDB_OK;
 }
+
+// One call at a time per context.  Also takes the "error word known zero"
+// mark for this call (clean_entry) and clears it: only the one-pass
+// compaction's read-back (finish) sets it again, after k_compact1 zeroed
+// the word — any other call may leave bits in it.
+struct CtxLock {
+  std::lock_guard<std::mutex> lk;
+  explicit CtxLock(otsdb_ctx* c) : lk(c->mu) {
+    c->clean_entry = c->err_clean;
+    c->err_clean = false;
+  }
+};
 
 // Binds a caller's stream to the context for one call and restores the
 // context's own stream on every exit path (early HIP_TRY returns included).
@@ -921,8 +944,17 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   if (rc) return rc;
   carve((char*)c->ws);
 
-  HIP_TRY(hipMemsetAsync(c->d_err, 0, 2 * sizeof(int), st));  // + cells "wide"
-  if (G * NB > 0 && mode != 1)
+  // the error word (+ the cells fold's "wide" word): zero already when the
+  // previous call ended in the one-pass compaction
+  if (cells || mode != 0 || !c->clean_entry)
+    HIP_TRY(hipMemsetAsync(c->d_err, 0, 2 * sizeof(int), st));
+  c->clean_entry = false;
+  // every (group, bucket) emit flag is written by the fold / k_group /
+  // k_combine of a group with members; only empty groups need the zeroes
+  bool empty_group = false;
+  for (int64_t g = 0; g < G && !empty_group; ++g)
+    empty_group = goff[g + 1] == goff[g];
+  if (G * NB > 0 && mode != 1 && empty_group)
     HIP_TRY(hipMemsetAsync(W.out_emit, 0, (size_t)G * NB, st));
   // the ring-sink k_bucketize leaves sentinel rows whose states k_transform
   // writes; the cells and selection downsamplers store states into a
@@ -1178,28 +1210,46 @@ otsdb_status compact(otsdb_ctx* c, const Params& P, int64_t G,
     return OTSDB_OK;
   }
   StageTimer tm(c, 4);
-  hipLaunchKernelGGL(k_compact, dim3(blocks_for(G, 4)), dim3(256), 0, st, P,
-                     G, out_val, out_emit, counts, (const int64_t*)nullptr,
-                     (int64_t)0, (int64_t*)nullptr, (int64_t*)nullptr,
-                     (uint8_t*)nullptr, 0);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, G,
-                     (const int64_t*)counts, out->offsets);
-  hipLaunchKernelGGL(k_compact, dim3(blocks_for(G, 4)), dim3(256), 0, st, P,
-                     G, out_val, out_emit, counts,
-                     (const int64_t*)out->offsets, out->capacity, out->ts,
-                     out->val, out->is_int, 1);
+  // one pass (k_compact1): count, look-back scan, scatter, and the call's
+  // {error word, total} for finish's single read-back
+  void* p = c->cmp_flags;
+  size_t cap = c->cmp_flags_cap;
+  const bool grow = (size_t)G * 8 > cap;
+  otsdb_status rc = ensure(&p, &cap, (size_t)G * 8);
+  c->cmp_flags = p;
+  c->cmp_flags_cap = cap;
+  if (rc) return rc;
+  if (grow) HIP_TRY(hipMemsetAsync(p, 0, cap, st));  // no stale epochs
+  c->cmp_epoch = (c->cmp_epoch + 1) & 0xFFFFFF;
+  if (c->cmp_epoch == 0) c->cmp_epoch = 1;
+  unsigned long long* ticket = (unsigned long long*)((char*)c->d_err + 192);
+  int64_t* small = (int64_t*)((char*)c->d_err + 128);
+  hipLaunchKernelGGL(k_compact1, dim3(blocks_for(G, 4)), dim3(256), 0, st, P,
+                     G, out_val, out_emit, (unsigned long long*)p, ticket,
+                     c->cmp_epoch, out->offsets, out->capacity, out->ts,
+                     out->val, out->is_int, c->d_err, small);
   HIP_TRY(hipGetLastError());
+  c->small_ready = true;
   return OTSDB_OK;
 }
 
 // reads the error word and the total point count; maps to a status
 otsdb_status finish(otsdb_ctx* c, int64_t G, otsdb_result* out) {
   hipStream_t st = c->stream;
-  HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
-                         hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipMemcpyAsync(&c->h_small[1], out->offsets + G, sizeof(int64_t),
-                         hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
+  if (c->small_ready) {
+    // k_compact1 left {error word, total} side by side and zeroed the word
+    c->small_ready = false;
+    HIP_TRY(hipMemcpyAsync(&c->h_small[0], (char*)c->d_err + 128,
+                           2 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    c->err_clean = true;
+  } else {
+    HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&c->h_small[1], out->offsets + G, sizeof(int64_t),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
   const int err = (int)(c->h_small[0] & 0xFFFFFFFF);
   const int64_t total = c->h_small[1];
   if (err & ERR_NONE_MULTI)
@@ -1249,7 +1299,10 @@ otsdb_status read_goff(otsdb_ctx* c, const otsdb_batch* b, bool device,
   goff.resize(b->n_groups + 1);
   if (b->n_groups < 0) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "n_groups < 0");
   if (!b->group_offsets) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "no groups");
-  if (device) {
+  if (device && b->group_offsets_host) {
+    // the caller's host copy of the same offsets: no read-back, no sync
+    memcpy(goff.data(), b->group_offsets_host, sizeof(int64_t) * goff.size());
+  } else if (device) {
     HIP_TRY(hipMemcpyAsync(goff.data(), b->group_offsets,
                            sizeof(int64_t) * goff.size(),
                            hipMemcpyDeviceToHost, c->stream));
@@ -2349,6 +2402,7 @@ otsdb_status otsdb_ctx_create(int device, otsdb_ctx** out) {
   // so tensors torch writes are complete before this context reads them
   HIP_TRY(hipStreamCreate(&c->stream));
   HIP_TRY(hipMalloc(&c->d_err, 256));
+  HIP_TRY(hipMemset(c->d_err, 0, 256));
   c->d_mm = (unsigned long long*)((char*)c->d_err + 64);
   HIP_TRY(hipHostMalloc(&c->h_small, 64));
   *out = c;
@@ -2375,6 +2429,7 @@ void otsdb_ctx_destroy(otsdb_ctx* c) {
     if (p) hipFree(p);
   if (c->raw_stage) hipFree(c->raw_stage);
   if (c->d_tiles) hipFree(c->d_tiles);
+  if (c->cmp_flags) hipFree(c->cmp_flags);
   if (c->d_err) hipFree(c->d_err);
   for (auto e : c->ev_pool) hipEventDestroy(e);
   if (c->h_small) hipHostFree(c->h_small);
@@ -2435,7 +2490,7 @@ otsdb_status otsdb_agg_run_device(otsdb_ctx* c, const otsdb_query_spec* spec,
                                   const otsdb_batch* b, otsdb_result* out,
                                   void* hip_stream) {
   if (!c || !spec || !b || !out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_TRY(hipSetDevice(c->device));
   StreamBinding bind(c, hip_stream);
   std::vector<int64_t> goff;
@@ -2451,7 +2506,7 @@ otsdb_status otsdb_agg_run_cells_device(otsdb_ctx* c,
                                         otsdb_result* out, void* hip_stream) {
   if (!c || !spec || !cells || !b || !out)
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_TRY(hipSetDevice(c->device));
   StreamBinding bind(c, hip_stream);
   std::vector<int64_t> goff;
@@ -2463,7 +2518,7 @@ otsdb_status otsdb_agg_run_cells_device(otsdb_ctx* c,
 otsdb_status otsdb_agg_run(otsdb_ctx* c, const otsdb_query_spec* spec,
                            const otsdb_batch* b, otsdb_result* out) {
   if (!c || !spec || !b || !out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_TRY(hipSetDevice(c->device));
   std::vector<int64_t> goff;
   otsdb_status rc = read_goff(c, b, false, goff);
@@ -2550,7 +2605,7 @@ otsdb_status partials_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
                            uint8_t* emit, void* hip_stream) {
   if (!c || !spec || !b || !partials || !emit || (!init != !init_emit))
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_TRY(hipSetDevice(c->device));
   StreamBinding bind(c, hip_stream);
   std::vector<int64_t> goff;
@@ -2627,7 +2682,7 @@ otsdb_status otsdb_agg_finalize_device(otsdb_ctx* c,
                                        const uint8_t* emit, otsdb_result* out,
                                        void* hip_stream) {
   if (!c || !spec || !out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_TRY(hipSetDevice(c->device));
   StreamBinding bind(c, hip_stream);
   otsdb_status rc = check_spec(spec);
@@ -2675,7 +2730,7 @@ otsdb_status otsdb_sel_prepare_device(otsdb_ctx* c, const otsdb_query_spec* spec
                                       uint8_t* emit, void* hip_stream) {
   if (!c || !spec || !b || !counts || !emit)
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_TRY(hipSetDevice(c->device));
   c->sel.active = false;
   StreamBinding bind(c, hip_stream);
@@ -2730,7 +2785,7 @@ otsdb_status otsdb_sel_hist_device(otsdb_ctx* c, int32_t pass,
                                    uint32_t* hist_prev, uint32_t* hist_out,
                                    void* hip_stream) {
   if (!c || !hist_out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   if (!c->sel.active) return fail(OTSDB_E_ILLEGAL_STATE, "no selection session");
   if (pass < 0 || pass > 7) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "pass %d", pass);
   HIP_TRY(hipSetDevice(c->device));
@@ -2778,7 +2833,7 @@ otsdb_status otsdb_sel_hist_wait(otsdb_ctx* c, void* hip_stream) {
 otsdb_status otsdb_sel_finish_device(otsdb_ctx* c, uint32_t* hist_last,
                                      otsdb_result* out, void* hip_stream) {
   if (!c || !hist_last || !out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   if (!c->sel.active) return fail(OTSDB_E_ILLEGAL_STATE, "no selection session");
   HIP_TRY(hipSetDevice(c->device));
   StreamBinding bind(c, hip_stream);
@@ -2808,7 +2863,7 @@ otsdb_status otsdb_decode_cells_device(otsdb_ctx* c, const otsdb_cells* cells,
   if (!c || !cells || !offsets) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
   if (ts_ms && (!val || !is_float))
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null output column");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   return decode_impl(c, cells, n_series, offsets, ts_ms, val, is_float,
@@ -2825,7 +2880,7 @@ otsdb_status otsdb_encode_cells_device(otsdb_ctx* c, const otsdb_batch* b,
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
   if (b->is_float)
     return fail(OTSDB_E_UNSUPPORTED, "per-point value types: use series_float");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   const int64_t S = b->n_series;
@@ -2848,7 +2903,7 @@ otsdb_status otsdb_compact_rows_device(otsdb_ctx* c, const otsdb_raw_rows* raw,
                                        int64_t val_capacity, int64_t* n_out_rows,
                                        void* hip_stream) {
   if (!c || !raw || !n_out_rows) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   return compact_impl(c, raw, fix_duplicates != 0, out, qual_capacity,
@@ -2864,7 +2919,7 @@ otsdb_status otsdb_span_assemble_device(otsdb_ctx* c, const otsdb_cells* cells,
   if (!c || !cells || !n_out_rows) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
   if (out && !out->row_series)
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null output row_series");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   bool identity = true;
@@ -2879,7 +2934,7 @@ otsdb_status otsdb_agg_run_raw_device(otsdb_ctx* c, const otsdb_query_spec* spec
                                       void* hip_stream) {
   if (!c || !spec || !raw || !b || !out)
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_TRY(hipSetDevice(c->device));
   StreamBinding bind(c, hip_stream);
   std::vector<int64_t> goff;
@@ -2894,7 +2949,7 @@ otsdb_status otsdb_agg_run_raw(otsdb_ctx* c, const otsdb_query_spec* spec,
                                const otsdb_batch* b, otsdb_result* out) {
   if (!c || !spec || !raw || !b || !out)
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_TRY(hipSetDevice(c->device));
   otsdb_status rc = check_spec(spec);
   if (rc) return rc;
@@ -3002,7 +3057,7 @@ otsdb_status otsdb_agg_run_cells(otsdb_ctx* c, const otsdb_query_spec* spec,
                                  otsdb_result* out) {
   if (!c || !spec || !cells || !b || !out)
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_TRY(hipSetDevice(c->device));
   otsdb_status rc = check_spec(spec);
   if (rc) return rc;
@@ -3110,7 +3165,7 @@ otsdb_status otsdb_agg_run_cells(otsdb_ctx* c, const otsdb_query_spec* spec,
 
 otsdb_status otsdb_prof_enable(otsdb_ctx* c, int enable) {
   if (!c) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   c->prof = enable != 0;
   return OTSDB_OK;
 }
@@ -3118,7 +3173,7 @@ otsdb_status otsdb_prof_enable(otsdb_ctx* c, int enable) {
 otsdb_status otsdb_prof_read(otsdb_ctx* c, double* ms, int64_t* launches,
                              int n, int reset) {
   if (!c) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
-  std::lock_guard<std::mutex> lk(c->mu);
+  CtxLock lk(c);
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   for (auto& p : c->ev_pending) {

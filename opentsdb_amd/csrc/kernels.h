@@ -14,7 +14,7 @@
 //   k_group       one thread per (series chunk, bucket): the cross-series
 //                 aggregator, sequential in SpanCmp order inside a chunk
 //   k_combine     merges chunk partials in order, finalises, flags Infinity
-//   k_compact     per group: emitted buckets -> (ts, value) arrays
+//   k_compact1    per group: emitted buckets -> (ts, value) arrays (one pass)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -1772,43 +1772,129 @@ __global__ __launch_bounds__(SEL_THREADS) void k_group_select(
 }
 
 // ------------------------------------------------------------------------
-// k_compact: dense (group, bucket) results -> per-group (ts, value) arrays.
-// One wavefront per group.  mode 0 counts (16 emit flags a lane per load:
-// 1,024 buckets a pass), mode 1 scatters (8 runs of 64 buckets a pass, their
-// loads issued together: the loop is latency-bound, not byte-bound).
+// k_compact1: dense (group, bucket) results -> per-group (ts, value) arrays
+// in ONE pass (count, exclusive scan across groups, scatter), the scan by
+// decoupled look-back.  One wavefront per
+// group, groups taken in ticket order (a block's logical index is an atomic
+// ticket, so every group it waits for belongs to a block that has already
+// started: no dependence on dispatch order or co-residency beyond that).  Each wave publishes its
+// group's count as an 8-byte granule {epoch:24, status:2, value:38} — the
+// data is the flag (status 1 = this group's count, 2 = the inclusive
+// prefix) — reads up to 64 predecessors' granules at once, sums back to the
+// nearest inclusive one, publishes its own inclusive prefix and scatters.
+// The epoch (per call, never 0) retires the previous call's granules
+// without a memset; the last group also writes offsets[G] and the call's
+// {error word, total points} pair for one read-back, and zeroes the error
+// word for the next call (the engine's memset of it is skipped then).
 // ------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_compact(
+constexpr int kCmpStatusShift = 38;
+constexpr int kCmpEpochShift = 40;
+constexpr uint64_t kCmpValueMask = (1ULL << kCmpStatusShift) - 1;
+
+DEV int compact_count(const uint8_t* __restrict__ em, int64_t nb, int lane) {
+  int n = 0;
+  for (int64_t c0 = 0; c0 < nb; c0 += 1024) {
+    const int64_t b = c0 + 16 * lane;
+    if (b + 16 <= nb) {
+      uint4 x;  // (rows of nb bytes: any alignment)
+      __builtin_memcpy(&x, em + b, 16);
+      auto nz = [](uint32_t w) {
+        return __builtin_popcount((((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) &
+                                  0x80808080u);
+      };
+      n += nz(x.x) + nz(x.y) + nz(x.z) + nz(x.w);
+    } else {
+      for (int64_t i = b; i < nb && i < b + 16; ++i) n += em[i] ? 1 : 0;
+    }
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) n += __shfl_xor(n, d);
+  return n;
+}
+
+__global__ __launch_bounds__(256) void k_compact1(
     Params P, int64_t G, const double* __restrict__ out_val,
-    const uint8_t* __restrict__ out_emit, int64_t* __restrict__ counts,
-    const int64_t* __restrict__ offsets, int64_t cap, int64_t* __restrict__ r_ts,
-    int64_t* __restrict__ r_val, uint8_t* __restrict__ r_isint, int mode) {
-  const int lane = LANE;
-  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint8_t* __restrict__ out_emit, unsigned long long* __restrict__ flags,
+    unsigned long long* __restrict__ ticket, uint32_t epoch,
+    int64_t* __restrict__ offsets, int64_t cap,
+    int64_t* __restrict__ r_ts, int64_t* __restrict__ r_val,
+    uint8_t* __restrict__ r_isint, int* err_word, int64_t* __restrict__ small) {
+  __shared__ unsigned long long s_blk;
+  const int lane = LANE, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    // the ticket word {epoch:32, count:32} restarts at each call's first
+    // ticket (no memset)
+    unsigned long long old = __hip_atomic_load(ticket, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      const bool same = (old >> 32) == epoch;
+      const unsigned long long want =
+          same ? old + 1 : (((unsigned long long)epoch << 32) | 1ULL);
+      if (__hip_atomic_compare_exchange_strong(
+              ticket, &old, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+              __HIP_MEMORY_SCOPE_AGENT)) {
+        s_blk = same ? (old & 0xFFFFFFFFULL) : 0;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t g = (int64_t)s_blk * 4 + w;
   if (g >= G) return;
   const int64_t nb = P.nb;
   const uint8_t* em = out_emit + g * nb;
-  if (!mode) {
-    int64_t n = 0;
-    for (int64_t c0 = 0; c0 < nb; c0 += 1024) {
-      const int64_t b = c0 + 16 * lane;
-      if (b + 16 <= nb) {
-        const uint4 x = *reinterpret_cast<const uint4*>(em + b);
-        // non-zero bytes: the high bit of ((byte & 0x7F) + 0x7F) | byte
-        auto nz = [](uint32_t w) {
-          return __builtin_popcount((((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u);
-        };
-        n += nz(x.x) + nz(x.y) + nz(x.z) + nz(x.w);
-      } else {
-        for (int64_t i = b; i < nb && i < b + 16; ++i) n += em[i] ? 1 : 0;
+  const int64_t n = compact_count(em, nb, lane);
+  const uint64_t tag = (uint64_t)epoch << kCmpEpochShift;
+  if (lane == 0)
+    __hip_atomic_store(&flags[g], tag | (1ULL << kCmpStatusShift) | (uint64_t)n,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // look back: lane l reads group j - l; sum every published count down to
+  // (and including) the nearest inclusive prefix
+  int64_t prefix = 0;
+  int64_t j = g - 1;
+  unsigned spins = 0;
+  while (j >= 0) {
+    const int64_t k = j - lane;
+    uint64_t v = 0;
+    if (k >= 0)
+      v = __hip_atomic_load(&flags[k], __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
+    const bool cur = k < 0 || (v >> kCmpEpochShift) == epoch;
+    const uint32_t st = k < 0 ? 2u : (uint32_t)((v >> kCmpStatusShift) & 3);
+    const uint64_t incl = __ballot(cur && st == 2);
+    const int stop = incl ? __builtin_ctzll(incl) : 64;  // nearest inclusive
+    const uint64_t upto = stop == 64 ? ~0ULL : ((2ULL << stop) - 1);
+    if (__ballot(!cur) & upto) {  // a predecessor not published yet
+      if (++spins > (1u << 22)) {  // (bounded: never expected)
+        if (lane == 0) atomicOr(err_word, ERR_INTERNAL);
+        break;
       }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
     }
+    int64_t x = (k >= 0 && (uint64_t)lane <= (uint64_t)stop)
+                    ? (int64_t)(v & kCmpValueMask) : 0;
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) n += __shfl_xor(n, d);
-    if (lane == 0) counts[g] = n;
-    return;
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+    prefix += x;
+    if (stop < 64) break;
+    j -= 64;
+  }
+  if (lane == 0) {
+    __hip_atomic_store(&flags[g],
+                       tag | (2ULL << kCmpStatusShift) | (uint64_t)(prefix + n),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    offsets[g] = prefix;
+    if (g == G - 1) {
+      offsets[G] = prefix + n;
+      small[1] = prefix + n;
+      // every kernel that reports into the error word ran before this one
+      small[0] = (int64_t)(uint32_t)__hip_atomic_exchange(
+          err_word, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   constexpr int U = 8;
-  int64_t pos = offsets[g];
+  int64_t pos = prefix;
   for (int64_t c0 = 0; c0 < nb; c0 += 64 * U) {
     bool e[U];
     double v[U];

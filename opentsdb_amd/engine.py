@@ -180,7 +180,19 @@ class DeviceBatch:
         b.n_groups = self.n_groups
         b.group_offsets = p(self.group_offsets)
         b.group_members = p(self.group_members)
+        b.group_offsets_host = self._goff_host().ctypes.data
         return b
+
+    def _goff_host(self):
+        """A host copy of group_offsets for otsdb_batch.group_offsets_host
+        (re-read when the tensor is replaced or written in place)."""
+        t = self.group_offsets
+        key = (id(t), t.data_ptr(), t.numel(), t._version)
+        c = getattr(self, "_goff_cache", None)
+        if c is None or c[0] != key:
+            c = (key, np.ascontiguousarray(t.cpu().numpy(), np.int64))
+            self._goff_cache = c
+        return c[1]
 
 
 class DeviceResult:

@@ -37,13 +37,13 @@ def test_library_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.otsdb_abi_version() == 3
+    assert lib.otsdb_abi_version() == 4
 
 
 def test_struct_sizes_match_header():
     assert C.sizeof(abi.QuerySpec) == (4 * 8 + 4 * 2 + 8 + 4 * 8 + 8 * 2 + 8 * 2
                                        + 8 * 3)  # calendar anchors
-    assert C.sizeof(abi.Batch) == 10 * 8
+    assert C.sizeof(abi.Batch) == 11 * 8  # + group_offsets_host (ABI 4)
     assert C.sizeof(abi.Result) == 5 * 8
     assert C.sizeof(abi.Partial) == 32
 
