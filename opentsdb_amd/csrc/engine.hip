@@ -1220,8 +1220,9 @@ otsdb_status compact(otsdb_ctx* c, const Params& P, int64_t G,
   c->cmp_flags_cap = cap;
   if (rc) return rc;
   if (grow) HIP_TRY(hipMemsetAsync(p, 0, cap, st));  // no stale epochs
-  c->cmp_epoch = (c->cmp_epoch + 1) & 0xFFFFFF;
-  if (c->cmp_epoch == 0) c->cmp_epoch = 1;
+  // epochs 1, 2, ..., 2^24 - 1, then 4, 5, ...: never 0 (fresh granules)
+  // and always one ticket slot on from the last call's (k_compact1)
+  c->cmp_epoch = c->cmp_epoch + 1 == (1u << 24) ? 4u : c->cmp_epoch + 1;
   unsigned long long* ticket = (unsigned long long*)((char*)c->d_err + 192);
   int64_t* small = (int64_t*)((char*)c->d_err + 128);
   hipLaunchKernelGGL(k_compact1, dim3(blocks_for(G, 4)), dim3(256), 0, st, P,

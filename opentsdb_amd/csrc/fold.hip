@@ -97,12 +97,23 @@ __global__ __launch_bounds__(256) void k_fold_prep(Params P, BatchDev B,
   const int64_t p = lower_bound_interp(B.ts, lo, hi, bucket_ts(P, j * WB));
   c.bnd = p;
   int err = 0;
+  // the buckets either side, reduced in point order; points are read 8 at a
+  // time (all eight loads in flight before the pushes: the loop was a
+  // dependent load per point, most of this latency-bound kernel's time)
+  constexpr int C8 = 8;
   if (p > lo) {
     const int64_t k = bucket_of(P, B.ts[p - 1]);
     const int64_t bt = bucket_ts(P, k);
     const int64_t q = lower_bound_interp(B.ts, lo, p, bt);
     M st = M::init();
-    for (int64_t i = q; i < p; ++i) st.push(point_value(B, i, B.val[i], sf));
+    for (int64_t i0 = q; i0 < p; i0 += C8) {
+      int64_t v[C8];
+#pragma unroll
+      for (int u = 0; u < C8; ++u) v[u] = i0 + u < p ? B.val[i0 + u] : 0;
+#pragma unroll
+      for (int u = 0; u < C8; ++u)
+        if (i0 + u < p) st.push(point_value(B, i0 + u, v[u], sf));
+    }
     c.prev_ts = bt;
     c.prev_val = st.finish(&err);
   }
@@ -110,8 +121,21 @@ __global__ __launch_bounds__(256) void k_fold_prep(Params P, BatchDev B,
     const int64_t k = bucket_of(P, B.ts[p]);
     const int64_t bt = bucket_ts(P, k), be = bucket_ts(P, k + 1);
     M st = M::init();
-    for (int64_t i = p; i < hi && B.ts[i] < be; ++i)
-      st.push(point_value(B, i, B.val[i], sf));
+    bool more = true;
+    for (int64_t i0 = p; more && i0 < hi; i0 += C8) {
+      int64_t t[C8], v[C8];
+#pragma unroll
+      for (int u = 0; u < C8; ++u) {
+        const bool in = i0 + u < hi;
+        t[u] = in ? B.ts[i0 + u] : INT64_MAX;
+        v[u] = in ? B.val[i0 + u] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < C8; ++u) {
+        more = more && t[u] < be;  // (INT64_MAX past hi)
+        if (more) st.push(point_value(B, i0 + u, v[u], sf));
+      }
+    }
     c.next_ts = bt;
     c.next_val = st.finish(&err);
   }

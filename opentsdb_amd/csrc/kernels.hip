@@ -1787,6 +1787,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_group_select(
 // {error word, total points} pair for one read-back, and zeroes the error
 // word for the next call (the engine's memset of it is skipped then).
 // ------------------------------------------------------------------------
+constexpr int kCmpSlots = 4;  // ticket counters, one per call in rotation
 constexpr int kCmpStatusShift = 38;
 constexpr int kCmpEpochShift = 40;
 constexpr uint64_t kCmpValueMask = (1ULL << kCmpStatusShift) - 1;
@@ -1822,21 +1823,15 @@ __global__ __launch_bounds__(256) void k_compact1(
   __shared__ unsigned long long s_blk;
   const int lane = LANE, w = threadIdx.x >> 6;
   if (threadIdx.x == 0) {
-    // the ticket word {epoch:32, count:32} restarts at each call's first
-    // ticket (no memset)
-    unsigned long long old = __hip_atomic_load(ticket, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-    for (;;) {
-      const bool same = (old >> 32) == epoch;
-      const unsigned long long want =
-          same ? old + 1 : (((unsigned long long)epoch << 32) | 1ULL);
-      if (__hip_atomic_compare_exchange_strong(
-              ticket, &old, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-              __HIP_MEMORY_SCOPE_AGENT)) {
-        s_blk = same ? (old & 0xFFFFFFFFULL) : 0;
-        break;
-      }
-    }
+    // this call's ticket counter: slot epoch % kCmpSlots (zero: the previous
+    // call's last block cleared it); the last block clears the next call's
+    unsigned long long* tk = ticket + (epoch & (kCmpSlots - 1));
+    const unsigned long long t = __hip_atomic_fetch_add(
+        tk, 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t + 1 == gridDim.x)
+      __hip_atomic_store(ticket + ((epoch + 1) & (kCmpSlots - 1)), 0ULL,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_blk = t;
   }
   __syncthreads();
   const int64_t g = (int64_t)s_blk * 4 + w;

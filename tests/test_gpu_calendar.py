@@ -213,11 +213,13 @@ def test_per_series_grids_from_cells(engine, ds):  # noqa: F811
 
 def test_per_series_grids_with_fill_chain_ends_inside_the_window(engine):  # noqa: F811
     """FillingDownsampler over per-series grids whose caller-supplied chains
-    end inside the window (every chain but the filling grid's own is cut at
-    the window's middle): a point past its chain's last edge may lie in a
-    bucket that starts on the filling grid, and the table cannot say which
-    — the engine must not drop it (and fill its bucket) silently:
-    E_UNSUPPORTED, the Java path's query (advisor, round 4)."""
+    end inside the window: every series anchored off the filling grid's own
+    chain (7mc grids restart each day: a series first seen on day 2 steps
+    its own chain) gets a chain that ends three edges past its anchor.  Its
+    later points lie in buckets the table cannot place — on the filling grid
+    (emitted) or not (dropped) — so the engine must not drop them (and fill
+    their buckets) silently: E_UNSUPPORTED, the Java path's query (advisor,
+    round 4)."""
     import numpy as np
     b = datasets.random_batch(197, n_series=24, n_groups=3, span_ms=3 * DAY,
                               cadence_ms=60000, t0=T_SPRING)
@@ -229,18 +231,20 @@ def test_per_series_grids_with_fill_chain_ends_inside_the_window(engine):  # noq
     big = np.iinfo(np.int64).max
     terms = np.nonzero(edges == big)[0]
     j = int(np.searchsorted(anchors, start, "right")) - 1
-    fd_term = int(terms[np.searchsorted(terms, aedge[j])])
-    mid = (start + end) // 2
-    a, cut_any = 0, False
-    for t in terms:
-        if t != fd_term:
-            seg = np.arange(a, t)
-            past = seg[edges[seg] > mid]
-            if len(past) > 1:
-                edges[past[0]] = big
-                cut_any = True
-        a = t + 1
-    assert cut_any
+    fd_chain = int(np.searchsorted(terms, aedge[j]))
+    cut = 0
+    for s in range(b.n_series):
+        ts = b.ts[b.offsets[s]:b.offsets[s + 1]]
+        ts = ts[ts >= start]
+        if not len(ts):
+            continue
+        k = int(np.searchsorted(anchors, ts[0], "right")) - 1
+        e = int(aedge[k])
+        if int(np.searchsorted(terms, e)) != fd_chain and \
+                edges[e + 3] != big and ts[-1] > edges[e + 3]:
+            edges[e + 3] = big  # the series' chain: 3 edges
+            cut += 1
+    assert cut > 0
     keep = edges[aedge] == anchors
     anchors, aedge = anchors[keep], aedge[keep]
     spec._cal_edges_ref, spec._cal_anchor_refs = edges, (anchors, aedge)
