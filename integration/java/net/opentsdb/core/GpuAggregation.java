@@ -274,8 +274,11 @@ public final class GpuAggregation {
           row_base, qual_off, qual, val_off, val, group_offsets,
           group_members, out_offsets, out_ts, out_val, out_is_int);
       if (st == CAPACITY) {
-        // the offsets carry the whole result's size (include/otsdb_agg.h)
-        cap = Math.max(cap + 1, out_offsets[groups.length]);
+        // the result's own shortfall fills the offsets with the size the
+        // whole result needs (include/otsdb_agg.h); any other capacity
+        // (decode / compaction workspace) leaves them zero: grow
+        // geometrically so a retry never re-runs the query for +1
+        cap = Math.max(cap * 2, out_offsets[groups.length]);
         continue;
       }
       if (st == UNSUPPORTED) {

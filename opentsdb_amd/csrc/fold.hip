@@ -94,46 +94,67 @@ __global__ __launch_bounds__(256) void k_fold_prep(Params P, BatchDev B,
     return;
   }
   const int sf = B.series_float ? (int)B.series_float[s] : 1;
-  const int64_t p = lower_bound_interp(B.ts, lo, hi, bucket_ts(P, j * WB));
+  const int64_t p = lower_bound_near(B.ts, lo, hi, bucket_ts(P, j * WB));
   c.bnd = p;
   int err = 0;
-  // the buckets either side, reduced in point order; points are read 8 at a
-  // time (all eight loads in flight before the pushes: the loop was a
-  // dependent load per point, most of this latency-bound kernel's time)
+  // the buckets either side, reduced in point order.  The 8 points either
+  // side of the boundary are read in ONE round of loads (a bucket of up to 8
+  // points needs nothing else; longer ones continue point-chunk by chunk):
+  // each dependent load round costs this latency-bound kernel ~2 us
   constexpr int C8 = 8;
+  int64_t t[2 * C8], v[2 * C8];
+#pragma unroll
+  for (int u = 0; u < 2 * C8; ++u) {
+    const int64_t i = p - C8 + u;
+    const bool in = i >= lo && i < hi;
+    t[u] = in ? B.ts[i] : (i < lo ? INT64_MIN : INT64_MAX);
+    v[u] = in ? B.val[i] : 0;
+  }
   if (p > lo) {
-    const int64_t k = bucket_of(P, B.ts[p - 1]);
+    const int64_t k = bucket_of(P, t[C8 - 1]);
     const int64_t bt = bucket_ts(P, k);
-    const int64_t q = lower_bound_interp(B.ts, lo, p, bt);
     M st = M::init();
-    for (int64_t i0 = q; i0 < p; i0 += C8) {
-      int64_t v[C8];
+    // the bucket starts before the chunk: its earlier points first
+    if (t[0] >= bt && p - C8 > lo) {
+      const int64_t q = lower_bound_interp(B.ts, lo, p - C8, bt);
+      for (int64_t i0 = q; i0 < p - C8; i0 += C8) {
+        int64_t w[C8];
 #pragma unroll
-      for (int u = 0; u < C8; ++u) v[u] = i0 + u < p ? B.val[i0 + u] : 0;
+        for (int u = 0; u < C8; ++u) w[u] = i0 + u < p - C8 ? B.val[i0 + u] : 0;
 #pragma unroll
-      for (int u = 0; u < C8; ++u)
-        if (i0 + u < p) st.push(point_value(B, i0 + u, v[u], sf));
+        for (int u = 0; u < C8; ++u)
+          if (i0 + u < p - C8) st.push(point_value(B, i0 + u, w[u], sf));
+      }
     }
+#pragma unroll
+    for (int u = 0; u < C8; ++u)
+      if (t[u] >= bt && t[u] != INT64_MAX)
+        st.push(point_value(B, p - C8 + u, v[u], sf));
     c.prev_ts = bt;
     c.prev_val = st.finish(&err);
   }
   if (p < hi) {
-    const int64_t k = bucket_of(P, B.ts[p]);
+    const int64_t k = bucket_of(P, t[C8]);
     const int64_t bt = bucket_ts(P, k), be = bucket_ts(P, k + 1);
     M st = M::init();
     bool more = true;
-    for (int64_t i0 = p; more && i0 < hi; i0 += C8) {
-      int64_t t[C8], v[C8];
+#pragma unroll
+    for (int u = C8; u < 2 * C8; ++u) {
+      more = more && t[u] < be;  // (INT64_MAX past hi)
+      if (more) st.push(point_value(B, p - C8 + u, v[u], sf));
+    }
+    for (int64_t i0 = p + C8; more && i0 < hi; i0 += C8) {
+      int64_t tt[C8], w[C8];
 #pragma unroll
       for (int u = 0; u < C8; ++u) {
         const bool in = i0 + u < hi;
-        t[u] = in ? B.ts[i0 + u] : INT64_MAX;
-        v[u] = in ? B.val[i0 + u] : 0;
+        tt[u] = in ? B.ts[i0 + u] : INT64_MAX;
+        w[u] = in ? B.val[i0 + u] : 0;
       }
 #pragma unroll
       for (int u = 0; u < C8; ++u) {
-        more = more && t[u] < be;  // (INT64_MAX past hi)
-        if (more) st.push(point_value(B, i0 + u, v[u], sf));
+        more = more && tt[u] < be;
+        if (more) st.push(point_value(B, i0 + u, w[u], sf));
       }
     }
     c.next_ts = bt;

@@ -106,6 +106,37 @@ DEV int64_t lower_bound_interp(const int64_t* ts, int64_t a, int64_t b,
   return lower_bound(ts, lo + 1, hi, t);
 }
 
+// lower_bound over [a, b) in two rounds of loads for near-regular series:
+// the ends, then the 8 points around the interpolated guess, which hold the
+// answer unless the cadence is irregular there (then lower_bound_interp's
+// gallop).  k_fold_prep's window edges: a chain of 4-6 dependent loads was
+// most of that latency-bound kernel.
+DEV int64_t lower_bound_near(const int64_t* ts, int64_t a, int64_t b,
+                             int64_t t) {
+  if (a >= b) return a;
+  const int64_t ta = ts[a];
+  if (ta >= t) return a;
+  const int64_t tb = ts[b - 1];
+  if (tb < t) return b;
+  // ts[a] < t <= ts[b - 1]
+  const double f = (double)(t - ta) / (double)(tb - ta);
+  const int64_t g = a + (int64_t)(f * (double)(b - 1 - a));
+  int64_t base = g - 4;
+  if (base > b - 8) base = b - 8;
+  if (base < a) base = a;
+  int cnt = 0;
+  bool last_ge = false;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int64_t i = base + u;
+    const int64_t x = i < b ? ts[i] : INT64_MAX;
+    cnt += x < t ? 1 : 0;
+    if (u == 0 && x >= t && base > a) last_ge = true;  // answer before base
+  }
+  if (!last_ge && cnt < 8) return base + cnt;
+  return lower_bound_interp(ts, a, b, t);
+}
+
 // lower bound of t in [a, b) found by galloping back from b - 1: the start
 // of the bucket that holds ts[b - 1] lies a few points before it
 DEV int64_t lower_bound_back(const int64_t* ts, int64_t a, int64_t b,
@@ -1838,7 +1869,26 @@ __global__ __launch_bounds__(256) void k_compact1(
   if (g >= G) return;
   const int64_t nb = P.nb;
   const uint8_t* em = out_emit + g * nb;
-  const int64_t n = compact_count(em, nb, lane);
+  // grids of up to 2,048 buckets (C1's 1,440, C2's 2,017): every emit flag
+  // and value read ONCE (lane = bucket, coalesced) and held in registers
+  // across the look-back, the count from the ballots
+  constexpr int U2 = 32;
+  const bool regs = nb <= 64 * U2;
+  uint64_t bm[U2];
+  double vv[U2];
+  int64_t n = 0;
+  if (regs) {
+#pragma unroll
+    for (int u = 0; u < U2; ++u) {
+      const int64_t b = 64 * u + lane;
+      const bool in = b < nb;
+      vv[u] = in ? out_val[g * nb + b] : 0.0;
+      bm[u] = __ballot(in && em[b]);
+      n += __popcll(bm[u]);
+    }
+  } else {
+    n = compact_count(em, nb, lane);
+  }
   const uint64_t tag = (uint64_t)epoch << kCmpEpochShift;
   if (lane == 0)
     __hip_atomic_store(&flags[g], tag | (1ULL << kCmpStatusShift) | (uint64_t)n,
@@ -1887,6 +1937,24 @@ __global__ __launch_bounds__(256) void k_compact1(
       small[0] = (int64_t)(uint32_t)__hip_atomic_exchange(
           err_word, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+  }
+  if (regs) {
+    int64_t pos = prefix;
+#pragma unroll
+    for (int u = 0; u < U2; ++u) {
+      const int64_t b = 64 * u + lane;
+      const uint64_t m = bm[u];
+      if ((m >> lane) & 1) {
+        const int64_t p = pos + __popcll(m & ((1ULL << lane) - 1));
+        if (p < cap) {
+          r_ts[p] = bucket_ts(P, b);
+          r_val[p] = __double_as_longlong(vv[u]);
+          r_isint[p] = 0;  // downsampled values are doubles
+        }
+      }
+      pos += __popcll(m);
+    }
+    return;
   }
   constexpr int U = 8;
   int64_t pos = prefix;

@@ -1,5 +1,5 @@
 """The device lower-bound searches (kernels.hip: lower_bound, lower_bound_interp,
-lower_bound_back) compiled for the host with gcc and checked against a linear
+lower_bound_back, lower_bound_near) compiled for the host with gcc and checked against a linear
 scan on random sorted series: regular, jittered, duplicated and gapped
 timestamps, every sub-range shape.  They decide where a query's span starts
 (k_prep's seek, which stands for Span.java:360 seekRow and 464 seek) and where each fold
@@ -15,6 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "opentsdb_amd", "csrc", "kernels.hip")
 
 HARNESS = r"""
+#include <stdbool.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -45,6 +46,7 @@ int main(void) {
       bad += lower_bound(ts, a, b, t) != r;
       bad += lower_bound_interp(ts, a, b, t) != r;
       bad += lower_bound_back(ts, a, b, t) != r;
+      bad += lower_bound_near(ts, a, b, t) != r;
     }
   }
   printf("%%ld %%ld\n", n, bad);
@@ -63,7 +65,8 @@ def _function(text, name):
 def test_lower_bounds_match_linear_scan(tmp_path):
     text = open(SRC).read()
     body = "".join(_function(text, n) for n in
-                   ("lower_bound", "lower_bound_interp", "lower_bound_back"))
+                   ("lower_bound", "lower_bound_interp", "lower_bound_back",
+                    "lower_bound_near"))
     c = tmp_path / "lb.c"
     c.write_text(HARNESS % body)
     exe = tmp_path / "lb"
@@ -71,3 +74,4 @@ def test_lower_bounds_match_linear_scan(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True)
     n, bad = map(int, out.stdout.split())
     assert n == 800000 and bad == 0, out.stdout
+
