@@ -161,8 +161,10 @@ def pmc_traffic(name):
     pmc = max(found)[1]
     with open(pmc) as f:
         d = json.load(f)
-    return d.get("hbm_bytes_per_launch",
-                 d.get("k_bucketize_hbm_bytes_per_launch"))
+    return {"step": d.get("step_hbm_bytes"),
+            "dominant_kernel": d.get("hbm_bytes_per_launch",
+                                     d.get("k_bucketize_hbm_bytes_per_launch")),
+            "source": os.path.relpath(pmc, ROOT)}
 
 
 def named_query_figure(eng, db, config, warm=3, reps=10):
@@ -633,9 +635,13 @@ def main():
                     / 1e9 / HBM_PEAK_GBS}
     # PMC traffic of this exact workload (scripts/gpu_pmc.sh, default size,
     # one GPU, the shipped kernels), per launch of the dominant kernel
-    traffic = None
+    traffic = tinfo = None
     if not args.series and world == 1 and not args.named_query:
-        traffic = pmc_traffic(args.config)
+        tinfo = pmc_traffic(args.config)
+        # HBM bytes of one whole query (every pipeline kernel, PMC), like
+        # `achieved`; the dominant kernel's own beside it
+        if tinfo:
+            traffic = tinfo["step"] or tinfo["dominant_kernel"]
 
     extra = {}
     if rank == 0 and world == 1:
@@ -697,6 +703,7 @@ def main():
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "timed_over": "ms_per_step (the whole query, per GPU)",
                 "traffic": traffic,
+                "traffic_pmc": tinfo,
                 "algorithmic_bytes_per_launch": BYTES_PER_POINT * n_points,
                 "kernel_ms": kb_s * 1e3,
                 "kernel_achieved": kernel_achieved,

@@ -225,9 +225,11 @@ __global__ __launch_bounds__(256) void k_raw_cand_fill(
   for (int64_t i = a + lane; i < b; i += 64) {
     const int64_t t = V.ts[i];
     // occurrence of t: the copies before it in the span (from its seek:
-    // copies before the first candidate were never in the next slot)
-    int64_t occ = 0;
-    while (i - occ > a && V.ts[i - occ - 1] == t && occ < kOccMax) ++occ;
+    // copies before the first candidate were never in the next slot); the
+    // run's first copy by a gallop back from i, O(log occ) loads, not a
+    // walk (a run of k copies cost O(k^2) walking; on a decreasing span the
+    // value is moot: the query is flagged below)
+    const int64_t occ = i - lower_bound_back(V.ts, a, i + 1, t);
     keys[o + i] = ((uint64_t)t << kOccBits) | (uint64_t)occ;
     if ((i > a && V.ts[i - 1] > t) || occ >= kOccMax || t >= kRawTsMax) bad = 1;
   }
@@ -315,9 +317,9 @@ DEV Slots span_slots(const Params& P, const RawView& V, int64_t s, int64_t x,
   r.state = 1;
   r.cur = last_le(V.ts, a, b, x);
   if (V.ts[r.cur] == x && (occ > 0 || (r.cur > a && V.ts[r.cur - 1] == x))) {
-    // copies of x: [f, r.cur]; emission occ holds copy occ
-    int64_t f = r.cur;
-    while (f > a && V.ts[f - 1] == x) --f;
+    // copies of x: [f, r.cur]; emission occ holds copy occ (f by a gallop
+    // back: O(log k) loads per (emission, member))
+    const int64_t f = lower_bound_back(V.ts, a, r.cur + 1, x);
     if (r.cur - f >= occ) {
       r.cur = f + occ;
     } else if (r.cur == b - 1) {  // fewer copies: the last point expired

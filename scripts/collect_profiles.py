@@ -1,4 +1,4 @@
-"""Copies one evidence run's results (scripts/gpu_r3_final.sh, merged into
+"""Copies one evidence run's results (scripts/gpu_r5_evidence.sh, merged into
 gpurun_out/) into profiles/ under a round tag: bench lines, rocprofv3
 kernel-stats summaries, PMC summaries, the storage-row / mixed-width kernel
 stats and the GPU test summary.  Usage: python scripts/collect_profiles.py r3"""
@@ -39,8 +39,11 @@ def main(tag):
             dst = os.path.join(PROF, "%s_%s_kernel_stats.csv" % (tag, cfg))
             shutil.copy(ks, dst)
             done.append(dst)
-    for name, src in (("pmc_C2.json", "pmc_C2/summary.json"),
+    for name, src in (("pmc_C1.json", "pmc_C1/summary.json"),
+                      ("pmc_C2.json", "pmc_C2/summary.json"),
+                      ("pmc_C3.json", "pmc_C3/summary.json"),
                       ("pmc_C4.json", "pmc_C4/summary.json"),
+                      ("pmc_C5.json", "pmc_C5/summary.json"),
                       ("pmc_cells_C2.json", "pmc_cells/summary.json"),
                       ("pmc_C2_named.json", "pmc_C2_named/summary.json")):
         p = os.path.join(OUT, src)
@@ -53,7 +56,7 @@ def main(tag):
             dst = os.path.join(PROF, "%s_%s_kernel_stats.csv" % (tag, what))
             shutil.copy(ks, dst)
             done.append(dst)
-    p = os.path.join(OUT, "pytest_gpu.log")
+    p = os.path.join(OUT, "r5_gpu_suite.log")
     if os.path.exists(p):
         with open(p) as f:
             tail = f.read().splitlines()[-3:]

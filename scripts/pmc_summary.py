@@ -41,6 +41,18 @@ def main(root):
             continue
         acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
     out = {}
+    # every kernel of the query pipeline (not the generator's, not the
+    # runtime's fills / copies): the HBM bytes of one whole query (per step)
+    step = 0.0
+    step_k = []
+    for k, cs in acc.items():
+        if ("k_gen" in k or "rocclr" in k or "at::native" in k or "rocprim" in k
+                or "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs):
+            continue
+        rd = sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"]) * 1024 * 2
+        wr = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"]) * 1024
+        step += rd + wr
+        step_k.append(short(k))
     for k, cs in acc.items():
         if ("bucketize" not in k and "k_fold" not in k
                 and "k_decode" not in k):
@@ -61,6 +73,8 @@ def main(root):
         out = {"hbm_bytes_per_launch":
                best["hbm_read_bytes_corrected"] + best["hbm_write_bytes"],
                "kernel": best_k, "kernels": out}
+    out["step_hbm_bytes"] = step
+    out["step_kernels"] = sorted(step_k)
     json.dump(out, sys.stdout, indent=1)
     print()
 
