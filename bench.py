@@ -458,6 +458,15 @@ def cpu_baseline(config, target_s):
             dtm = time.perf_counter() - t
         out["all_cores"] = {"value": pts / dtm, "cores": threads,
                             "seconds": dtm}
+        # the whole host, for a node-level comparison: NOT measured (a GPU
+        # box's share is its per-GPU slice of the cores); the measured
+        # per-thread rate scaled linearly to every CPU, an upper bound for
+        # an embarrassingly parallel per-group evaluation
+        per_thread = pts / dtm / threads
+        out["whole_host_projection"] = {
+            "value": per_thread * host["nproc"], "cores": host["nproc"],
+            "kind": "projection: measured %d-thread rate x %d / %d CPUs" % (
+                threads, host["nproc"], threads)}
     return out
 
 

@@ -7,8 +7,8 @@ mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 N=${1:-10000}
 NC=${2:-1500}
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
-  tests/test_gpu_fillins.py tests/test_gpu_sweep.py tests/test_gpu_dev_order.py \
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+  -m gpu tests/ \
   > gpurun_out/r5_tests.log 2>&1
 r0=$?; tail -3 gpurun_out/r5_tests.log
 [ $r0 -gt 1 ] && exit $r0
@@ -18,6 +18,6 @@ r1=$?; tail -2 gpurun_out/r5_sweep_general.log; grep FAIL gpurun_out/r5_sweep_ge
 timeout -k 10 500 python -u scripts/sweep_many.py 0 $N 0 > gpurun_out/r5_sweep_rate.log 2>&1
 r2=$?; tail -2 gpurun_out/r5_sweep_rate.log; grep FAIL gpurun_out/r5_sweep_rate.log | head
 [ $r2 -gt 1 ] && exit $r2
-timeout -k 10 250 python -u scripts/sweep_cells.py $NC 0 > gpurun_out/r5_sweep_cells.log 2>&1
+timeout -k 10 420 python -u scripts/sweep_cells.py $NC 0 > gpurun_out/r5_sweep_cells.log 2>&1
 r3=$?; tail -2 gpurun_out/r5_sweep_cells.log; grep FAIL gpurun_out/r5_sweep_cells.log | head
 exit $(( r0 | r1 | r2 | r3 ))
