@@ -99,7 +99,10 @@ constexpr int64_t kChunk = 256;  // series per cross-series chunk
 // datacenters per GPU) are cut finer than kChunk — 256-member tiles of one
 // day of points leave the last round of workgroups half empty (C3 fold:
 // 256 -> 2.9 ms, 64 -> 2.57 ms, 32 -> 2.53 ms)
-constexpr int64_t kFoldChunk = 32;
+#ifndef OTSDB_FOLD_CHUNK  // tuning builds override
+#define OTSDB_FOLD_CHUNK 32
+#endif
+constexpr int64_t kFoldChunk = OTSDB_FOLD_CHUNK;
 // Order-sensitive aggregators whose merge of partial states is
 // ill-conditioned (dev: Chan's merge of Welford runs over offset data lands
 // ~1e-11 from the reference's one sequential pass, Aggregators.java:547-568)
@@ -113,6 +116,7 @@ constexpr int64_t kFoldChunk = 32;
 // handed on (otsdb_agg_partials_chained_device).
 constexpr int64_t kOrderedFoldChunk = 256;
 constexpr int64_t kOrderedChunk = 65536;
+constexpr int64_t kOrderedChunkMerged = 16384;
 // below this many (tile, window) workgroups the fold narrows its windows,
 // down to kFoldMinWindow buckets
 #ifndef OTSDB_FOLD_MIN_BLOCKS  // tuning builds override
@@ -855,9 +859,15 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   // verbatim storage rows: the single-window cells fold only (it checks
   // what compaction would change; window boundaries it does not see)
   if (c->verbatim && (!cfold || NW > 1)) return spec_miss(c);
+  // one chain per (group, bucket) up to kOrderedChunk members; partials for
+  // the merge across ranks (a group too large to hand on, dist.py) keep
+  // round 4's shorter chains, merged in order anyway
   otsdb_status rc = build_tiles(
       c, goff, mode == 2, fold ? kFoldChunk : kChunk,
-      ordered ? (fold ? kOrderedFoldChunk : kOrderedChunk) : 0);
+      ordered ? (fold ? kOrderedFoldChunk
+                      : (mode == 1 && !ginit ? kOrderedChunkMerged
+                                             : kOrderedChunk))
+              : 0);
   if (rc) return rc;
   const Tiles T = tiles_of(c, G);
   P.fold_wb = 0;  // (P may come from an earlier pipeline run)

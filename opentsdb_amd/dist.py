@@ -25,6 +25,9 @@ PARTIAL_WORDS = 4  # otsdb_partial = 3 doubles + int64
 # aggregators whose partial states are handed on across ranks, not merged
 # (monoids.h kOrdered)
 ORDERED_AGGS = ("dev",)
+# groups up to this many members (over all ranks) are handed on as one
+# chain (the engine's kOrderedChunk); larger ones merge per-rank partials
+CHAIN_MAX_MEMBERS = 65536
 
 
 def shard_range(n_series, world, rank, offsets=None):
@@ -205,7 +208,21 @@ class ShardPlan:
                                             device=dev)[:len(m)],
                                dbatch.is_float, dbatch.series_float)
         self.local_batch = sub(self.local)
-        self.shared_batch = sub(self.shared)
+        # order-sensitive aggregators: shared groups small enough to be one
+        # chain over all ranks are handed on (hand_on_partials), the rest
+        # merge per-rank partials like every other aggregator
+        self.chain = np.zeros(0, np.int64)
+        self.merge = self.shared
+        if _agg_name(spec) in ORDERED_AGGS and len(self.shared):
+            sizes = torch.from_numpy(
+                (goff[self.shared + 1] - goff[self.shared]).astype(np.int64))
+            if not _staged(group):
+                sizes = sizes.to(dev)
+            all_reduce(sizes, "sum", group)
+            small = sizes.cpu().numpy() <= CHAIN_MAX_MEMBERS
+            self.chain, self.merge = self.shared[small], self.shared[~small]
+        self.chain_batch = sub(self.chain)
+        self.shared_batch = sub(self.merge)
         sz = engine.plan(spec, self.local_batch)
         self.nb = int(sz.n_buckets)
         from .engine import DeviceResult
@@ -217,26 +234,30 @@ class ShardPlan:
 class ShardedResult:
     """Per-rank result of a sharded query: the groups this rank holds alone
     (`local_ids`, `local`) and every group spanning ranks (`shared_ids`,
-    `shared`, identical on every rank); DeviceResult tensors."""
+    identical on every rank: merged partials, `shared`, and groups whose
+    states were handed on, `chained`); DeviceResult tensors."""
 
-    def __init__(self, local_ids, local, shared_ids, shared):
+    def __init__(self, local_ids, local, shared_ids, shared, chain_ids=(),
+                 chained=None):
         self.local_ids, self.local = local_ids, local
-        self.shared_ids, self.shared = shared_ids, shared
+        self.merge_ids, self.shared = shared_ids, shared
+        self.chain_ids, self.chained = np.asarray(chain_ids, np.int64), chained
+        self.shared_ids = np.concatenate([np.asarray(shared_ids, np.int64),
+                                          self.chain_ids])
+
+    def _parts(self):
+        return [(ids, res) for ids, res in
+                ((self.local_ids, self.local), (self.merge_ids, self.shared),
+                 (self.chain_ids, self.chained)) if len(ids)]
 
     def n_points(self):
-        n = int(self.local.offsets[-1].item()) if len(self.local_ids) else 0
-        if len(self.shared_ids):
-            n += int(self.shared.offsets[-1].item())
-        return n
+        return sum(int(res.offsets[-1].item()) for _, res in self._parts())
 
     def host_groups(self):
         """{global group id: (ts, value bits, is_int)} numpy arrays of the
         groups this rank holds the result of (its own and the shared ones)."""
         out = {}
-        for ids, res in ((self.local_ids, self.local),
-                         (self.shared_ids, self.shared)):
-            if not len(ids):
-                continue
+        for ids, res in self._parts():
             out.update(_host_slices(ids, res))
         return out
 
@@ -280,28 +301,26 @@ def run_sharded(engine, spec, dbatch, n_groups_global, torch_mod=None,
                                           n_groups_global, group)
     if len(plan.local):
         run_device(engine, spec, plan.local_batch, plan.local_res)
-    shared_res = None
-    n_sh = len(plan.shared)
-    if n_sh:
-        nb = plan.nb
-        GB = n_sh * nb
-        dev = dbatch.ts.device
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    dev = dbatch.ts.device
+    nb = plan.nb
+
+    def exchange(ids, sub, chained):
+        GB = len(ids) * nb
         parts = torch.zeros((max(GB, 1), PARTIAL_WORDS), dtype=torch.int64,
                             device=dev)
         emit = torch.zeros(max(GB, 1), dtype=torch.uint8, device=dev)
-        b = plan.shared_batch.as_abi()
-        stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-        if _agg_name(spec) in ORDERED_AGGS:
+        b = sub.as_abi()
+        if chained:
+            # every rank continues its predecessor's states; rank 0 from
+            # empty ones (the dev state's zero bits)
             def step(init_p, init_e):
                 if init_p is None:
-                    engine._check(engine.lib.otsdb_agg_partials_device(
-                        engine.ctx, C.byref(spec), C.byref(b),
-                        parts.data_ptr(), emit.data_ptr(), stream))
-                else:
-                    engine._check(engine.lib.otsdb_agg_partials_chained_device(
-                        engine.ctx, C.byref(spec), C.byref(b),
-                        init_p.data_ptr(), init_e.data_ptr(),
-                        parts.data_ptr(), emit.data_ptr(), stream))
+                    init_p, init_e = torch.zeros_like(parts), torch.zeros_like(emit)
+                engine._check(engine.lib.otsdb_agg_partials_chained_device(
+                    engine.ctx, C.byref(spec), C.byref(b), init_p.data_ptr(),
+                    init_e.data_ptr(), parts.data_ptr(), emit.data_ptr(),
+                    stream))
             hand_on_partials(step, parts, emit, group)
             gp, ge, n_ranks = parts[:GB], emit[:GB], 1
         else:
@@ -310,13 +329,20 @@ def run_sharded(engine, spec, dbatch, n_groups_global, torch_mod=None,
                 emit.data_ptr(), stream))
             gp, ge = all_gather_partials(parts[:GB], emit[:GB], group)
             n_ranks = plan.world
-        shared_res = DeviceResult(torch, n_sh, GB, dev)
-        r = shared_res.as_abi()
+        res = DeviceResult(torch, len(ids), max(GB, 1), dev)
+        r = res.as_abi()
         engine._check(engine.lib.otsdb_agg_finalize_device(
-            engine.ctx, C.byref(spec), n_sh, nb, n_ranks,
+            engine.ctx, C.byref(spec), len(ids), nb, n_ranks,
             gp.contiguous().data_ptr(), ge.contiguous().data_ptr(),
             C.byref(r), stream))
-    return ShardedResult(plan.local, plan.local_res, plan.shared, shared_res)
+        return res
+
+    merged = exchange(plan.merge, plan.shared_batch, False) \
+        if len(plan.merge) else None
+    chained = exchange(plan.chain, plan.chain_batch, True) \
+        if len(plan.chain) else None
+    return ShardedResult(plan.local, plan.local_res, plan.merge, merged,
+                         plan.chain, chained)
 
 
 class ShardedSelect:

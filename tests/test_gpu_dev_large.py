@@ -85,9 +85,9 @@ def test_dev_offset_gauge_20000_members(engine, ds):
 
 
 def _chained_emulated(engines, spec, hb, world):
-    """dist.hand_on_partials with the ranks run one after another in this
-    process: rank 0's partials, each later rank's continued from the
-    previous output, the last one finalised."""
+    """dist.run_sharded's chained exchange with the ranks run one after
+    another in this process: rank 0 from empty states, each later rank
+    continuing the previous output, the last one finalised."""
     import ctypes as C
     import torch
     from opentsdb_amd.engine import DeviceResult
@@ -102,14 +102,11 @@ def _chained_emulated(engines, spec, hb, world):
         p = torch.zeros((GB, 4), dtype=torch.int64, device="cuda")
         m = torch.zeros(GB, dtype=torch.uint8, device="cuda")
         b = db.as_abi()
-        if prev is None:
-            e._check(e.lib.otsdb_agg_partials_device(
-                e.ctx, C.byref(spec), C.byref(b), p.data_ptr(), m.data_ptr(),
-                None))
-        else:
-            e._check(e.lib.otsdb_agg_partials_chained_device(
-                e.ctx, C.byref(spec), C.byref(b), prev[0].data_ptr(),
-                prev[1].data_ptr(), p.data_ptr(), m.data_ptr(), None))
+        if prev is None:  # rank 0: empty states (dev's zero bits)
+            prev = (torch.zeros_like(p), torch.zeros_like(m))
+        e._check(e.lib.otsdb_agg_partials_chained_device(
+            e.ctx, C.byref(spec), C.byref(b), prev[0].data_ptr(),
+            prev[1].data_ptr(), p.data_ptr(), m.data_ptr(), None))
         prev = (p, m)
     res = DeviceResult(torch, G, max(G * nb, 1), "cuda")
     r = res.as_abi()
