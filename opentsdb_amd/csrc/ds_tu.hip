@@ -39,6 +39,9 @@
 #ifndef OTSDB_RATE_FL
 #define OTSDB_RATE_FL 512
 #endif
+#ifndef OTSDB_PREP_TPB  // threads per block of the latency-bound prep kernels
+#define OTSDB_PREP_TPB 64  // (k_prep, k_fold_prep): 4x the CUs of 256-thread
+#endif                     // blocks on small queries (C1 prep 33 -> 27 us)
 #ifndef OTSDB_RATE_PF
 #define OTSDB_RATE_PF 0
 #endif
@@ -65,14 +68,16 @@ bool launch_cells(DsKernel k, const DsLaunch& a) {
   switch (k) {
     case DS_CELLS_PREP:
       if (S > 0)
-        hipLaunchKernelGGL(k_cells_prep<M>, dim3(ds_blocks(S, 256)), dim3(256),
-                           0, a.st, a.P, a.cf, S, a.SM, a.err);
+        hipLaunchKernelGGL(k_cells_prep<M>, dim3(ds_blocks(S, OTSDB_PREP_TPB)),
+                           dim3(OTSDB_PREP_TPB), 0, a.st, a.P, a.cf, S, a.SM,
+                           a.err);
       OTSDB_DBG(a.st, "k_cells_prep");
       return true;
     case DS_CELLS_FOLD_PREP:
       if (a.NW > 1 && S > 0)
         hipLaunchKernelGGL(k_cells_fold_prep<M>,
-                           dim3(ds_blocks(S * (a.NW - 1), 256)), dim3(256), 0,
+                           dim3(ds_blocks(S * (a.NW - 1), OTSDB_PREP_TPB)),
+                           dim3(OTSDB_PREP_TPB), 0,
                            a.st, a.P, a.cf, S, a.SM, a.NW, a.WB, a.wc, a.err);
       OTSDB_DBG(a.st, "k_cells_fold_prep");
       return true;
@@ -112,8 +117,8 @@ bool launch_ds(DsKernel k, const DsLaunch& a) {
   const int64_t S = a.B.S;
   switch (k) {
     case DS_PREP:
-      hipLaunchKernelGGL(k_prep<M>, dim3(ds_blocks(S, 256)), dim3(256), 0,
-                         a.st, a.P, a.B, a.SM, a.err);
+      hipLaunchKernelGGL(k_prep<M>, dim3(ds_blocks(S, OTSDB_PREP_TPB)),
+                         dim3(OTSDB_PREP_TPB), 0, a.st, a.P, a.B, a.SM, a.err);
       OTSDB_DBG(a.st, "k_prep");
       return true;
     case DS_RING:  // production: LDS ring sink, sentinel rows, DPP scan
@@ -140,7 +145,8 @@ bool launch_ds(DsKernel k, const DsLaunch& a) {
     case DS_FOLD_PREP:
       if (a.NW > 1 && S > 0)
         hipLaunchKernelGGL(k_fold_prep<M>,
-                           dim3(ds_blocks(S * (a.NW - 1), 256)), dim3(256), 0,
+                           dim3(ds_blocks(S * (a.NW - 1), OTSDB_PREP_TPB)),
+                           dim3(OTSDB_PREP_TPB), 0,
                            a.st, a.P, a.B, a.SM, a.NW, a.WB, a.wc);
       return true;
     case DS_FOLD:

@@ -103,6 +103,10 @@ constexpr int64_t kChunk = 256;  // series per cross-series chunk
 #define OTSDB_FOLD_CHUNK 32
 #endif
 constexpr int64_t kFoldChunk = OTSDB_FOLD_CHUNK;
+#ifndef OTSDB_FOLD_SMALL_CHUNK  // tuning builds: 0 = off
+#define OTSDB_FOLD_SMALL_CHUNK 0
+#endif
+constexpr int64_t kFoldSmallChunk = OTSDB_FOLD_SMALL_CHUNK;
 // Order-sensitive aggregators whose merge of partial states is
 // ill-conditioned (dev: Chan's merge of Welford runs over offset data lands
 // ~1e-11 from the reference's one sequential pass, Aggregators.java:547-568)
@@ -862,8 +866,20 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   // one chain per (group, bucket) up to kOrderedChunk members; partials for
   // the merge across ranks (a group too large to hand on, dist.py) keep
   // round 4's shorter chains, merged in order anyway
+  // few tiles (small queries: C1's 100 groups of 10 series are 100 tiles):
+  // smaller tiles first, so each workgroup streams fewer members one after
+  // another (tile partials then merge in k_combine), then narrower windows
+  // below.  Decided from the group sizes alone, so the tile plan stays
+  // cached across calls.
+  int64_t fold_chunk = kFoldChunk;
+  if (fold && !ordered && kFoldSmallChunk > 0 && NW > 0) {
+    int64_t t_full = 0;
+    for (int64_t g = 0; g < G; ++g)
+      t_full += (goff[g + 1] - goff[g] + kFoldChunk - 1) / kFoldChunk;
+    if (t_full * NW < kFoldMinBlocks) fold_chunk = kFoldSmallChunk;
+  }
   otsdb_status rc = build_tiles(
-      c, goff, mode == 2, fold ? kFoldChunk : kChunk,
+      c, goff, mode == 2, fold ? fold_chunk : kChunk,
       ordered ? (fold ? kOrderedFoldChunk
                       : (mode == 1 && !ginit ? kOrderedChunkMerged
                                              : kOrderedChunk))
@@ -1235,7 +1251,12 @@ otsdb_status compact(otsdb_ctx* c, const Params& P, int64_t G,
   c->cmp_epoch = c->cmp_epoch + 1 == (1u << 24) ? 4u : c->cmp_epoch + 1;
   unsigned long long* ticket = (unsigned long long*)((char*)c->d_err + 192);
   int64_t* small = (int64_t*)((char*)c->d_err + 128);
-  hipLaunchKernelGGL(k_compact1, dim3(blocks_for(G, 4)), dim3(256), 0, st, P,
+  // few groups (C1's 100): one group (wavefront) per block, spread over more
+  // CUs; many (C2's 10k): four per block (one wave per block ran C2's
+  // compaction 0.20 -> 0.27 ms)
+  const int gpb = G < 4096 ? 1 : 4;
+  hipLaunchKernelGGL(k_compact1, dim3(blocks_for(G, gpb)), dim3(64 * gpb), 0,
+                     st, P,
                      G, out_val, out_emit, (unsigned long long*)p, ticket,
                      c->cmp_epoch, out->offsets, out->capacity, out->ts,
                      out->val, out->is_int, c->d_err, small);

@@ -1865,7 +1865,7 @@ __global__ __launch_bounds__(256) void k_compact1(
     s_blk = t;
   }
   __syncthreads();
-  const int64_t g = (int64_t)s_blk * 4 + w;
+  const int64_t g = (int64_t)s_blk * (blockDim.x >> 6) + w;
   if (g >= G) return;
   const int64_t nb = P.nb;
   const uint8_t* em = out_emit + g * nb;
