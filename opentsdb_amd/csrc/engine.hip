@@ -103,10 +103,6 @@ constexpr int64_t kChunk = 256;  // series per cross-series chunk
 #define OTSDB_FOLD_CHUNK 32
 #endif
 constexpr int64_t kFoldChunk = OTSDB_FOLD_CHUNK;
-#ifndef OTSDB_FOLD_SMALL_CHUNK  // tuning builds: 0 = off
-#define OTSDB_FOLD_SMALL_CHUNK 0
-#endif
-constexpr int64_t kFoldSmallChunk = OTSDB_FOLD_SMALL_CHUNK;
 // Order-sensitive aggregators whose merge of partial states is
 // ill-conditioned (dev: Chan's merge of Welford runs over offset data lands
 // ~1e-11 from the reference's one sequential pass, Aggregators.java:547-568)
@@ -866,20 +862,8 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   // one chain per (group, bucket) up to kOrderedChunk members; partials for
   // the merge across ranks (a group too large to hand on, dist.py) keep
   // round 4's shorter chains, merged in order anyway
-  // few tiles (small queries: C1's 100 groups of 10 series are 100 tiles):
-  // smaller tiles first, so each workgroup streams fewer members one after
-  // another (tile partials then merge in k_combine), then narrower windows
-  // below.  Decided from the group sizes alone, so the tile plan stays
-  // cached across calls.
-  int64_t fold_chunk = kFoldChunk;
-  if (fold && !ordered && kFoldSmallChunk > 0 && NW > 0) {
-    int64_t t_full = 0;
-    for (int64_t g = 0; g < G; ++g)
-      t_full += (goff[g + 1] - goff[g] + kFoldChunk - 1) / kFoldChunk;
-    if (t_full * NW < kFoldMinBlocks) fold_chunk = kFoldSmallChunk;
-  }
   otsdb_status rc = build_tiles(
-      c, goff, mode == 2, fold ? fold_chunk : kChunk,
+      c, goff, mode == 2, fold ? kFoldChunk : kChunk,
       ordered ? (fold ? kOrderedFoldChunk
                       : (mode == 1 && !ginit ? kOrderedChunkMerged
                                              : kOrderedChunk))
