@@ -1220,12 +1220,16 @@ otsdb_status compact(otsdb_ctx* c, const Params& P, int64_t G,
     return OTSDB_OK;
   }
   StageTimer tm(c, 4);
-  // one pass (k_compact1): count, look-back scan, scatter, and the call's
-  // {error word, total} for finish's single read-back
+  // grids of up to kCmpRegBuckets: one pass (k_compact1: count, look-back
+  // scan, scatter); longer: k_compact_count + k_compact_scatter.  Either way
+  // the call's {error word, total} lands in `small` for finish's read-back.
+  // Scratch: flags [G] (one pass) or counts [G] + 64-group tile words
+  const size_t n_tiles = (size_t)((G + 63) >> 6);
   void* p = c->cmp_flags;
   size_t cap = c->cmp_flags_cap;
-  const bool grow = (size_t)G * 8 > cap;
-  otsdb_status rc = ensure(&p, &cap, (size_t)G * 8);
+  const size_t need = (size_t)G * 8 + n_tiles * 8 + 256;
+  const bool grow = need > cap;
+  otsdb_status rc = ensure(&p, &cap, need);
   c->cmp_flags = p;
   c->cmp_flags_cap = cap;
   if (rc) return rc;
@@ -1239,11 +1243,24 @@ otsdb_status compact(otsdb_ctx* c, const Params& P, int64_t G,
   // CUs; many (C2's 10k): four per block (one wave per block ran C2's
   // compaction 0.20 -> 0.27 ms)
   const int gpb = G < 4096 ? 1 : 4;
-  hipLaunchKernelGGL(k_compact1, dim3(blocks_for(G, gpb)), dim3(64 * gpb), 0,
-                     st, P,
-                     G, out_val, out_emit, (unsigned long long*)p, ticket,
-                     c->cmp_epoch, out->offsets, out->capacity, out->ts,
-                     out->val, out->is_int, c->d_err, small);
+  if (P.nb <= kCmpRegBuckets) {
+    hipLaunchKernelGGL(k_compact1, dim3(blocks_for(G, gpb)),
+                       dim3(64 * gpb), 0, st, P, G, out_val, out_emit,
+                       (unsigned long long*)p, ticket, c->cmp_epoch,
+                       out->offsets, out->capacity, out->ts, out->val,
+                       out->is_int, c->d_err, small);
+  } else {
+    int64_t* cnt = (int64_t*)p;
+    unsigned long long* tw = (unsigned long long*)((char*)p + (size_t)G * 8);
+    hipLaunchKernelGGL(k_compact_count, dim3(blocks_for(G, gpb)),
+                       dim3(64 * gpb), 0, st, P, G, out_emit, cnt, tw,
+                       ticket, c->cmp_epoch);
+    hipLaunchKernelGGL(k_compact_scatter, dim3(blocks_for(G, gpb)),
+                       dim3(64 * gpb), 0, st, P, G, out_val, out_emit,
+                       (const int64_t*)cnt, (const unsigned long long*)tw,
+                       out->offsets, out->capacity, out->ts, out->val,
+                       out->is_int, c->d_err, small);
+  }
   HIP_TRY(hipGetLastError());
   c->small_ready = true;
   return OTSDB_OK;

@@ -1822,6 +1822,8 @@ constexpr int kCmpSlots = 4;  // ticket counters, one per call in rotation
 constexpr int kCmpStatusShift = 38;
 constexpr int kCmpEpochShift = 40;
 constexpr uint64_t kCmpValueMask = (1ULL << kCmpStatusShift) - 1;
+constexpr int kCmpRegChunks = 32;  // k_compact1 holds grids of 64 x this
+constexpr int64_t kCmpRegBuckets = 64 * kCmpRegChunks;
 
 DEV int compact_count(const uint8_t* __restrict__ em, int64_t nb, int lane) {
   int n = 0;
@@ -1842,6 +1844,107 @@ DEV int compact_count(const uint8_t* __restrict__ em, int64_t nb, int lane) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) n += __shfl_xor(n, d);
   return n;
+}
+
+// Long grids (more than 2,048 buckets: the named query's 10,081) take two
+// launches instead: the single pass's count phase is long enough there that
+// most waves reach the look-back together and walk far back for an
+// inclusive prefix (the named query's compaction: 1.2 ms).  k_compact_count: each wave counts
+// its group's emitted buckets and adds the count into its 64-group tile's
+// word {epoch:24, sum:40} (at most 64 adders a word; the first of a call
+// restarts it); k_compact_scatter: each wave's prefix is the sum of the
+// earlier tiles' words plus its tile's earlier counts (two load rounds, no
+// waiting), then the scatter.
+constexpr int kCmpTileShift = 6;  // 64 groups a tile
+constexpr uint64_t kCmpSumMask = (1ULL << kCmpEpochShift) - 1;
+
+__global__ __launch_bounds__(256) void k_compact_count(
+    Params P, int64_t G, const uint8_t* __restrict__ out_emit,
+    int64_t* __restrict__ counts, unsigned long long* __restrict__ tiles,
+    unsigned long long* __restrict__ ticket, uint32_t epoch) {
+  const int lane = LANE;
+  // k_compact1's ticket slots rotate with the epoch whichever path a call
+  // takes: clear the next call's slot as its last block would
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(ticket + ((epoch + 1) & (kCmpSlots - 1)), 0ULL,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int64_t g = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (g >= G) return;
+  const int64_t n = compact_count(out_emit + g * P.nb, P.nb, lane);
+  if (lane == 0) {
+    counts[g] = n;
+    unsigned long long* tw = tiles + (g >> kCmpTileShift);
+    unsigned long long old = __hip_atomic_load(tw, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      const bool cur = (old >> kCmpEpochShift) == epoch;
+      const unsigned long long want =
+          cur ? old + (unsigned long long)n
+              : (((unsigned long long)epoch << kCmpEpochShift) |
+                 (unsigned long long)n);
+      if (__hip_atomic_compare_exchange_strong(
+              tw, &old, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+              __HIP_MEMORY_SCOPE_AGENT))
+        break;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_compact_scatter(
+    Params P, int64_t G, const double* __restrict__ out_val,
+    const uint8_t* __restrict__ out_emit, const int64_t* __restrict__ counts,
+    const unsigned long long* __restrict__ tiles, int64_t* __restrict__ offsets,
+    int64_t cap, int64_t* __restrict__ r_ts, int64_t* __restrict__ r_val,
+    uint8_t* __restrict__ r_isint, int* err_word, int64_t* __restrict__ small) {
+  const int lane = LANE;
+  const int64_t g = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (g >= G) return;
+  const int64_t nb = P.nb;
+  const int64_t t = g >> kCmpTileShift;
+  int64_t x = 0;
+  for (int64_t i = lane; i < t; i += 64) x += (int64_t)(tiles[i] & kCmpSumMask);
+  const int64_t g0 = t << kCmpTileShift;
+  if (g0 + lane < g) x += counts[g0 + lane];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+  const int64_t prefix = x;
+  const uint8_t* em = out_emit + g * nb;
+  if (lane == 0) {
+    offsets[g] = prefix;
+    if (g == G - 1) {
+      const int64_t tot = prefix + counts[g];
+      offsets[G] = tot;
+      small[1] = tot;
+      small[0] = (int64_t)(uint32_t)__hip_atomic_exchange(
+          err_word, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  constexpr int U = 16;
+  int64_t pos = prefix;
+  for (int64_t c0 = 0; c0 < nb; c0 += 64 * U) {
+    bool e[U];
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t b = c0 + 64 * u + lane;
+      e[u] = b < nb && em[b];
+      v[u] = b < nb ? out_val[g * nb + b] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t b = c0 + 64 * u + lane;
+      const uint64_t m = __ballot(e[u]);
+      if (e[u]) {
+        const int64_t p = pos + __popcll(m & ((1ULL << lane) - 1));
+        if (p < cap) {
+          r_ts[p] = bucket_ts(P, b);
+          r_val[p] = __double_as_longlong(v[u]);
+          r_isint[p] = 0;  // downsampled values are doubles
+        }
+      }
+      pos += __popcll(m);
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void k_compact1(
@@ -1869,25 +1972,21 @@ __global__ __launch_bounds__(256) void k_compact1(
   if (g >= G) return;
   const int64_t nb = P.nb;
   const uint8_t* em = out_emit + g * nb;
-  // grids of up to 2,048 buckets (C1's 1,440, C2's 2,017): every emit flag
-  // and value read ONCE (lane = bucket, coalesced) and held in registers
-  // across the look-back, the count from the ballots
-  constexpr int U2 = 32;
-  const bool regs = nb <= 64 * U2;
+  // grids of up to 2,048 buckets (C1's 1,440, C2's 2,017; the engine sends
+  // longer ones to the two-launch path above): every emit flag and value
+  // read ONCE (lane = bucket, coalesced) and held in registers across the
+  // look-back, the count from the ballots
+  constexpr int U2 = kCmpRegChunks;
   uint64_t bm[U2];
   double vv[U2];
   int64_t n = 0;
-  if (regs) {
 #pragma unroll
-    for (int u = 0; u < U2; ++u) {
-      const int64_t b = 64 * u + lane;
-      const bool in = b < nb;
-      vv[u] = in ? out_val[g * nb + b] : 0.0;
-      bm[u] = __ballot(in && em[b]);
-      n += __popcll(bm[u]);
-    }
-  } else {
-    n = compact_count(em, nb, lane);
+  for (int u = 0; u < U2; ++u) {
+    const int64_t b = 64 * u + lane;
+    const bool in = b < nb;
+    vv[u] = in ? out_val[g * nb + b] : 0.0;
+    bm[u] = __ballot(in && em[b]);
+    n += __popcll(bm[u]);
   }
   const uint64_t tag = (uint64_t)epoch << kCmpEpochShift;
   if (lane == 0)
@@ -1938,49 +2037,20 @@ __global__ __launch_bounds__(256) void k_compact1(
           err_word, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (regs) {
-    int64_t pos = prefix;
-#pragma unroll
-    for (int u = 0; u < U2; ++u) {
-      const int64_t b = 64 * u + lane;
-      const uint64_t m = bm[u];
-      if ((m >> lane) & 1) {
-        const int64_t p = pos + __popcll(m & ((1ULL << lane) - 1));
-        if (p < cap) {
-          r_ts[p] = bucket_ts(P, b);
-          r_val[p] = __double_as_longlong(vv[u]);
-          r_isint[p] = 0;  // downsampled values are doubles
-        }
-      }
-      pos += __popcll(m);
-    }
-    return;
-  }
-  constexpr int U = 8;
   int64_t pos = prefix;
-  for (int64_t c0 = 0; c0 < nb; c0 += 64 * U) {
-    bool e[U];
-    double v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t b = c0 + 64 * u + lane;
-      e[u] = b < nb && em[b];
-      v[u] = b < nb ? out_val[g * nb + b] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t b = c0 + 64 * u + lane;
-      const uint64_t m = __ballot(e[u]);
-      if (e[u]) {
-        const int64_t p = pos + __popcll(m & ((1ULL << lane) - 1));
-        if (p < cap) {
-          r_ts[p] = bucket_ts(P, b);
-          r_val[p] = __double_as_longlong(v[u]);
-          r_isint[p] = 0;  // downsampled values are doubles
-        }
+  for (int u = 0; u < U2; ++u) {
+    const int64_t b = 64 * u + lane;
+    const uint64_t m = bm[u];
+    if ((m >> lane) & 1) {
+      const int64_t p = pos + __popcll(m & ((1ULL << lane) - 1));
+      if (p < cap) {
+        r_ts[p] = bucket_ts(P, b);
+        r_val[p] = __double_as_longlong(vv[u]);
+        r_isint[p] = 0;  // downsampled values are doubles
       }
-      pos += __popcll(m);
     }
+    pos += __popcll(m);
   }
 }
 
