@@ -149,6 +149,13 @@ bool launch_ds(DsKernel k, const DsLaunch& a) {
                            dim3(OTSDB_PREP_TPB), 0,
                            a.st, a.P, a.B, a.SM, a.NW, a.WB, a.wc);
       return true;
+    case DS_PREP_FOLD:
+      if (a.NW > 1 && S > 0)
+        hipLaunchKernelGGL(k_prep_fold<M>,
+                           dim3(ds_blocks(S * (a.NW - 1), OTSDB_PREP_TPB)),
+                           dim3(OTSDB_PREP_TPB), 0, a.st, a.P, a.B, a.SM,
+                           a.err, a.NW, a.WB, a.wc);
+      return true;
     case DS_FOLD:
       return with_monoid(a.agg_id, [&](auto tag) {
         using A = decltype(tag);

@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -126,6 +127,18 @@ constexpr int64_t kOrderedChunkMerged = 16384;
 #define OTSDB_FOLD_MIN_WINDOW 128
 #endif
 constexpr int64_t kFoldMinBlocks = OTSDB_FOLD_MIN_BLOCKS;
+// up to this many (series, window boundary) pairs k_prep and k_fold_prep run
+// as one launch (each pair's thread finds its series' bounds again: cheap
+// next to a launch on small queries, not on the named query's 400,000)
+#ifndef OTSDB_PREP_FOLD_MAX
+#define OTSDB_PREP_FOLD_MAX 65536
+#endif
+// (the environment's OTSDB_PREP_FOLD_MAX overrides it: the tests run both
+// forms on one process)
+int64_t prep_fold_max() {
+  const char* e = getenv("OTSDB_PREP_FOLD_MAX");
+  return e ? atoll(e) : (int64_t)OTSDB_PREP_FOLD_MAX;
+}
 constexpr int64_t kFoldMinWindow = OTSDB_FOLD_MIN_WINDOW;
 
 // the storage rows cannot be taken verbatim (run_raw_verbatim): flagged on
@@ -176,6 +189,10 @@ struct otsdb_ctx {
   int* d_err = nullptr;                 // device error word
   unsigned long long* d_mm = nullptr;   // k_bounds min/max
   int64_t* h_small = nullptr;           // pinned readback
+  // {error word, total points} of the last compaction, written by the
+  // kernel straight into host memory (coherent, mapped): no read-back copy
+  int64_t* h_done = nullptr;
+  int64_t* d_done = nullptr;            // its device address
   // tile plan cache (keyed by the group offsets)
   std::vector<int64_t> goff_cache;
   int64_t* d_tiles = nullptr;
@@ -999,6 +1016,11 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
             a.WB = WB;
             launch_cells<M>(DS_CELLS_FOLD_PREP, a);
           }
+        } else if (NW > 1 && S * (NW - 1) <= prep_fold_max()) {
+          a.wc = wc;
+          a.NW = NW;
+          a.WB = WB;
+          launch_ds<M>(DS_PREP_FOLD, a);
         } else {
           launch_ds<M>(DS_PREP, a);
           if (NW > 1) {
@@ -1238,7 +1260,7 @@ otsdb_status compact(otsdb_ctx* c, const Params& P, int64_t G,
   // and always one ticket slot on from the last call's (k_compact1)
   c->cmp_epoch = c->cmp_epoch + 1 == (1u << 24) ? 4u : c->cmp_epoch + 1;
   unsigned long long* ticket = (unsigned long long*)((char*)c->d_err + 192);
-  int64_t* small = (int64_t*)((char*)c->d_err + 128);
+  int64_t* small = c->d_done;
   // few groups (C1's 100): one group (wavefront) per block, spread over more
   // CUs; many (C2's 10k): four per block (one wave per block ran C2's
   // compaction 0.20 -> 0.27 ms)
@@ -1270,11 +1292,12 @@ otsdb_status compact(otsdb_ctx* c, const Params& P, int64_t G,
 otsdb_status finish(otsdb_ctx* c, int64_t G, otsdb_result* out) {
   hipStream_t st = c->stream;
   if (c->small_ready) {
-    // k_compact1 left {error word, total} side by side and zeroed the word
+    // the compaction left {error word, total} in host memory and zeroed the
+    // word (one synchronisation, no copy launch)
     c->small_ready = false;
-    HIP_TRY(hipMemcpyAsync(&c->h_small[0], (char*)c->d_err + 128,
-                           2 * sizeof(int64_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    c->h_small[0] = __atomic_load_n(&c->h_done[0], __ATOMIC_ACQUIRE);
+    c->h_small[1] = __atomic_load_n(&c->h_done[1], __ATOMIC_ACQUIRE);
     c->err_clean = true;
   } else {
     HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
@@ -2438,6 +2461,9 @@ otsdb_status otsdb_ctx_create(int device, otsdb_ctx** out) {
   HIP_TRY(hipMemset(c->d_err, 0, 256));
   c->d_mm = (unsigned long long*)((char*)c->d_err + 64);
   HIP_TRY(hipHostMalloc(&c->h_small, 64));
+  HIP_TRY(hipHostMalloc(&c->h_done, 64,
+                        hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_TRY(hipHostGetDevicePointer((void**)&c->d_done, c->h_done, 0));
   *out = c;
   return OTSDB_OK;
 }
@@ -2466,6 +2492,7 @@ void otsdb_ctx_destroy(otsdb_ctx* c) {
   if (c->d_err) hipFree(c->d_err);
   for (auto e : c->ev_pool) hipEventDestroy(e);
   if (c->h_small) hipHostFree(c->h_small);
+  if (c->h_done) hipHostFree(c->h_done);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }

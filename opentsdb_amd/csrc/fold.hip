@@ -75,19 +75,13 @@ constexpr int32_t kProgDone = INT32_MAX;
 
 // k_fold_prep: one thread per (series, inner boundary).  The boundary
 // buckets' values are folded sequentially (Java order) from the points.
+// (series s, boundary j) given the series' k_prep bounds
 template <class M>
-__global__ __launch_bounds__(256) void k_fold_prep(Params P, BatchDev B,
-                                                   SeriesMeta SM, int64_t NW,
-                                                   int64_t WB,
-                                                   WinCtx* __restrict__ wc) {
-  const int64_t nbd = NW - 1;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t s = idx / nbd;
-  if (s >= B.S) return;
-  const int64_t j = idx - s * nbd + 1;
+DEV void fold_prep_one(const Params& P, const BatchDev& B, int64_t s,
+                       int64_t j, int64_t nbd, int64_t WB, bool keep,
+                       int64_t lo_s, int64_t hi_s, WinCtx* __restrict__ wc) {
   WinCtx c{0, INT64_MIN, 0.0, INT64_MIN, 0.0};
-  const bool keep = SM.keep[s];
-  const int64_t lo = keep ? SM.lo[s] : 0, hi = keep ? SM.hi[s] : 0;
+  const int64_t lo = keep ? lo_s : 0, hi = keep ? hi_s : 0;
   if (lo >= hi) {
     c.bnd = lo;
     wc[s * nbd + j - 1] = c;
@@ -161,6 +155,40 @@ __global__ __launch_bounds__(256) void k_fold_prep(Params P, BatchDev B,
     c.next_val = st.finish(&err);
   }
   wc[s * nbd + j - 1] = c;
+}
+
+template <class M>
+__global__ __launch_bounds__(256) void k_fold_prep(Params P, BatchDev B,
+                                                   SeriesMeta SM, int64_t NW,
+                                                   int64_t WB,
+                                                   WinCtx* __restrict__ wc) {
+  const int64_t nbd = NW - 1;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t s = idx / nbd;
+  if (s >= B.S) return;
+  const bool keep = SM.keep[s];
+  fold_prep_one<M>(P, B, s, idx - s * nbd + 1, nbd, WB, keep, SM.lo[s],
+                   SM.hi[s], wc);
+}
+
+// k_prep and k_fold_prep in one launch for small queries (C1: 1,000 series
+// x 7 boundaries; one launch and one dependent round of SeriesMeta loads
+// fewer): every (series, boundary) thread finds the series' bounds itself,
+// the series' first thread also does the rest of k_prep
+template <class M>
+__global__ __launch_bounds__(256) void k_prep_fold(Params P, BatchDev B,
+                                                   SeriesMeta SM, int* err_word,
+                                                   int64_t NW, int64_t WB,
+                                                   WinCtx* __restrict__ wc) {
+  const int64_t nbd = NW - 1;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t s = idx / nbd;
+  if (s >= B.S) return;
+  const int64_t j0 = idx - s * nbd;
+  bool keep;
+  int64_t lo, hi;
+  prep_series<M>(P, B, SM, err_word, s, j0 == 0, &keep, &lo, &hi);
+  fold_prep_one<M>(P, B, s, j0 + 1, nbd, WB, keep, lo, hi, wc);
 }
 
 // One wavefront's view of the fold (wave-uniform except the pointers).

@@ -101,7 +101,8 @@ enum DsKernel {
   DS_CELLS_FOLD_PREP, // k_cells_fold_prep: window boundaries of a cells fold
   DS_CELLS_FOLD2, // the cells fold of a batch whose kept series all have
                   // 2-byte qualifiers (the width a compile-time constant)
-  DS_CELLS_FOLD4  // ... all 4-byte ones
+  DS_CELLS_FOLD4, // ... all 4-byte ones
+  DS_PREP_FOLD    // k_prep_fold: k_prep + k_fold_prep in one launch
 };
 
 struct DsLaunch {
