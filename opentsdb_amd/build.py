@@ -90,7 +90,7 @@ def build(force=False, verbose=False, jobs=None, defines=(), out=None):
     # sources only engine.hip includes (ds_tu.hip's include graph:
     # kernels.hip, decode.hip, fold.hip, cellfold.hip and the headers)
     engine_only = ("engine.hip", "select.hip", "raw.hip", "rows.hip",
-                   "calendar.hip")
+                   "calendar.hip", "compact.hip")
 
     def stale(u):
         src, extra, obj = u

@@ -24,6 +24,7 @@
 
 #include "../../include/otsdb_agg.h"
 #include "kernels.hip"
+#include "compact.hip"
 #include "select.hip"
 #include "decode.hip"
 #include "raw.hip"
@@ -1243,13 +1244,12 @@ otsdb_status compact(otsdb_ctx* c, const Params& P, int64_t G,
   }
   StageTimer tm(c, 4);
   // grids of up to kCmpRegBuckets: one pass (k_compact1: count, look-back
-  // scan, scatter); longer: k_compact_count + k_compact_scatter.  Either way
-  // the call's {error word, total} lands in `small` for finish's read-back.
-  // Scratch: flags [G] (one pass) or counts [G] + 64-group tile words
-  const size_t n_tiles = (size_t)((G + 63) >> 6);
+  // scan, scatter); longer: k_compact_count, k_scan, k_compact_scatter.
+  // Either way the call's {error word, total} lands in `small` (mapped host
+  // memory) for finish.  Scratch: flags [G] (one pass) or counts [G]
   void* p = c->cmp_flags;
   size_t cap = c->cmp_flags_cap;
-  const size_t need = (size_t)G * 8 + n_tiles * 8 + 256;
+  const size_t need = (size_t)G * 8 + 256;
   const bool grow = need > cap;
   otsdb_status rc = ensure(&p, &cap, need);
   c->cmp_flags = p;
@@ -1273,15 +1273,16 @@ otsdb_status compact(otsdb_ctx* c, const Params& P, int64_t G,
                        out->is_int, c->d_err, small);
   } else {
     int64_t* cnt = (int64_t*)p;
-    unsigned long long* tw = (unsigned long long*)((char*)p + (size_t)G * 8);
     hipLaunchKernelGGL(k_compact_count, dim3(blocks_for(G, gpb)),
-                       dim3(64 * gpb), 0, st, P, G, out_emit, cnt, tw,
-                       ticket, c->cmp_epoch);
+                       dim3(64 * gpb), 0, st, P, G, out_emit, cnt, ticket,
+                       c->cmp_epoch);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, G,
+                       (const int64_t*)cnt, out->offsets);
     hipLaunchKernelGGL(k_compact_scatter, dim3(blocks_for(G, gpb)),
                        dim3(64 * gpb), 0, st, P, G, out_val, out_emit,
-                       (const int64_t*)cnt, (const unsigned long long*)tw,
-                       out->offsets, out->capacity, out->ts, out->val,
-                       out->is_int, c->d_err, small);
+                       (const int64_t*)cnt, (const int64_t*)out->offsets,
+                       out->capacity, out->ts, out->val, out->is_int,
+                       c->d_err, small);
   }
   HIP_TRY(hipGetLastError());
   c->small_ready = true;

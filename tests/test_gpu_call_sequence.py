@@ -119,6 +119,27 @@ def test_one_and_two_pass_compactions_alternate(engine):
                     where="alt%d/%s" % (k, interval))
 
 
+def test_long_grid_dense_and_sparse_groups(engine):
+    """Grids past 2,048 buckets compact in three launches; a group whose
+    every bucket is emitted (FillingDownsampler) takes the scatter's straight
+    copy, the others the flag-driven one; is_int is zeroed over each group's
+    range by wide stores.  Host and device entries, and a device result one
+    point short of the total."""
+    hb = datasets.random_batch(308, n_series=24, n_groups=4)
+    end = datasets.T0 + 8 * 3600 * 1000
+    for fill in ("zero", "none"):
+        spec = _spec("sum", "sum", fill=fill, interval="10s", end=end)
+        ref = pyoracle.group_by(spec, hb)
+        compare(engine.run(spec, hb), ref, False, where="host/" + fill)
+        got = _run_device(engine, spec, _device(hb))
+        compare(got, ref, False, where="device/" + fill)
+        for g in got:
+            assert not np.any(g.is_int)
+        total = sum(len(g) for g in ref)
+        with pytest.raises(core.OpenTSDBException):
+            _run_device(engine, spec, _device(hb), cap=total - 1)
+
+
 def test_short_result_then_good(engine):
     """A device result too small (E_CAPACITY: nothing written past it, the
     error word and look-back state left consistent), then the same query with
