@@ -266,6 +266,7 @@ __global__ __launch_bounds__(256) void k_compact1(
           err_word, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  zero_bytes(r_isint, prefix, prefix + n, cap, lane);
   int64_t pos = prefix;
 #pragma unroll
   for (int u = 0; u < U2; ++u) {
@@ -276,7 +277,6 @@ __global__ __launch_bounds__(256) void k_compact1(
       if (p < cap) {
         r_ts[p] = bucket_ts(P, b);
         r_val[p] = __double_as_longlong(vv[u]);
-        r_isint[p] = 0;  // downsampled values are doubles
       }
     }
     pos += __popcll(m);
