@@ -159,10 +159,19 @@ bool launch_ds(DsKernel k, const DsLaunch& a) {
     case DS_FOLD:
       return with_monoid(a.agg_id, [&](auto tag) {
         using A = decltype(tag);
+        // member contexts preloaded into LDS only while the workgroup stays
+        // within 40 KB (4 a CU: C2's 2,017-bucket windows leave room for 10)
+        Params P = a.P;
+        size_t lds = fold_lds_bytes<A>(P);
+        if (P.fold_ctx > 0 && lds + (size_t)P.fold_ctx * sizeof(FoldMember) <=
+                                  kFoldDynBudget)
+          lds += (size_t)P.fold_ctx * sizeof(FoldMember);
+        else
+          P.fold_ctx = 0;
         hipLaunchKernelGGL((k_fold<M, A, 8>),
                            dim3((unsigned)(a.n_tiles * a.NW)), dim3(256),
-                           (unsigned)fold_lds_bytes<A>(a.P),
-                           a.st, a.P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
+                           (unsigned)lds,
+                           a.st, P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
                            a.tm1, a.single, a.members, a.wc, a.NW, a.partial,
                            a.tile_emit, a.out_val, a.out_emit, a.err,
                            a.always_partial, a.cf);

@@ -105,6 +105,9 @@ constexpr int64_t kChunk = 256;  // series per cross-series chunk
 #define OTSDB_FOLD_CHUNK 32
 #endif
 constexpr int64_t kFoldChunk = OTSDB_FOLD_CHUNK;
+#ifndef OTSDB_FOLD_CTX  // tuning builds: 0 = no preloaded member contexts
+#define OTSDB_FOLD_CTX 1
+#endif
 // Order-sensitive aggregators whose merge of partial states is
 // ill-conditioned (dev: Chan's merge of Welford runs over offset data lands
 // ~1e-11 from the reference's one sequential pass, Aggregators.java:547-568)
@@ -889,6 +892,16 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   if (rc) return rc;
   const Tiles T = tiles_of(c, G);
   P.fold_wb = 0;  // (P may come from an earlier pipeline run)
+  P.fold_ctx = 0;
+  if (fold && OTSDB_FOLD_CTX) {
+    // tiles of up to 64 members load every member context at workgroup
+    // start (k_fold; ds_tu.hip drops it when the LDS would cost occupancy)
+    int64_t tile_max = 0;
+    for (size_t g = 0; g + 1 < goff.size(); ++g)
+      tile_max = std::max(tile_max, goff[g + 1] - goff[g]);
+    tile_max = std::min(tile_max, ordered ? kOrderedFoldChunk : kFoldChunk);
+    if (tile_max > 0 && tile_max <= 64) P.fold_ctx = (int32_t)tile_max;
+  }
   // few tiles (small queries, e.g. C1's 100 groups of 10 series): narrower
   // fold windows give the grid more workgroups — each window's workgroup
   // streams only that window's points (k_fold_prep hands it the context)

@@ -381,6 +381,9 @@ struct FoldMember {
   double py, ny;
   int32_t kept, sf, has_prev, has_next;
 };
+// the dynamic LDS a k_fold workgroup may take and still run 4 to a CU (160 KB)
+// beside its static arrays (rings, marks, contexts: ~5.6 KB)
+constexpr size_t kFoldDynBudget = 40960 - 6144;
 
 template <class A>
 DEV void fold_member_init(const Params& P, FoldSink<A>& F,
@@ -642,6 +645,53 @@ __global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
   if (CELLS && s_next < 0) return;  // (block-uniform)
   int dbg_n = 0;
   FoldSink<A> F{st, emit, ring[w], prog, err_word, 0, 0, W0, W1, W0, -1, 0, 0.0};
+  // a member's window context (k_prep / k_fold_prep's results for series s)
+  auto member_ctx = [&](int64_t s) {
+    const SeriesMeta& sm = kc.SM;
+    const int64_t nbd = kc.nbd, win = kc.win;
+    FoldMember m;
+    m.kept = sm.keep[s] != 0;
+    m.pa = m.kept ? sm.lo[s] : 0;
+    m.pb = m.kept ? sm.hi[s] : 0;
+    m.has_prev = m.has_next = 0;
+    m.px = m.nx = 0;
+    m.py = m.ny = 0.0;
+    if (win > 0) {
+      const WinCtx& c = kc.wc[s * nbd + win - 1];
+      m.pa = c.bnd;
+      if (c.prev_ts != INT64_MIN) {
+        m.has_prev = 1;
+        m.px = c.prev_ts;
+        m.py = c.prev_val;
+      }
+    }
+    if (win < nbd) {
+      const WinCtx& c = kc.wc[s * nbd + win];
+      m.pb = c.bnd;
+      if (c.next_ts != INT64_MIN) {
+        m.has_next = 1;
+        m.nx = c.next_ts;
+        m.ny = c.next_val;
+      }
+    }
+    if (!m.has_next && sm.of_has[s]) {  // toward the point past the grid
+      m.has_next = 1;
+      m.nx = sm.of_ts[s];
+      m.ny = sm.of_val[s];
+    }
+    m.sf = kc.series_float ? (int)kc.series_float[s] : 1;
+    return m;
+  };
+  // tiles of at most P.fold_ctx members (the host sized the dynamic LDS for
+  // them): every context loaded here at once — two dependent load rounds per
+  // workgroup instead of two per member on the path of each wavefront
+  const int64_t n_mem = kc.m1 - kc.m0;
+  const bool ctx_on = !CELLS && P.fold_ctx > 0 && n_mem <= P.fold_ctx;
+  FoldMember* ctx = reinterpret_cast<FoldMember*>(fold_dyn + fold_lds_bytes<A>(P));
+  if (ctx_on) {
+    for (int64_t j = tid; j < n_mem; j += 256) ctx[j] = member_ctx(kc.members[kc.m0 + j]);
+    __syncthreads();
+  }
   for (;;) {
     int i = 0;
     if (lane == 0) i = atomicAdd(&s_next, 1);
@@ -651,44 +701,14 @@ __global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
     FOLD_GUARD(dbg_n, 1 << 20, err_word, "claim loop i=%d\n", i)
     F.mi = i;
     F.eff = 0;
-    // the member's window context, lane 0 -> LDS
-    if (lane == 0) {
-      const SeriesMeta& sm = kc.SM;
+    // the member's window context, lane 0 -> LDS (preloaded: a copy)
+    if (lane == 0 && ctx_on) {
+      mc[w] = ctx[i];
+    } else if (lane == 0) {
       const int64_t s = kc.members[m0 + i];
-      const int64_t nbd = kc.nbd, win = kc.win;
-      FoldMember m;
-      m.kept = sm.keep[s] != 0;
-      m.pa = m.kept ? sm.lo[s] : 0;
-      m.pb = m.kept ? sm.hi[s] : 0;
-      m.has_prev = m.has_next = 0;
-      m.px = m.nx = 0;
-      m.py = m.ny = 0.0;
-      if (win > 0) {
-        const WinCtx& c = kc.wc[s * nbd + win - 1];
-        m.pa = c.bnd;
-        if (c.prev_ts != INT64_MIN) {
-          m.has_prev = 1;
-          m.px = c.prev_ts;
-          m.py = c.prev_val;
-        }
-      }
-      if (win < nbd) {
-        const WinCtx& c = kc.wc[s * nbd + win];
-        m.pb = c.bnd;
-        if (c.next_ts != INT64_MIN) {
-          m.has_next = 1;
-          m.nx = c.next_ts;
-          m.ny = c.next_val;
-        }
-      }
-      if (!m.has_next && sm.of_has[s]) {  // toward the point past the grid
-        m.has_next = 1;
-        m.nx = sm.of_ts[s];
-        m.ny = sm.of_val[s];
-      }
-      m.sf = kc.series_float ? (int)kc.series_float[s] : 1;
-      mc[w] = m;
+      mc[w] = member_ctx(s);
       if (CELLS) {
+        const int64_t nbd = kc.nbd, win = kc.win;
         CellsMember c;
         c.qb = CF.C.qual_off[CF.series_row[s]];
         c.vb0 = CF.C.val_off[CF.series_row[s]];

@@ -95,6 +95,10 @@ struct Params {
   // that does not follow its predecessor strictly (ERR_SPEC_MISS /
   // ERR_NOT_SORTED: the caller compacts and re-runs)
   int32_t check_order;
+  // k_fold: every member context of a tile (at most this many members) is
+  // loaded into LDS at workgroup start, all members at once; 0: each member
+  // loads its own when a wavefront claims it
+  int32_t fold_ctx;
 };
 
 // value bits of an absent bucket in sentinel rows: a signalling NaN, which
