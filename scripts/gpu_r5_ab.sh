@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 CFG=${CFG:-C5}
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for v in prod ${VARIANTS}; do
     lib=opentsdb_amd/_build/libotsdb_agg.so
     [ "$v" != prod ] && lib=opentsdb_amd/_build/var_$v/libotsdb_agg.so
