@@ -81,3 +81,17 @@ def test_fused_prep_seek_and_stop_inside_series(engine):
         compare(fused, ref, False, where="cut-fused")
         for a, b in zip(sep, fused):
             assert np.array_equal(a.bits, b.bits)
+
+
+@pytest.mark.parametrize("agg", ["dev", "sum", "max"])
+def test_wide_windows_without_preloaded_contexts(engine, agg):
+    """1,200 single-series groups on a 2,160-bucket grid: enough tiles that
+    the fold keeps full 2,048-bucket windows, whose states leave no LDS for
+    the preloaded member contexts (ds_tu.hip drops them: each member loads
+    its own), next to the small-window queries above that preload them."""
+    hb = datasets.random_batch(403, n_series=1200, n_groups=1200,
+                               cadence_ms=60000)
+    spec = _spec(agg, "avg", interval="5s")
+    ref = pyoracle.group_by(spec, hb)
+    got = engine.run(spec, hb)
+    compare(got, ref, False, where="wide/" + agg)
