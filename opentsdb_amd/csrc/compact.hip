@@ -202,7 +202,7 @@ __global__ __launch_bounds__(256) void k_compact1(
   const int64_t nb = P.nb;
   const uint8_t* em = out_emit + g * nb;
   // grids of up to 2,048 buckets (C1's 1,440, C2's 2,017; the engine sends
-  // longer ones to the two-launch path above): every emit flag and value
+  // longer ones to the three-launch path above): every emit flag and value
   // read ONCE (lane = bucket, coalesced) and held in registers across the
   // look-back, the count from the ballots
   constexpr int U2 = kCmpRegChunks;
