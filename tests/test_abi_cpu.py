@@ -104,3 +104,26 @@ def test_rate_options_defaults():
     r = core.RateOptions()
     assert not r.isCounter() and r.getCounterMax() == 2**63 - 1
     assert r.getResetValue() == 0 and not r.getDropResets()
+
+
+def test_run_device_struct_cache():
+    """run_device reuses the batch / result ctypes structs while the same
+    tensors stay attached (engine._abi_cached), and rebuilds them when a
+    tensor is replaced or the group offsets are written in place."""
+    import torch
+    from opentsdb_amd import engine as E
+    z = lambda n, d=torch.int64: torch.zeros(n, dtype=d)
+    db = E.DeviceBatch(z(5), z(40), z(40), z(3), z(4),
+                       is_float=z(40, torch.uint8))
+    get = lambda: E._abi_cached(db, E._BATCH_TENSORS, db.as_abi,
+                                db.group_offsets._version)
+    b1 = get()
+    assert get() is b1
+    assert b1.ts_ms == db.ts.data_ptr() and b1.n_points == 40
+    db.group_offsets.add_(1)          # in place: the host copy is re-read
+    b2 = get()
+    assert b2 is not b1
+    assert list(db._goff_host()) == [1, 1, 1]
+    db.val = z(40)                    # replaced
+    b3 = get()
+    assert b3 is not b2 and b3.val == db.val.data_ptr()
