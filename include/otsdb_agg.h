@@ -511,6 +511,14 @@ otsdb_status otsdb_prof_enable(otsdb_ctx* ctx, int enable);
 otsdb_status otsdb_prof_read(otsdb_ctx* ctx, double* ms, int64_t* launches,
                              int n, int reset);
 
+/* ---- diagnostics ---------------------------------------------------------
+ * Counters since the context was created (no reference counterpart: the
+ * operator's view of which cells-fold kernel ran): out[0] cells folds run
+ * with the uniform kernel (every kept series one value type and width),
+ * out[1] with the general one, out[2] uniform folds that met a qualifier of
+ * other flags and were re-run with the general kernel.                      */
+otsdb_status otsdb_ctx_counters(otsdb_ctx* ctx, int64_t* out, int n);
+
 /* ---- synthetic workload generator (bench / tests) ----------- */
 /* Generates the columnar batch of `n_series` series starting at global
  * series index `series0` directly in HBM.  Pass offsets=NULL first to get

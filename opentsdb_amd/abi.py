@@ -140,6 +140,7 @@ EXPORTS = [
     "otsdb_agg_partials_chained_device", "otsdb_agg_finalize_device",
     "otsdb_gen_counts_device",
     "otsdb_gen_fill_device", "otsdb_prof_enable", "otsdb_prof_read",
+    "otsdb_ctx_counters",
     "otsdb_decode_cells_device", "otsdb_sel_prepare_device",
     "otsdb_sel_hist_device", "otsdb_sel_hist_wait", "otsdb_sel_finish_device",
     "otsdb_encode_cells_device", "otsdb_agg_run_cells_device",
@@ -236,6 +237,8 @@ def load(path=None):
     lib.otsdb_prof_enable.restype = C.c_int
     lib.otsdb_prof_read.argtypes = [vp, vp, vp, C.c_int, C.c_int]
     lib.otsdb_prof_read.restype = C.c_int
+    lib.otsdb_ctx_counters.argtypes = [vp, vp, C.c_int]
+    lib.otsdb_ctx_counters.restype = C.c_int
     if path is None:
         _lib = lib
     return lib

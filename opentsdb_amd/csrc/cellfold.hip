@@ -216,6 +216,52 @@ __global__ __launch_bounds__(256) void k_cells_prep(Params P, CellsFold CF,
   store(true, lo, hi, rlo, vlo, qw, vl0, of_has, of_ts, of_val);
 }
 
+// ------------------------------------------------------------- uniform
+// k_cells_uniform: one wavefront per series, after k_cells_prep.  A kept
+// series is uniform when every row of it is one column of the series'
+// qualifier width whose value bytes add up to (points x the length its
+// first qualifier states) + the meta byte a multi-point column ends with
+// (CompactionQueue.java:594-616, read back by RowSeq.java:552-643): facts of
+// the row offsets alone, read coalesced 64 rows a pass — what compaction
+// writes for a series of one value type.  The uniform fold then needs no
+// value-length logic and no row-end checks per step; it verifies only that
+// each streamed qualifier carries the series' width and flags.  Any other
+// series (a row that does not add up, an illegal length, an empty row)
+// makes the engine launch the general fold for the batch, which decodes
+// point by point and raises the reference's errors.
+template <class M>
+__global__ __launch_bounds__(256) void k_cells_uniform(CellsFold CF, int64_t S,
+                                                       SeriesMeta SM) {
+  const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= S) return;
+  const int lane = LANE;
+  if (!SM.keep[s]) {
+    if (lane == 0) CF.uf[s] = 0xFF;
+    return;
+  }
+  const CellsDev& C = CF.C;
+  const int64_t r0 = CF.series_row[s], r1 = CF.series_row[s + 1];
+  const int qw = CF.qw[s], qsh = qw == 4 ? 2 : 1;
+  const uint32_t f = C.qual[C.qual_off[r0] + qw - 1] & 0xFu;
+  const int vl = (int)(f & 7) + 1;
+  const bool legal = (f & 8) ? (vl == 4 || vl == 8)
+                             : (vl == 1 || vl == 2 || vl == 4 || vl == 8);
+  const int vsh = vl == 1 ? 0 : (vl == 2 ? 1 : (vl == 4 ? 2 : 3));
+  bool bad = !legal;
+  for (int64_t r = r0 + lane; r < r1; r += 64) {
+    const int64_t ql = C.qual_off[r + 1] - C.qual_off[r];
+    const int64_t vb = C.val_off[r + 1] - C.val_off[r];
+    const int64_t n = ql >> qsh;
+    bad |= ql <= 0 || (ql & (qw - 1)) != 0 ||
+           vb != (n << vsh) + (n > 1 ? 1 : 0);
+  }
+  const bool ok = __ballot(bad) == 0;
+  if (lane == 0) {
+    CF.uf[s] = ok ? (uint8_t)f : (uint8_t)0xFF;
+    if (!ok) atomicOr(CF.wide, 4);
+  }
+}
+
 // ------------------------------------------------------------ fold prep
 // k_cells_fold_prep: one thread per (series, inner window boundary j) of a
 // grid wider than one fold window — k_fold_prep's WinCtx (the first point of
@@ -879,6 +925,322 @@ DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
   }
   if (fault) {
     // the query fails or is re-run by the generic decode; the member's
+    // remaining work is moot, the chain of progress marks must still end
+    if (lane == 0) atomicOr(F.err, fault);
+    return;
+  }
+  if (carry_key >= 0 && carry_key < P.nb && lane == 0)
+    S.put(carry_key, carry.finish(&err));
+  if (prev_hi >= 0) fold_flush(P, F, prev_hi + 1);
+  fold_member_tail(P, F, mc);
+}
+
+// The uniform cells fold: fold_member_cells for a series k_cells_uniform
+// proved uniform (every kept series of the batch is).  Each value is `vl`
+// bytes of one type, so a lane's values start at the stream cursor +
+// (its first point's index in the step << vsh) + the meta bytes of the rows
+// before it, lengths need no speculation and no prefix sums, and the rows'
+// value bytes add up by construction: no row-start / row-end cursor checks,
+// no value-length legality per step.  What a step still does: the row window
+// (first points with the meta byte before each row packed into bit 31, base
+// times), the qualifier -> time decode, one packed compare per 4 qualifier
+// bytes that every streamed qualifier has the series' width and flags (a
+// miss — a column whose lengths add up by accident — raises
+// ERR_CELLS_NONUNI and the engine folds the batch again with the general
+// kernel), the value extraction and the shared reduction.
+// Reference: RowSeq.java:552-643, Internal.java:621-690.
+template <int VL, int FL, int K>
+DEV void cells_vload_u(const uint8_t* vp, int32_t a, bool near, int32_t vlim,
+                       uint32_t* d) {
+  // the lane's K values plus the one meta byte it may skip: VL*K + 1 bytes
+  constexpr int NB = VL * K + 1;
+  constexpr int ND = (NB + 3) / 4;
+  if (near) {
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int32_t x = a + 4 * i + b;
+        w |= (x < vlim ? (uint32_t)vp[x] : 0u) << (8 * b);
+      }
+      d[i] = w;
+    }
+    return;
+  }
+  const uint8_t* s = vp + (uint32_t)a;
+  if (VL >= 2) {
+#pragma unroll
+    for (int i = 0; i < (VL * K) / 16; ++i) {
+      const uint4 w = *reinterpret_cast<const uint4*>(s + 16 * i);
+      d[4 * i] = w.x; d[4 * i + 1] = w.y; d[4 * i + 2] = w.z; d[4 * i + 3] = w.w;
+    }
+  } else {
+    const uint2 w = *reinterpret_cast<const uint2*>(s);
+    d[0] = w.x; d[1] = w.y;
+  }
+  d[ND - 1] = *reinterpret_cast<const uint32_t*>(s + 4 * (ND - 1));
+}
+
+template <class M, class A, int K, int QW>
+DEV void fold_member_cells_u(const Params& P, const CellsDev& C, FoldSink<A>& F,
+                             const FoldMember* mc, const CellsMember* cm) {
+  constexpr int PTS = 64 * K;
+  constexpr int32_t BIG = 0x40000000;  // first point of rows past the series
+  constexpr int qsh = QW == 4 ? 2 : 1;
+  static_assert(K == 8 && (QW == 2 || QW == 4), "8 points per lane, QW 2 / 4");
+  const int lane = LANE;
+  const bool kept = uni(mc->kept) != 0;
+  fold_member_init(P, F, mc);
+  if (!kept) return;
+  const int32_t pe = (int32_t)uni(mc->pb);
+  const int64_t r1 = uni(cm->r1);
+  const int64_t qb = uni(cm->qb), vb0 = uni(cm->vb0);
+  const uint8_t* qp = C.qual + qb;
+  const uint8_t* vp = C.val + vb0;
+  const int64_t ql64 = uni(cm->qend) - qb, vl64 = uni(cm->vend) - vb0;
+  const int32_t qlim = ql64 > INT32_MAX ? INT32_MAX : (int32_t)ql64;
+  const int32_t vlim = vl64 > INT32_MAX ? INT32_MAX : (int32_t)vl64;
+  int32_t vcur = (int32_t)(uni(cm->vcur) - vb0);
+  int64_t ra = uni(cm->rlo);
+  const uint32_t f = (uint32_t)uni(cm->uf) & 0xFu;
+  const int vl = (int)(f & 7) + 1, fl = (f & 8) ? 1 : 0;
+  const int vsh = vl == 1 ? 0 : (vl == 2 ? 1 : (vl == 4 ? 2 : 3));
+  // the packed check.  QW 2: a dword is two big-endian qualifiers b0 b1 |
+  // b2 b3; width: b0 / b2's high nibble is not 0xF (+0x10 carries into bit
+  // 8 / 24 only from 0xF0); flags: b1 / b3's low nibble is f.  QW 4: one
+  // qualifier b0..b3; b0's high nibble 0xF, b3's low nibble f.
+  const uint32_t fpat = QW == 2 ? (f << 8) | (f << 24) : (f << 24) | 0xF0u;
+  RowSink S{nullptr, nullptr, F.ring, FOLD_WIN - 1, 0, 0, 0, 0};
+  const BatchDev Bd{0, nullptr, nullptr, nullptr, nullptr, nullptr};
+  int err = 0;
+  int carry_key = INT32_MIN;
+  M carry = M::init();
+  int32_t prev_hi = -1;
+  int fault = 0;  // ERR_CELLS_NONUNI / ERR_NOT_SORTED / ERR_INTERNAL
+  // row window, row mb + lane: first point | (meta byte before the row) << 31,
+  // base time (ms since the grid base, mod 2^32)
+  int64_t mb = -(int64_t)BIG;
+  int32_t w_ps = 0, w_br = 0;
+  const int64_t gbase = P.gbase;
+  auto load_window = [&](int64_t m) {
+    mb = m;
+    const int64_t x = m + lane;
+    int32_t ps = BIG, br = 0;
+    if (x <= r1) {
+      ps = (int32_t)((C.qual_off[x] - qb) >> qsh);
+      if (x < r1) br = (int32_t)(uint32_t)(C.row_base_s[x] * 1000 - gbase);
+    }
+    // the previous row's first point (wave_shr:1; lane 0's row is the
+    // cursor's own, whose meta byte before it is never read)
+    const int32_t pp = dpp32<0x138, 0xF>(ps, ps);
+    const int32_t meta = (ps != BIG && ps - pp > 1) ? 1 : 0;
+    w_ps = (int32_t)((uint32_t)ps | ((uint32_t)meta << 31));
+    w_br = br;
+  };
+  int32_t p = (int32_t)uni(mc->pa);
+  const int32_t pa0 = p;
+  uint32_t t_last_prev = 0;  // check_order: the previous step's last time
+  const int32_t n_guard = pe - p + 64;  // every step consumes >= 1 point
+  int dbg_n = 0;
+  while (p < pe) {
+    FOLD_GUARD(dbg_n, n_guard, F.err, "uniform cells stream mi=%d p=%d pe=%d\n",
+               F.mi, p, pe)
+    if (ra < mb || ra + 3 >= mb + 64) load_window(ra);
+    const int j0 = (int)(ra - mb);
+    const uint32_t x1 = (uint32_t)__builtin_amdgcn_readlane(w_ps, j0 + 1);
+    const uint32_t x2 = (uint32_t)__builtin_amdgcn_readlane(w_ps, j0 + 2);
+    const uint32_t x3 = (uint32_t)__builtin_amdgcn_readlane(w_ps, j0 + 3);
+    const int32_t ps1 = (int32_t)(x1 & 0x7FFFFFFFu);
+    const int32_t ps2 = (int32_t)(x2 & 0x7FFFFFFFu);
+    const int32_t ps3 = (int32_t)(x3 & 0x7FFFFFFFu);
+    const int32_t m0 = (int32_t)(x1 >> 31), m1 = (int32_t)(x2 >> 31),
+                  m2 = (int32_t)(x3 >> 31);
+    // the step: at most three rows, every row wholly inside it >= K points
+    int32_t sb = p + PTS < pe ? p + PTS : pe;
+    if (ps2 <= sb && ps2 - ps1 < K) sb = ps1;
+    else if (ps3 <= sb && ps3 - ps2 < K) sb = ps2;
+    if (sb > ps3) sb = ps3;
+    if (sb <= p) {  // the row of p is not ra: an engine invariant broke
+      fault |= ERR_INTERNAL;
+      break;
+    }
+    const bool full = sb - p == PTS;  // (wave-uniform) every lane holds K points
+    const uint32_t rb0 = (uint32_t)__builtin_amdgcn_readlane(w_br, j0);
+    const uint32_t rb1 = (uint32_t)__builtin_amdgcn_readlane(w_br, j0 + 1);
+    const uint32_t rb2 = (uint32_t)__builtin_amdgcn_readlane(w_br, j0 + 2);
+    const uint32_t rb3 = (uint32_t)__builtin_amdgcn_readlane(w_br, j0 + 3);
+    // ---- this lane's points p0 .. p0 + nv - 1: its row, the boundary it
+    // may cross before point jb, the meta byte there
+    const int32_t p0 = p + K * lane;
+    const int32_t rem = sb - p0;
+    const int nv = rem < 0 ? 0 : (rem > K ? K : rem);
+    const bool c1 = p0 >= ps1, c2 = p0 >= ps2;
+    const int32_t nbnd = c2 ? ps3 : (c1 ? ps2 : ps1);
+    const int jb = nbnd - p0 < K ? nbnd - p0 : K;
+    const int32_t mnext = c2 ? m2 : (c1 ? m1 : m0);
+    const int32_t mbefore = (c1 ? m0 : 0) + (c2 ? m1 : 0);
+    const uint32_t bcur = c2 ? rb2 : (c1 ? rb1 : rb0);
+    const uint32_t bnext = c2 ? rb3 : (c1 ? rb2 : rb1);
+    // ---- loads: qualifiers, then values (the lane's K values from its
+    // row's cursor; lanes past the step load inside the pools too)
+    uint32_t dq[QW == 4 ? 8 : 4];
+    if (((p + PTS) << qsh) + 32 <= qlim) {
+      const uint32_t qoff = (uint32_t)p0 << qsh;
+      const uint4 w = *reinterpret_cast<const uint4*>(qp + qoff);
+      dq[0] = w.x; dq[1] = w.y; dq[2] = w.z; dq[3] = w.w;
+      if constexpr (QW == 4) {
+        const uint4 w2 = *reinterpret_cast<const uint4*>(qp + qoff + 16);
+        dq[4] = w2.x; dq[5] = w2.y; dq[6] = w2.z; dq[7] = w2.w;
+      }
+    } else {  // the end of the pool: byte loads, never past it
+      const int32_t qoff = nv > 0 ? p0 << qsh : 0;
+#pragma unroll
+      for (int i = 0; i < (QW == 4 ? 8 : 4); ++i) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int32_t x = qoff + 4 * i + b;
+          w |= (x < qlim ? (uint32_t)qp[x] : 0u) << (8 * b);
+        }
+        dq[i] = w;
+      }
+    }
+    const bool vnear = vcur + 9 * PTS + 128 > vlim;
+    const int32_t a0 = vcur + ((K * lane) << vsh) + mbefore;
+    uint32_t d[17];
+    switch (vsh) {
+      case 3: cells_vload_u<8, 0, K>(vp, a0, vnear, vlim, d); break;
+      case 2: cells_vload_u<4, 0, K>(vp, a0, vnear, vlim, d); break;
+      case 1: cells_vload_u<2, 0, K>(vp, a0, vnear, vlim, d); break;
+      default: cells_vload_u<1, 0, K>(vp, a0, vnear, vlim, d); break;
+    }
+#if defined(OTSDB_CELLS_ABL) && OTSDB_CELLS_ABL == 2  // timing: loads only
+    {
+      uint32_t x = 0;
+#pragma unroll
+      for (int i = 0; i < (QW == 4 ? 8 : 4); ++i) x ^= dq[i];
+#pragma unroll
+      for (int i = 0; i < 17; ++i) x ^= d[i];
+      if (x == 42) F.emit[0] = 1;
+      vcur += ((sb - p) << vsh) + (ps1 <= sb ? m0 : 0) + (ps2 <= sb ? m1 : 0) +
+              (ps3 <= sb ? m2 : 0);
+      ra += (ps1 <= sb ? 1 : 0) + (ps2 <= sb ? 1 : 0) + (ps3 <= sb ? 1 : 0);
+      p = sb;
+      continue;
+    }
+#endif
+    // ---- every streamed qualifier: the series' width and flags
+    uint32_t bad = 0;
+#pragma unroll
+    for (int i = 0; i < (QW == 4 ? 8 : 4); ++i) {
+      const uint32_t w = dq[i];
+      uint32_t b;
+      if constexpr (QW == 2) {
+        b = (((w & 0x00F000F0u) + 0x00100010u) & 0x01000100u) |
+            ((w & 0x0F000F00u) ^ fpat);
+        if (!full)
+          b &= (2 * i < nv ? 0x0000FFFFu : 0u) | (2 * i + 1 < nv ? 0xFFFF0000u : 0u);
+      } else {
+        b = (w & 0x0F0000F0u) ^ fpat;
+        if (!full) b = i < nv ? b : 0u;
+      }
+      bad |= b;
+    }
+#if defined(OTSDB_CELLS_ABL) && OTSDB_CELLS_ABL == 3  // timing: no check
+    if (bad == 0x12345678u) F.emit[1] = 1;
+#else
+    if (__ballot(bad != 0)) {
+      fault |= ERR_CELLS_NONUNI;
+      break;
+    }
+#endif
+    // ---- qualifiers -> grid-relative times
+    uint32_t t[K];
+    if constexpr (QW == 2) {
+#pragma unroll
+      for (int j = 0; j < K; j += 2) {  // bytes b0 b1 b2 b3 -> b1 b0 b3 b2
+        const uint32_t w = __builtin_amdgcn_perm(dq[j >> 1], dq[j >> 1], 0x02030001u);
+        t[j] = ((w >> 4) & 0xFFFu) * 1000u + (j >= jb ? bnext : bcur);
+        t[j + 1] = ((w >> 20) & 0xFFFu) * 1000u + (j + 1 >= jb ? bnext : bcur);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        t[j] = ((__builtin_bswap32(dq[j]) & 0x0FFFFFC0u) >> 6) +
+               (j >= jb ? bnext : bcur);
+    }
+    if (P.check_order) {
+      // verbatim storage rows: each point strictly after its predecessor
+      // (the lane before it; lane 0: the previous step's last point)
+      const uint32_t tp = (uint32_t)dpp32<0x138, 0xF>((int32_t)t_last_prev,
+                                                      (int32_t)t[K - 1]);
+      int ob = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        if (j < nv) ob |= (j == 0 ? (p0 > pa0 && t[0] <= tp) : t[j] <= t[j - 1]);
+      if (__ballot(ob)) {
+        fault |= ERR_NOT_SORTED;
+        break;
+      }
+    }
+    // ---- values (the boundary's meta byte skipped from point jb on)
+    int64_t v[K];
+    cells_vextract_vl<K>(vl, fl, d, jb, (uint32_t)mnext, v);
+    // ---- the downsample over [p, hs) (fold_member's ring bookkeeping)
+    const int32_t k_hi = bucket_rel(
+        P, full ? (uint32_t)__builtin_amdgcn_readlane((int32_t)t[K - 1], 63)
+                : cells_pick<K>(t, sb - 1 - p));
+    const bool carry_ok = carry_key >= 0 && carry_key < P.nb;
+    int32_t limit = carry_ok ? carry_key : prev_hi + 1;
+    int32_t hs = sb;
+    if (k_hi >= F.flushed + FOLD_WIN) {
+      const int32_t k_first = bucket_rel(P, cells_pick<K>(t, 0));
+      if (carry_ok && carry_key < k_first) {
+        if (lane == 0) S.put(carry_key, carry.finish(&err));
+        carry_key = INT32_MIN;
+        limit = k_first;
+      } else if (!carry_ok) {
+        limit = k_first;
+      }
+      fold_flush(P, F, limit);
+      if (k_hi >= F.flushed + FOLD_WIN) {
+        // the ring's end (k_hi lies past it, so inside the narrow grid)
+        const uint32_t T =
+            (uint32_t)((int64_t)(F.flushed + FOLD_WIN) * P.interval);
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) cnt += (j < nv && t[j] < T) ? 1 : 0;
+        hs = p + uni((int32_t)wave_sum(cnt));
+      }
+    }
+    const int32_t k_last =
+        hs == sb ? k_hi : bucket_rel(P, cells_pick<K>(t, hs - 1 - p));
+    if (P.check_order) t_last_prev = cells_pick<K>(t, hs - 1 - p);
+#if defined(OTSDB_CELLS_ABL) && OTSDB_CELLS_ABL == 1  // timing: no reduction
+    {
+      int64_t x = 0;
+#pragma unroll
+      for (int j = 0; j < K; ++j) x ^= t[j] + v[j];
+      if (x == 42) F.emit[0] = 1;
+    }
+#else
+    reduce_step<M, K, 1, uint32_t, 1>(P, Bd, 1, p, hs, p, p0, t, v, S, err,
+                                      carry_key, carry, hs < pe);
+#endif
+    vcur += ((hs - p) << vsh) + (ps1 <= hs ? m0 : 0) + (ps2 <= hs ? m1 : 0) +
+            (ps3 <= hs ? m2 : 0);
+    ra += (ps1 <= hs ? 1 : 0) + (ps2 <= hs ? 1 : 0) + (ps3 <= hs ? 1 : 0);
+    prev_hi = k_last;
+    {  // the buckets this step finished (the load registers are dead here)
+      const int32_t lim = (carry_key >= 0 && carry_key < P.nb) ? carry_key
+                                                                 : prev_hi + 1;
+      if (lim - F.flushed >= FOLD_FL) fold_flush(P, F, lim);
+    }
+    p = hs;
+  }
+  if (fault) {
+    // the query fails or is re-run by the general fold; the member's
     // remaining work is moot, the chain of progress marks must still end
     if (lane == 0) atomicOr(F.err, fault);
     return;

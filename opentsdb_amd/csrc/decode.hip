@@ -508,6 +508,10 @@ __global__ __launch_bounds__(256) void k_encode(
 // (Internal.extractDataPoints, Internal.java:307-321).
 // ------------------------------------------------------------------------
 enum : int { ERR_CELLS_GENERIC = 1 << 20 };
+// the uniform cells fold (fold_member_cells_u) met a qualifier whose flags
+// are not its series' one: the engine runs the batch's fold again with the
+// general kernel (which decodes mixed value lengths point by point)
+enum : int { ERR_CELLS_NONUNI = 1 << 24 };
 
 struct CellRow {
   const uint8_t* q;

@@ -93,6 +93,36 @@ bool launch_cells(DsKernel k, const DsLaunch& a) {
                            a.always_partial, a.cf);
         OTSDB_DBG(a.st, "k_fold<cells, qw 4>");
       });
+    case DS_CELLS_UNIFORM:
+      if (S > 0)
+        hipLaunchKernelGGL(k_cells_uniform<M>, dim3(ds_blocks(S, 4)), dim3(256),
+                           0, a.st, a.cf, S, a.SM);
+      OTSDB_DBG(a.st, "k_cells_uniform");
+      return true;
+    case DS_CELLS_FOLD4U:
+      return with_monoid(a.agg_id, [&](auto tag) {
+        using A = decltype(tag);
+        hipLaunchKernelGGL((k_fold<M, A, 8, 12>),
+                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(256),
+                           (unsigned)fold_lds_bytes<A>(a.P),
+                           a.st, a.P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
+                           a.tm1, a.single, a.members, a.wc, a.NW, a.partial,
+                           a.tile_emit, a.out_val, a.out_emit, a.err,
+                           a.always_partial, a.cf);
+        OTSDB_DBG(a.st, "k_fold<cells, qw 4, uniform>");
+      });
+    case DS_CELLS_FOLD2U:
+      return with_monoid(a.agg_id, [&](auto tag) {
+        using A = decltype(tag);
+        hipLaunchKernelGGL((k_fold<M, A, 8, 10>),
+                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(256),
+                           (unsigned)fold_lds_bytes<A>(a.P),
+                           a.st, a.P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
+                           a.tm1, a.single, a.members, a.wc, a.NW, a.partial,
+                           a.tile_emit, a.out_val, a.out_emit, a.err,
+                           a.always_partial, a.cf);
+        OTSDB_DBG(a.st, "k_fold<cells, qw 2, uniform>");
+      });
     case DS_CELLS_FOLD2:
       return with_monoid(a.agg_id, [&](auto tag) {
         using A = decltype(tag);

@@ -207,6 +207,12 @@ struct otsdb_ctx {
   int64_t tiles_chunk = 0;
   int64_t tiles_whole = 0;
   bool verbatim = false;  // run_raw_verbatim: the cells query's rows as stored
+  // the cells fold's uniform kernel met a qualifier that is not its series'
+  // (ERR_CELLS_NONUNI): this call's next attempt takes the general kernel
+  bool cells_no_uni = false;
+  // otsdb_ctx_counters: cells folds launched uniform / general, uniform
+  // folds that missed (ERR_CELLS_NONUNI, re-run with the general kernel)
+  int64_t n_cells_uniform = 0, n_cells_general = 0, n_cells_uni_miss = 0;
   bool spec_miss = false;  // ... and they cannot be: the caller compacts
   bool result_short = false;  // the last E_CAPACITY was the result's (finish)
   std::mutex mu;  // one query at a time per context
@@ -960,6 +966,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       CF.vlo = cv.take<int64_t>(S);
       CF.qw = cv.take<uint8_t>(S);
       CF.vl0 = cv.take<uint8_t>(S);
+      CF.uf = cv.take<uint8_t>(S);
       if (NW > 1) {
         CF.wrlo = cv.take<int64_t>((size_t)S * (NW - 1));
         CF.wvlo = cv.take<int64_t>((size_t)S * (NW - 1));
@@ -1024,6 +1031,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         if (cfold) {
           a.cf = CF;
           launch_cells<M>(DS_CELLS_PREP, a);
+          if (!c->cells_no_uni) launch_cells<M>(DS_CELLS_UNIFORM, a);
           if (NW > 1) {
             a.wc = wc;
             a.NW = NW;
@@ -1068,18 +1076,27 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
           // than a width read per member).  k_cells_prep's bits 0 / 1: 4- /
           // 2-byte series kept; both -> ERR_CELLS_GENERIC, and the engine
           // rewrites the batch with one width (k_requal) and runs again
+          // k_cells_uniform's bit 2: some kept series is not uniform (or
+          // the uniform kernel already missed in this call): the general one
           int widths = 3;
+          bool uniform = false;
           if (hipMemcpyAsync(&c->h_small[2], c->d_err, 2 * sizeof(int),
                              hipMemcpyDeviceToHost, st) == hipSuccess &&
-              hipStreamSynchronize(st) == hipSuccess)
+              hipStreamSynchronize(st) == hipSuccess) {
             widths = (int)((c->h_small[2] >> 32) & 3);
+            uniform = !c->cells_no_uni && !((c->h_small[2] >> 32) & 4);
+          }
           if (widths == 3) {
             const int e = (int)(c->h_small[2] & 0xFFFFFFFF) | ERR_CELLS_GENERIC;
             c->h_small[3] = e;
             hipMemcpyAsync(c->d_err, &c->h_small[3], sizeof(int),
                            hipMemcpyHostToDevice, st);
+          } else if (uniform) {
+            launch_cells<M>(widths == 1 ? DS_CELLS_FOLD4U : DS_CELLS_FOLD2U, a);
+            ++c->n_cells_uniform;
           } else {
             launch_cells<M>(widths == 1 ? DS_CELLS_FOLD4 : DS_CELLS_FOLD2, a);
+            ++c->n_cells_general;
           }
         }
         else launch_ds<M>(DS_FOLD, a);
@@ -1897,8 +1914,12 @@ otsdb_status run_cells_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
     // mixed inside a row or across a series' rows — is rewritten with
     // 4-byte qualifiers (k_requal) and the fused path runs again; what it
     // still does not take re-runs through the decode below
+    // (a uniform fold that meets a qualifier of other flags is run again
+    // with the general kernel: ERR_CELLS_NONUNI, one more attempt)
     CellsDev CQ = C;
-    for (int attempt = 0; attempt < 2; ++attempt) {
+    c->cells_no_uni = false;
+    bool requaled = false;
+    for (int attempt = 0; attempt < 4; ++attempt) {
       Work W;
       rc = run_pipeline(c, spec, B, b->group_members, goff, P, W, 0, nullptr,
                         nullptr, &CQ, series_row);
@@ -1907,6 +1928,11 @@ otsdb_status run_cells_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
                              hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
       const int e = (int)(c->h_small[0] & 0xFFFFFFFF);
+      if ((e & ERR_CELLS_NONUNI) && !c->cells_no_uni) {
+        ++c->n_cells_uni_miss;
+        c->cells_no_uni = true;
+        continue;
+      }
       if (c->verbatim && (e & (ERR_CORRUPT_CELL | ERR_CELLS_GENERIC |
                                ERR_NOT_SORTED | ERR_SPEC_MISS)))
         return spec_miss(c);
@@ -1919,12 +1945,16 @@ otsdb_status run_cells_impl(otsdb_ctx* c, const otsdb_query_spec* spec,
         if (rc) return rc;
         return finish(c, G, out);
       }
-      if (attempt == 0) {
+      if (requaled) break;
+      requaled = true;
+      c->cells_no_uni = false;
+      {
         std::unique_ptr<StageTimer> rq_tm(new StageTimer(c, 7));
         rc = requal_impl(c, C, &CQ, st);
         if (rc) return rc;
       }
     }
+    c->cells_no_uni = false;
   }
   // (verbatim storage rows take only the cells fold)
   if (c->verbatim) return spec_miss(c);
@@ -3268,6 +3298,15 @@ otsdb_status otsdb_prof_read(otsdb_ctx* c, double* ms, int64_t* launches,
       c->prof_ms[i] = 0;
       c->prof_n[i] = 0;
     }
+  return OTSDB_OK;
+}
+
+otsdb_status otsdb_ctx_counters(otsdb_ctx* c, int64_t* out, int n) {
+  if (!c || (n > 0 && !out)) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  CtxLock lk(c);
+  const int64_t v[3] = {c->n_cells_uniform, c->n_cells_general,
+                        c->n_cells_uni_miss};
+  for (int i = 0; i < n && i < 3; ++i) out[i] = v[i];
   return OTSDB_OK;
 }
 

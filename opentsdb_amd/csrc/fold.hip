@@ -572,11 +572,15 @@ struct CellsMember {
   int64_t r1;     // one past the series' last row
   int64_t qend, vend;  // readable bytes of the pools
   int32_t qw, vl0;
+  int32_t uf;     // the uniform series' flags nibble (CellsFold.uf)
 };
 
 template <class M, class A, int K, int QW>
 DEV void fold_member_cells(const Params& P, const CellsDev& C, FoldSink<A>& F,
                            const FoldMember* mc, const CellsMember* cm);
+template <class M, class A, int K, int QW>
+DEV void fold_member_cells_u(const Params& P, const CellsDev& C, FoldSink<A>& F,
+                             const FoldMember* mc, const CellsMember* cm);
 
 template <class M, class A, int K, int CELLS = 0>
 __global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
@@ -724,12 +728,15 @@ __global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
           c.vl0 = CF.vl0[s];
         }
         c.qw = CF.qw[s];
+        c.uf = CF.uf ? CF.uf[s] : 0xFF;
         c.qend = CF.C.qual_off[CF.C.R];
         c.vend = CF.C.val_off[CF.C.R];
         cm[CELLS ? w : 0] = c;
       }
     }
-    if constexpr (CELLS != 0)
+    if constexpr (CELLS >= 8)  // every kept series uniform (k_cells_uniform)
+      fold_member_cells_u<M, A, K, CELLS - 8>(P, CF.C, F, &mc[w], &cm[w]);
+    else if constexpr (CELLS != 0)
       fold_member_cells<M, A, K, CELLS == 1 ? 0 : CELLS>(P, CF.C, F, &mc[w], &cm[w]);
     else
       fold_member<M, A, K>(P, B, F, &mc[w]);

@@ -51,7 +51,14 @@ struct CellsFold {
   uint8_t* wvl0;
   int* wide;                  // k_cells_prep: bit 0 / 1 = some kept series
                               // has 4- / 2-byte qualifiers (one width: the
-                              // fold with that width fixed runs)
+                              // fold with that width fixed runs); bit 2
+                              // (k_cells_uniform): some kept series is not
+                              // uniform
+  // k_cells_uniform: the series' one flags nibble (value length and type)
+  // when every row of it is uniform — one qualifier width, value bytes
+  // adding up to points x length (+ the meta byte of a multi-point column)
+  // — else 0xFF
+  uint8_t* uf;
 };
 
 // buckets per fold window: the aggregator states of a window live in LDS
@@ -102,7 +109,10 @@ enum DsKernel {
   DS_CELLS_FOLD2, // the cells fold of a batch whose kept series all have
                   // 2-byte qualifiers (the width a compile-time constant)
   DS_CELLS_FOLD4, // ... all 4-byte ones
-  DS_PREP_FOLD    // k_prep_fold: k_prep + k_fold_prep in one launch
+  DS_PREP_FOLD,   // k_prep_fold: k_prep + k_fold_prep in one launch
+  DS_CELLS_UNIFORM, // k_cells_uniform: which kept series are uniform
+  DS_CELLS_FOLD2U,  // the uniform cells fold (fold_member_cells_u), 2-byte
+  DS_CELLS_FOLD4U   // ... 4-byte qualifiers
 };
 
 struct DsLaunch {

@@ -107,6 +107,14 @@ class Engine:
         self._check(self.lib.otsdb_ctx_create(int(device), C.byref(self.ctx)))
         self.device = device
 
+    def counters(self):
+        """otsdb_ctx_counters: {cells folds run uniform / general, uniform
+        folds re-run with the general kernel}."""
+        out = (C.c_int64 * 3)()
+        self._check(self.lib.otsdb_ctx_counters(self.ctx, out, 3))
+        return dict(cells_uniform=out[0], cells_general=out[1],
+                    cells_uniform_miss=out[2])
+
     def close(self):
         if self.ctx:
             self.lib.otsdb_ctx_destroy(self.ctx)

@@ -542,3 +542,101 @@ def test_fused_cells_mixed_cut_qualifier(engine):
     res = DeviceResult(torch, db.n_groups, 4096, "cuda")
     with pytest.raises(core.IllegalDataException):
         workload.run_cells_device(engine, spec, dc, db, res)
+
+
+# (name, value kind, int range, float4 fraction, ms fraction, what the
+# kernel choice must be): the uniform cells fold (every kept series one value
+# length / type and one qualifier width, k_cells_uniform) for every value
+# width and both qualifier widths; batches with a series of mixed lengths
+# (the general kernel), and with a series whose rows add up although a point
+# is an 8-byte long among 8-byte doubles (the uniform kernel misses on its
+# flags and the engine re-runs the general one)
+UNIFORM_CASES = [("f8", "float", None, 0.0, 0.0, "uniform"),
+                 ("f4", "float", None, 1.0, 0.0, "uniform"),
+                 ("i1", "int", (-120, 120), 0, 0, "uniform"),
+                 ("i2", "int", (300, 30000), 0, 0, "uniform"),
+                 ("i4", "int", (1 << 20, 1 << 30), 0, 0, "uniform"),
+                 ("i8", "int", (1 << 40, 1 << 50), 0, 0, "uniform"),
+                 ("f8ms", "float", None, 0.0, 1.0, "uniform"),
+                 ("i2ms", "int", (300, 30000), 0, 1.0, "uniform"),
+                 ("imix", "int", (-(1 << 40), 1 << 40), 0, 0, "general"),
+                 ("f8i8", "float", None, 0.0, 0.0, "miss")]
+
+
+@pytest.mark.parametrize("name,kind,rng_i,f4,ms,path", UNIFORM_CASES,
+                         ids=[c[0] for c in UNIFORM_CASES])
+@pytest.mark.parametrize("agg,ds,span", [("sum", "1m-avg", 3), ("dev", "5m-sum", 3),
+                                         ("zimsum", "1m-max", 40)])
+def test_fused_cells_uniform_kernel(engine, name, kind, rng_i, f4, ms, path,
+                                    agg, ds, span):
+    """The cells fold's uniform kernel (fold_member_cells_u) against the
+    oracle on the points RowSeq decodes, and which kernel ran
+    (otsdb_ctx_counters): uniform for uniform series (one and several fold
+    windows: 40 h of 1 m buckets), the general kernel for a batch with a
+    mixed-length series, and a re-run with the general kernel when a row's
+    lengths add up but a qualifier's flags differ."""
+    import torch
+    from opentsdb_amd import workload
+    from opentsdb_amd.batch import HostBatch
+    from opentsdb_amd.engine import DeviceResult
+    from tests.test_gpu_parity import cancel_floor, compare
+    rng = np.random.default_rng(23)
+    b = datasets.random_batch(19, n_series=24, n_groups=3, value_kind=kind,
+                              span_ms=span * 3600000,
+                              cadence_ms=7000 if ms else 10000)
+    if ms:
+        b.ts = b.ts + rng.integers(0, 999, len(b.ts))
+        for s in range(b.n_series):
+            a, z = b.offsets[s], b.offsets[s + 1]
+            b.ts[a:z] = np.sort(b.ts[a:z])
+    else:
+        b.ts = b.ts - b.ts % 1000
+    if rng_i is not None:
+        b.val = rng.integers(rng_i[0], rng_i[1], len(b.ts)).astype(np.int64)
+        b.is_float = np.zeros(len(b.ts), np.uint8)
+    else:
+        b.is_float = np.ones(len(b.ts), np.uint8)
+    if name == "f8i8":  # series 5: every 7th point an 8-byte long
+        a, z = b.offsets[5], b.offsets[6]
+        assert z - a > 50
+        sel = np.arange(a, z, 7)
+        b.val[sel] = (1 << 40) + sel
+        b.is_float[sel] = 0
+    enc = cells.encode_batch(b, rng, f4, ms)
+    ts, bits, isint = [], [], []
+    for s in range(b.n_series):
+        for r in np.nonzero(enc["row_series"] == s)[0]:
+            q = enc["qual"][enc["qual_off"][r]:enc["qual_off"][r + 1]]
+            v = enc["val"][enc["val_off"][r]:enc["val_off"][r + 1]]
+            p = pyoracle.decode_row(q.tobytes(), v.tobytes(),
+                                    enc["row_base_s"][r])
+            ts.append(p["ts"])
+            bits.append(p["bits"])
+            isint.append(p["is_int"])
+    rts = np.concatenate(ts).astype(np.int64)
+    rbits = np.concatenate(bits).astype(np.int64)
+    risf = (np.concatenate(isint).astype(np.uint8) == 0).astype(np.uint8)
+    hb = HostBatch(b.offsets, rts, rbits, risf, None, b.group_offsets,
+                   b.group_members)
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda()
+         for k, v in enc.items()}
+    dc = workload.DeviceCells(d, b.n_series)
+    db = _device_batch(hb, "float" if kind == "float" else "int")
+    t0 = datasets.T0 + 600000
+    t1 = datasets.T0 + span * 3600000 - 300000
+    spec = core.make_spec(t0, t1, core.Aggregators.get(agg),
+                          core.DownsamplingSpecification(ds), t0, t1)
+    ref = pyoracle.group_by(spec, hb)
+    res = DeviceResult(torch, db.n_groups, 4 * len(hb.ts) + 64, "cuda")
+    c0 = engine.counters()
+    workload.run_cells_device(engine, spec, dc, db, res)
+    c1 = engine.counters()
+    du = c1["cells_uniform"] - c0["cells_uniform"]
+    dg = c1["cells_general"] - c0["cells_general"]
+    dm = c1["cells_uniform_miss"] - c0["cells_uniform_miss"]
+    assert (du, dg, dm) == {"uniform": (1, 0, 0), "general": (0, 1, 0),
+                            "miss": (1, 1, 1)}[path], (du, dg, dm)
+    got = _result_points(res, db.n_groups)
+    fl = cancel_floor(hb, 60) if kind == "int" else 0.0
+    compare(got, ref, agg == "zimsum" and kind == "int", floor=fl,
+            where="uniform/%s/%s/%s" % (name, agg, ds))
