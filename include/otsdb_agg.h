@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OTSDB_ABI_VERSION 4
+#define OTSDB_ABI_VERSION 5
 
 /* ------------------------------------------------------------------------ */
 /* Status codes — 1:1 with the exceptions of the reference path.             */
@@ -119,6 +119,7 @@ typedef enum {
 /* ------------------------------------------------------------------------ */
 /* Query spec: one per query (all groups share it).                          */
 /* ------------------------------------------------------------------------ */
+#define OTSDB_SPEC_EXACT_ORDER 1
 typedef struct {
   /* AggregationIterator window, ms, inclusive on both ends
    * (SpanGroup ctor normalises the scan bounds to ms, SpanGroup.java:267-270;
@@ -140,7 +141,20 @@ typedef struct {
   int32_t rate;            /* RateSpan applied after downsampling          */
   int32_t counter;         /* RateOptions.counter                          */
   int32_t drop_resets;     /* RateOptions.drop_resets                      */
-  int32_t _pad;
+  /* OTSDB_SPEC_* bits (ABI 5; the padding word before, callers pass 0).
+   * OTSDB_SPEC_EXACT_ORDER: an order-sensitive aggregator (dev) reduces
+   * every (group, timestamp) in ONE sequential chain over the group's
+   * members in SpanCmp order, whatever the group's size — StdDev.runDouble's
+   * one Welford loop (Aggregators.java:547-568) bit for bit.  Without it a
+   * group of more than 65,536 members on one device merges in-order chunk
+   * states with Chan's formula: on well-conditioned contributions (counter
+   * rates, C4) within 1e-12 of the loop, on offset gauges (~3e9 +- 1e4,
+   * where the loop itself lies ~1e-11 from the exact sigma) measured
+   * ~1e-11 off (tests/test_gpu_dev_large.py); the chain costs ~100-180 ns a
+   * member per bucket (tools/chain_probe.hip: a 500k-member group ~50-90 ms).
+   * A chain whose bucket rows (9 B per member and bucket) pass the engine's
+   * fixed row budget is OTSDB_E_CAPACITY with the flag, merged without.    */
+  int32_t flags;
   int64_t counter_max;     /* RateOptions.counter_max (default Long.MAX)   */
   int64_t reset_value;     /* RateOptions.reset_value (default 0)          */
   /* Calendar downsampling (use_calendar = 1): the bucket edges, ms, strictly
@@ -518,6 +532,9 @@ otsdb_status otsdb_prof_read(otsdb_ctx* ctx, double* ms, int64_t* launches,
  * out[1] with the general one, out[2] uniform folds that met a qualifier of
  * other flags and were re-run with the general kernel.                      */
 otsdb_status otsdb_ctx_counters(otsdb_ctx* ctx, int64_t* out, int n);
+/* Test hook: the one-pass compaction's epoch (1 .. 2^24 - 1) the context's
+ * next call increments, so tests can drive it across its wrap.            */
+otsdb_status otsdb_test_set_compact_epoch(otsdb_ctx* ctx, uint32_t epoch);
 
 /* ---- synthetic workload generator (bench / tests) ----------- */
 /* Generates the columnar batch of `n_series` series starting at global

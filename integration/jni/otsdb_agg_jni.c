@@ -132,6 +132,13 @@ JNIEXPORT jint JNICALL Java_net_opentsdb_core_GpuAggregation_nativeRunCells(
   s.drop_resets = (int32_t)spec_v[SPEC_DROP_RESETS];
   s.counter_max = spec_v[SPEC_COUNTER_MAX];
   s.reset_value = spec_v[SPEC_RESET_VALUE];
+  /* optional trailing word (ABI 5): otsdb_query_spec.flags, e.g.
+   * OTSDB_SPEC_EXACT_ORDER for dev over groups past 65,536 members */
+  if ((*env)->GetArrayLength(env, jspec) > SPEC_LEN) {
+    jlong fl = 0;
+    (*env)->GetLongArrayRegion(env, jspec, SPEC_LEN, 1, &fl);
+    s.flags = (int32_t)fl;
+  }
   const jsize n_rows = jrow_series ? (*env)->GetArrayLength(env, jrow_series) : 0;
   const jsize n_groups = (*env)->GetArrayLength(env, jgoff) - 1;
   const jsize n_out_off = (*env)->GetArrayLength(env, jooff);

@@ -39,7 +39,7 @@ class QuerySpec(C.Structure):
         ("rate", C.c_int32),
         ("counter", C.c_int32),
         ("drop_resets", C.c_int32),
-        ("_pad", C.c_int32),
+        ("flags", C.c_int32),  # OTSDB_SPEC_* (ABI 5)
         ("counter_max", C.c_int64),
         ("reset_value", C.c_int64),
         ("cal_edges", C.c_void_p),
@@ -132,6 +132,9 @@ class GenSpec(C.Structure):
     ]
 
 
+SPEC_EXACT_ORDER = 1  # otsdb_query_spec.flags
+
+
 EXPORTS = [
     "otsdb_abi_version", "otsdb_ctx_create", "otsdb_ctx_destroy",
     "otsdb_last_error", "otsdb_agg_lookup", "otsdb_agg_name",
@@ -140,7 +143,7 @@ EXPORTS = [
     "otsdb_agg_partials_chained_device", "otsdb_agg_finalize_device",
     "otsdb_gen_counts_device",
     "otsdb_gen_fill_device", "otsdb_prof_enable", "otsdb_prof_read",
-    "otsdb_ctx_counters",
+    "otsdb_ctx_counters", "otsdb_test_set_compact_epoch",
     "otsdb_decode_cells_device", "otsdb_sel_prepare_device",
     "otsdb_sel_hist_device", "otsdb_sel_hist_wait", "otsdb_sel_finish_device",
     "otsdb_encode_cells_device", "otsdb_agg_run_cells_device",
@@ -239,6 +242,9 @@ def load(path=None):
     lib.otsdb_prof_read.restype = C.c_int
     lib.otsdb_ctx_counters.argtypes = [vp, vp, C.c_int]
     lib.otsdb_ctx_counters.restype = C.c_int
+    if hasattr(lib, "otsdb_test_set_compact_epoch"):  # (test hook)
+        lib.otsdb_test_set_compact_epoch.argtypes = [vp, C.c_uint32]
+        lib.otsdb_test_set_compact_epoch.restype = C.c_int
     if path is None:
         _lib = lib
     return lib

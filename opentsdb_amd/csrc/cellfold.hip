@@ -982,6 +982,46 @@ DEV void cells_vload_u(const uint8_t* vp, int32_t a, bool near, int32_t vlim,
   d[ND - 1] = *reinterpret_cast<const uint32_t*>(s + 4 * (ND - 1));
 }
 
+// The uniform fold's value extraction: 8- and 4-byte values with one
+// v_perm each 4 bytes (the byte swap and the meta-byte shift in one
+// selector, per lane: 0x00010203 + shift x 0x01010101), 1- and 2-byte ones
+// as cells_vextract.
+template <int VL, int FL, int K>
+DEV void cells_vextract_p(const uint32_t* d, int jb, uint32_t sh, int64_t* v) {
+  if constexpr (VL == 8 || VL == 4) {
+    const uint32_t s0 = 0x00010203u, s1 = s0 + sh * 0x01010101u;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint32_t sel = j >= jb ? s1 : s0;
+      if constexpr (VL == 8) {
+        const uint32_t hi = __builtin_amdgcn_perm(d[2 * j + 1], d[2 * j], sel);
+        const uint32_t lo = __builtin_amdgcn_perm(d[2 * j + 2], d[2 * j + 1], sel);
+        const int64_t x = (int64_t)(((uint64_t)hi << 32) | lo);
+        v[j] = FL ? x : __double_as_longlong((double)x);
+      } else {
+        const uint32_t x = __builtin_amdgcn_perm(d[j + 1], d[j], sel);
+        v[j] = __double_as_longlong(FL ? (double)__uint_as_float(x)
+                                       : (double)(int32_t)x);
+      }
+    }
+  } else {
+    cells_vextract<VL, FL, K>(d, jb, sh, v);
+  }
+}
+
+template <int K>
+DEV void cells_vextract_pl(int vl, int fl, const uint32_t* d, int jb,
+                           uint32_t sh, int64_t* v) {
+  switch (vl + 16 * fl) {
+    case 8 + 16: cells_vextract_p<8, 1, K>(d, jb, sh, v); break;
+    case 4 + 16: cells_vextract_p<4, 1, K>(d, jb, sh, v); break;
+    case 8: cells_vextract_p<8, 0, K>(d, jb, sh, v); break;
+    case 4: cells_vextract_p<4, 0, K>(d, jb, sh, v); break;
+    case 2: cells_vextract_p<2, 0, K>(d, jb, sh, v); break;
+    default: cells_vextract_p<1, 0, K>(d, jb, sh, v); break;
+  }
+}
+
 template <class M, class A, int K, int QW>
 DEV void fold_member_cells_u(const Params& P, const CellsDev& C, FoldSink<A>& F,
                              const FoldMember* mc, const CellsMember* cm) {
@@ -1043,6 +1083,7 @@ DEV void fold_member_cells_u(const Params& P, const CellsDev& C, FoldSink<A>& F,
   uint32_t t_last_prev = 0;  // check_order: the previous step's last time
   const int32_t n_guard = pe - p + 64;  // every step consumes >= 1 point
   int dbg_n = 0;
+  L2Touch pq_, pv_;
   while (p < pe) {
     FOLD_GUARD(dbg_n, n_guard, F.err, "uniform cells stream mi=%d p=%d pe=%d\n",
                F.mi, p, pe)
@@ -1108,6 +1149,17 @@ DEV void fold_member_cells_u(const Params& P, const CellsDev& C, FoldSink<A>& F,
     }
     const bool vnear = vcur + 9 * PTS + 128 > vlim;
     const int32_t a0 = vcur + ((K * lane) << vsh) + mbefore;
+    if (OTSDB_PF_CELLS) {
+      // the lines OTSDB_PF_CELLS steps ahead into L2 (one dword a lane: the
+      // lane's 64 value bytes and 16 qualifier bytes of that step)
+      pq_.retire();
+      pv_.retire();
+      if (((p + (OTSDB_PF_CELLS + 1) * PTS) << qsh) + 16 <= qlim)
+        pq_.touch(qp + ((uint32_t)(p + OTSDB_PF_CELLS * PTS + K * lane) << qsh));
+      const int32_t pvo = vcur + ((OTSDB_PF_CELLS * PTS + K * lane) << vsh);
+      if (vcur + (((OTSDB_PF_CELLS + 1) * PTS) << vsh) + 128 <= vlim)
+        pv_.touch(vp + (uint32_t)pvo);
+    }
     uint32_t d[17];
     switch (vsh) {
       case 3: cells_vload_u<8, 0, K>(vp, a0, vnear, vlim, d); break;
@@ -1131,22 +1183,30 @@ DEV void fold_member_cells_u(const Params& P, const CellsDev& C, FoldSink<A>& F,
     }
 #endif
     // ---- every streamed qualifier: the series' width and flags
-    uint32_t bad = 0;
+    // (flags: xor with the pattern, or-accumulated, masked once; QW 2's
+    // width: +0x10 carries out of a 0xF0 nibble only; qualifiers of a
+    // lane's points past the step replaced by the pattern itself)
+    constexpr int NQ = QW == 4 ? 8 : 4;
+    uint32_t qc[NQ];
 #pragma unroll
-    for (int i = 0; i < (QW == 4 ? 8 : 4); ++i) {
-      const uint32_t w = dq[i];
-      uint32_t b;
-      if constexpr (QW == 2) {
-        b = (((w & 0x00F000F0u) + 0x00100010u) & 0x01000100u) |
-            ((w & 0x0F000F00u) ^ fpat);
-        if (!full)
-          b &= (2 * i < nv ? 0x0000FFFFu : 0u) | (2 * i + 1 < nv ? 0xFFFF0000u : 0u);
-      } else {
-        b = (w & 0x0F0000F0u) ^ fpat;
-        if (!full) b = i < nv ? b : 0u;
+    for (int i = 0; i < NQ; ++i) qc[i] = dq[i];
+    if (!full) {
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const uint32_t m = QW == 2 ? ((2 * i < nv ? 0x0000FFFFu : 0u) |
+                                      (2 * i + 1 < nv ? 0xFFFF0000u : 0u))
+                                   : (i < nv ? 0xFFFFFFFFu : 0u);
+        qc[i] = (qc[i] & m) | (fpat & ~m);
       }
-      bad |= b;
     }
+    uint32_t fx = 0, wx = 0;
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      fx |= qc[i] ^ fpat;
+      if constexpr (QW == 2) wx |= (qc[i] & 0x00F000F0u) + 0x00100010u;
+    }
+    const uint32_t bad = (fx & (QW == 2 ? 0x0F000F00u : 0x0F0000F0u)) |
+                         (wx & 0x01000100u);
 #if defined(OTSDB_CELLS_ABL) && OTSDB_CELLS_ABL == 3  // timing: no check
     if (bad == 0x12345678u) F.emit[1] = 1;
 #else
@@ -1186,7 +1246,7 @@ DEV void fold_member_cells_u(const Params& P, const CellsDev& C, FoldSink<A>& F,
     }
     // ---- values (the boundary's meta byte skipped from point jb on)
     int64_t v[K];
-    cells_vextract_vl<K>(vl, fl, d, jb, (uint32_t)mnext, v);
+    cells_vextract_pl<K>(vl, fl, d, jb, (uint32_t)mnext, v);
     // ---- the downsample over [p, hs) (fold_member's ring bookkeeping)
     const int32_t k_hi = bucket_rel(
         P, full ? (uint32_t)__builtin_amdgcn_readlane((int32_t)t[K - 1], 63)

@@ -239,7 +239,13 @@ __global__ __launch_bounds__(256) void k_compact1(
     const uint64_t upto = stop == 64 ? ~0ULL : ((2ULL << stop) - 1);
     if (__ballot(!cur) & upto) {  // a predecessor not published yet
       if (++spins > (1u << 22)) {  // (bounded: never expected)
-        if (lane == 0) atomicOr(err_word, ERR_INTERNAL);
+        // reported through host memory: the last group may have swapped
+        // the error word out already (finish reads small[2])
+        if (lane == 0) {
+          atomicOr(err_word, ERR_INTERNAL);
+          __hip_atomic_store(&small[2], (int64_t)1, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         break;
       }
       __builtin_amdgcn_s_sleep(1);

@@ -122,6 +122,10 @@ constexpr int64_t kFoldChunk = OTSDB_FOLD_CHUNK;
 constexpr int64_t kOrderedFoldChunk = 256;
 constexpr int64_t kOrderedChunk = 65536;
 constexpr int64_t kOrderedChunkMerged = 16384;
+// the row path's bucket rows an ordered (dev) query may take for groups past
+// one fold tile: fixed, so the path (and the reduction order) never depends
+// on the device's free memory at call time
+constexpr double kOrderedRowBudget = 48.0e9;
 // below this many (tile, window) workgroups the fold narrows its windows,
 // down to kFoldMinWindow buckets
 #ifndef OTSDB_FOLD_MIN_BLOCKS  // tuning builds override
@@ -865,21 +869,28 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   with_monoid(spec->agg_id, [&](auto tag) {
     ordered = decltype(tag)::kOrdered;
   });
+  // OTSDB_SPEC_EXACT_ORDER: every group one chain, whatever its size
+  const bool exact = ordered && (spec->flags & OTSDB_SPEC_EXACT_ORDER) != 0;
   if (ordered && fold) {
     // a group past one fold tile takes the row path (one chain per bucket)
     // when its bucket matrix (8-byte value + state byte per series and
-    // bucket) fits in what the device has free; otherwise the fold's tiles
-    // stay, merged in order (Chan) like a group past the exact-chain bound
+    // bucket) fits the fixed row budget — a bound of the query alone, so
+    // identical queries always take the same path (and the same order);
+    // otherwise the fold's tiles stay, merged in order (Chan) like a group
+    // past the exact-chain bound, or E_CAPACITY when the caller asked for
+    // the exact order
     int64_t kmax = 0;
     for (size_t g = 0; g + 1 < goff.size(); ++g)
       kmax = std::max(kmax, goff[g + 1] - goff[g]);
-    size_t free_b = 0, total_b = 0;
-    if (kmax > kOrderedFoldChunk &&
-        hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
-        (double)S * (double)NB * 9.0 + (double)c->ws_cap <=
-            0.8 * ((double)free_b + (double)c->ws_cap)) {
-      fold = false;
-      WB = NW = 0;
+    if (kmax > kOrderedFoldChunk) {
+      if ((double)S * (double)NB * 9.0 <= kOrderedRowBudget) {
+        fold = false;
+        WB = NW = 0;
+      } else if (exact) {
+        return fail(OTSDB_E_CAPACITY,
+                    "exact-order dev: %lld x %lld bucket rows past the row "
+                    "budget", (long long)S, (long long)NB);
+      }
     }
   }
   const bool cfold = cells && fold;
@@ -889,11 +900,22 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   // one chain per (group, bucket) up to kOrderedChunk members; partials for
   // the merge across ranks (a group too large to hand on, dist.py) keep
   // round 4's shorter chains, merged in order anyway
+  // the chained entry always takes the row path (its chains continue from
+  // the previous rank's states): past the row budget a clear E_CAPACITY
+  if (ginit && (double)S * (double)NB * 9.0 > kOrderedRowBudget)
+    return fail(OTSDB_E_CAPACITY,
+                "chained partials: %lld x %lld bucket rows past the row budget",
+                (long long)S, (long long)NB);
+  if (exact && mode == 1 && !ginit)
+    return fail(OTSDB_E_UNSUPPORTED,
+                "exact-order dev across ranks: hand the chains on "
+                "(otsdb_agg_partials_chained_device)");
   otsdb_status rc = build_tiles(
       c, goff, mode == 2, fold ? kFoldChunk : kChunk,
       ordered ? (fold ? kOrderedFoldChunk
-                      : (mode == 1 && !ginit ? kOrderedChunkMerged
-                                             : kOrderedChunk))
+                      : (exact ? INT64_MAX
+                               : (mode == 1 && !ginit ? kOrderedChunkMerged
+                                                      : kOrderedChunk)))
               : 0);
   if (rc) return rc;
   const Tiles T = tiles_of(c, G);
@@ -1285,10 +1307,15 @@ otsdb_status compact(otsdb_ctx* c, const Params& P, int64_t G,
   c->cmp_flags = p;
   c->cmp_flags_cap = cap;
   if (rc) return rc;
-  if (grow) HIP_TRY(hipMemsetAsync(p, 0, cap, st));  // no stale epochs
   // epochs 1, 2, ..., 2^24 - 1, then 4, 5, ...: never 0 (fresh granules)
-  // and always one ticket slot on from the last call's (k_compact1)
-  c->cmp_epoch = c->cmp_epoch + 1 == (1u << 24) ? 4u : c->cmp_epoch + 1;
+  // and always one ticket slot on from the last call's (k_compact1).  A
+  // granule is taken as this call's by its epoch alone, so when the epoch
+  // wraps every granule is cleared: one a call 2^24 - 4 calls ago left (a
+  // group index only smaller or long-grid calls used since) would otherwise
+  // read as published now
+  const bool wrap = c->cmp_epoch + 1 == (1u << 24);
+  c->cmp_epoch = wrap ? 4u : c->cmp_epoch + 1;
+  if (grow || wrap) HIP_TRY(hipMemsetAsync(p, 0, cap, st));  // no stale epochs
   unsigned long long* ticket = (unsigned long long*)((char*)c->d_err + 192);
   int64_t* small = c->d_done;
   // few groups (C1's 100): one group (wavefront) per block, spread over more
@@ -1329,7 +1356,16 @@ otsdb_status finish(otsdb_ctx* c, int64_t G, otsdb_result* out) {
     HIP_TRY(hipStreamSynchronize(st));
     c->h_small[0] = __atomic_load_n(&c->h_done[0], __ATOMIC_ACQUIRE);
     c->h_small[1] = __atomic_load_n(&c->h_done[1], __ATOMIC_ACQUIRE);
-    c->err_clean = true;
+    // a look-back that gave up (k_compact1's bounded spin: never expected)
+    // marks h_done[2] with a plain store, after the last group may already
+    // have swapped the error word out: report it here, and leave the device
+    // word (which may hold its bit) to the next call's memset
+    if (__atomic_load_n(&c->h_done[2], __ATOMIC_ACQUIRE)) {
+      c->h_done[2] = 0;
+      c->h_small[0] |= ERR_INTERNAL;
+    } else {
+      c->err_clean = true;
+    }
   } else {
     HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
                            hipMemcpyDeviceToHost, st));
@@ -2508,6 +2544,7 @@ otsdb_status otsdb_ctx_create(int device, otsdb_ctx** out) {
   HIP_TRY(hipHostMalloc(&c->h_done, 64,
                         hipHostMallocMapped | hipHostMallocCoherent));
   HIP_TRY(hipHostGetDevicePointer((void**)&c->d_done, c->h_done, 0));
+  for (int i = 0; i < 8; ++i) c->h_done[i] = 0;
   *out = c;
   return OTSDB_OK;
 }
@@ -3307,6 +3344,14 @@ otsdb_status otsdb_ctx_counters(otsdb_ctx* c, int64_t* out, int n) {
   const int64_t v[3] = {c->n_cells_uniform, c->n_cells_general,
                         c->n_cells_uni_miss};
   for (int i = 0; i < n && i < 3; ++i) out[i] = v[i];
+  return OTSDB_OK;
+}
+
+otsdb_status otsdb_test_set_compact_epoch(otsdb_ctx* c, uint32_t epoch) {
+  if (!c || epoch == 0 || epoch >= (1u << 24))
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "epoch %u", epoch);
+  CtxLock lk(c);
+  c->cmp_epoch = epoch;
   return OTSDB_OK;
 }
 

@@ -853,6 +853,14 @@ DEV void reduce_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
     fold_lane<M, K, FO != 0, true, TT>(P, B, sf, i0, lo, hi, t, v, S,
                                        err, nseg, cur_key, head_key, cur, head);
   }
+#if defined(OTSDB_REDUCE_ABL) && OTSDB_REDUCE_ABL == 1  // timing: lane fold only
+  {
+    const double x = cur.finish(&err) + head.finish(&err);
+    if (x == 1234.5678) S.put(cur_key, x);
+    carry_key = __builtin_amdgcn_readlane(cur_key, 63);
+    return;
+  }
+#endif
   if (nseg == 0) {  // lane wholly before lo (first step) or past hi
     cur_key = (i0 < lo) ? -1 : INT32_MAX;
     head_key = cur_key;
@@ -926,12 +934,25 @@ DEV void reduce_step(const Params& P, const BatchDev& B, int sf, int64_t lo,
     pst.shfl_up(1);
     next_head = __shfl_down(head_key, 1);
   }
-  if (nseg >= 2) {  // head run closes inside this lane
-    const M full = (lane > 0 && pkey == head_key) ? M::combine(pst, head) : head;
-    S.put(head_key, full.finish(&err));
-  }
-  if (nseg >= 1 && lane < 63 && next_head != key) {
-    S.put(key, st.finish(&err));
+  const bool put_head = nseg >= 2;  // head run closes inside this lane
+  const bool put_tail = nseg >= 1 && lane < 63 && next_head != key;
+  M hfull = head;
+  if (put_head && lane > 0 && pkey == head_key) hfull = M::combine(pst, head);
+  if constexpr (M::kCostlyFinish) {
+    // (a division / square root each: one finish a lane when no lane
+    // closes both its head and its tail run, as with buckets of > K points)
+    if (__ballot(put_head && put_tail) == 0) {
+      if (put_head || put_tail) {
+        const M& r = put_head ? hfull : st;
+        S.put(put_head ? head_key : key, r.finish(&err));
+      }
+    } else {
+      if (put_head) S.put(head_key, hfull.finish(&err));
+      if (put_tail) S.put(key, st.finish(&err));
+    }
+  } else {
+    if (put_head) S.put(head_key, hfull.finish(&err));
+    if (put_tail) S.put(key, st.finish(&err));
   }
   Packed p = st.pack();
   if (DPP) {

@@ -70,6 +70,7 @@ struct Packed {
 template <int KIND>  // 0 sum, 1 avg, 2 squareSum, 3 count
 struct MSum {
   static constexpr bool kOrdered = false;
+  static constexpr bool kCostlyFinish = KIND == 1;  // s / n
   double s;
   int32_t n;
   DEV static MSum init() { return {0.0, 0}; }
@@ -114,6 +115,7 @@ struct MSum {
 template <bool MAX>
 struct MMinMax {
   static constexpr bool kOrdered = false;
+  static constexpr bool kCostlyFinish = false;
   double m;
   DEV static MMinMax init() { return {MAX ? -__builtin_inf() : __builtin_inf()}; }
   DEV static MMinMax from(double v) {
@@ -143,6 +145,7 @@ struct MMinMax {
 // population sigma; Chan et al. merge for runs.
 struct MDev {
   static constexpr bool kOrdered = true;
+  static constexpr bool kCostlyFinish = false;
   double mean, m2;
   int32_t n;
   DEV static MDev init() { return {0.0, 0.0, 0}; }
@@ -202,6 +205,7 @@ struct MDev {
 template <bool LAST>
 struct MFirstLast {
   static constexpr bool kOrdered = false;
+  static constexpr bool kCostlyFinish = false;
   double v;
   int64_t has;
   DEV static MFirstLast init() { return {0.0, 0}; }
@@ -235,6 +239,7 @@ struct MFirstLast {
 // Multiply.runDouble (:476-484): product of every value, NaN included.
 struct MMult {
   static constexpr bool kOrdered = false;
+  static constexpr bool kCostlyFinish = false;
   double p;
   int64_t has;
   DEV static MMult init() { return {1.0, 0}; }
@@ -270,6 +275,7 @@ struct MMult {
 // 0 when the first non-NaN value is the last value.
 struct MDiff {
   static constexpr bool kOrdered = false;
+  static constexpr bool kCostlyFinish = false;
   double fnn, last;
   int64_t flags;  // bit0 has_any, bit1 has_fnn, bit2 has_after_fnn
   DEV static MDiff init() { return {0.0, 0.0, 0}; }
@@ -323,6 +329,7 @@ struct MDiff {
 // None.runDouble (:439-461): exactly one value, else IllegalDataException.
 struct MNone {
   static constexpr bool kOrdered = false;
+  static constexpr bool kCostlyFinish = false;
   double v;
   int32_t n;
   DEV static MNone init() { return {0.0, 0}; }

@@ -21,6 +21,8 @@ series (gather_shared_series).
 """
 import numpy as np
 
+from . import abi
+
 PARTIAL_WORDS = 4  # otsdb_partial = 3 doubles + int64
 # aggregators whose partial states are handed on across ranks, not merged
 # (monoids.h kOrdered)
@@ -116,8 +118,10 @@ def hand_on_partials(local_step, partials, emit, group=None):
     (a point-to-point send / recv in rank = series order), so the last
     rank's states are those of ONE pass over every member; they are
     broadcast and returned (the tensors passed in, overwritten) on every
-    rank.  The ranks run their downsampling in parallel; only the hand-offs
-    are sequential."""
+    rank.  local_step is the whole chained partials call (downsampling
+    included), so the ranks run it one after another: a chained group costs
+    about world x one rank's step (only shared groups of an order-sensitive
+    aggregator take this path; every other group runs in parallel)."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -220,6 +224,8 @@ class ShardPlan:
                 sizes = sizes.to(dev)
             all_reduce(sizes, "sum", group)
             small = sizes.cpu().numpy() <= CHAIN_MAX_MEMBERS
+            if spec.flags & abi.SPEC_EXACT_ORDER:
+                small[:] = True  # every shared group one chain over the ranks
             self.chain, self.merge = self.shared[small], self.shared[~small]
         self.chain_batch = sub(self.chain)
         self.shared_batch = sub(self.merge)

@@ -1477,6 +1477,622 @@ _sp("timestampMixedNormalized", [(_B, _sq(0) + _msq(8), _sv(4, 5))],
     [(1356998400000, 4), (1356998400008, 5)], ":592-607")
 
 
+# ------------------------------------------- round 6: the remaining in-scope
+# TestDownsampler / TestFillingDownsampler tests (rollup tests excluded: out
+# of scope).  Same conventions as above; `prefix` marks a test
+# that asserts only the first point(s) after a seek.
+TDS = "test/core/TestDownsampler.java"
+TFD = "test/core/TestFillingDownsampler.java"
+DS6 = [L(BASE + 5000, 1), L(BASE + 15000, 2), L(BASE + 25000, 4),
+       L(BASE + 35000, 8), L(BASE + 45000, 16), L(BASE + 55000, 32)]
+# testDownsamplerDeprecated :108-132 (Downsampler(source, 1000 s, avg):
+# query_start = query_end = 0, Downsampler.java:76-91)
+add(kind="view", name="ds_deprecated_1000s_avg",
+    spec=dict(ds_interval_ms=1000000, ds_agg="avg", query_start_ms=0,
+              query_end_ms=0), points=DS_DATA,
+    expect=[D(BASE - 400000, 40), D(BASE + 1600000, 50),
+            D(BASE + 3600000, 45), D(BASE + 6600000, 40),
+            D(BASE + 8600000, 50)], tol=1e-7, cite=TDS + ":108-132")
+# testDownsamplerDeprecated_10seconds :134-173 (10000 ms sum)
+add(kind="view", name="ds_deprecated_10s_sum",
+    spec=dict(ds_interval_ms=10000, ds_agg="sum", query_start_ms=0,
+              query_end_ms=0), points=P10,
+    expect=[D(BASE, 3), D(BASE + 10000, 12), D(BASE + 20000, 48),
+            D(BASE + 30000, 192), D(BASE + 40000, 768),
+            D(BASE + 50000, 1024)], tol=1e-7, cite=TDS + ":134-173")
+# testDownsamplerDeprecated_15seconds :217-247
+add(kind="view", name="ds_deprecated_15s_sum",
+    spec=dict(ds_interval_ms=15000, ds_agg="sum", query_start_ms=0,
+              query_end_ms=0), points=P15,
+    expect=[D(BASE, 1), D(BASE + 15000, 6), D(BASE + 30000, 8),
+            D(BASE + 45000, 48)], tol=1e-7, cite=TDS + ":217-247")
+# testDownsampler_allFullRange :282-308 ("0all-sum", [0, Long.MAX])
+add(kind="view", name="ds_all_full_range",
+    spec=dict(ds_string="0all-sum", query_start_ms=0, query_end_ms=LMAX),
+    points=DS6, expect=[D(0, 63)], tol=1e-7, cite=TDS + ":282-308")
+# testDownsampler_allFilterOnQuery :310-336 (query [BASE+15 s, BASE+45 s])
+add(kind="view", name="ds_all_filter_on_query",
+    spec=dict(ds_string="0all-sum", query_start_ms=BASE + 15000,
+              query_end_ms=BASE + 45000),
+    points=DS6, expect=[D(BASE + 15000, 14)], tol=1e-7, cite=TDS + ":310-336")
+# testDownsampler_allFilterOnQueryOutOfRangeEarly :338-362
+add(kind="view", name="ds_all_out_of_range_early",
+    spec=dict(ds_string="0all-sum", query_start_ms=BASE + 65000,
+              query_end_ms=BASE + 75000),
+    points=DS6, expect=[], tol=0, cite=TDS + ":338-362")
+# testDownsampler_allFilterOnQueryOutOfRangeLate :364-388
+add(kind="view", name="ds_all_out_of_range_late",
+    spec=dict(ds_string="0all-sum", query_start_ms=BASE - 15000,
+              query_end_ms=BASE - 5000),
+    points=DS6, expect=[], tol=0, cite=TDS + ":364-388")
+# testDownsampler_noData :833-840, testDownsampler_noDataCalendar :842-849
+add(kind="view", name="ds_no_data",
+    spec=dict(ds_string="1d-sum", query_start_ms=0, query_end_ms=LMAX),
+    points=[], expect=[], tol=0, cite=TDS + ":833-840")
+add(kind="view", name="ds_no_data_calendar",
+    spec=dict(ds_string="1mc-sum", query_start_ms=0, query_end_ms=LMAX),
+    points=[], expect=[], tol=0, cite=TDS + ":842-849")
+# testDownsampler_1day :851-872 (fixed 86,400,000 ms grid, sum)
+add(kind="view", name="ds_1day_fixed",
+    spec=dict(ds_interval_ms=86400000, ds_agg="sum", query_start_ms=0,
+              query_end_ms=0),
+    points=[L(BASE, 1), L(BASE + 43200000, 2), L(BASE + 86400000, 4),
+            L(BASE + 129600000, 8)],
+    expect=[D(BASE, 3), D(1357084800000, 12)], tol=1e-6, cite=TDS + ":851-872")
+EST = "EST"
+
+
+def _seq_two(t0, v0, t1, v1):
+    def g():
+        yield t0, v0
+        while True:
+            yield t1, v1
+    return g
+
+
+# testDownsampler_1day_timezone :874-898 (1dc in EST)
+_cal_case("cal_1dc_est", "1dc-sum", EST,
+          [L(1357016400000, 1), L(1357059600000, 2), L(1357102800000, 4),
+           L(1357146000000, 8)],
+          _seq_two(1357016400000, 3, 1357102800000, 12), TDS + ":874-898")
+# testDownsampler_1week :900-924 (1wc UTC, Sunday weeks)
+_cal_case("cal_1wc_utc_b", "1wc-sum", None,
+          [L(1356825600000, 1), L(1357128000000, 2), L(1357430400000, 4),
+           L(1357732800000, 8)],
+          _seq_two(1356825600000, 3, 1357430400000, 12), TDS + ":900-924")
+# testDownsampler_1week_timezone :926-950 (1wc EST)
+_cal_case("cal_1wc_est", "1wc-sum", EST,
+          [L(1356843600000, 1), L(1357146000000, 2), L(1357448400000, 4),
+           L(1357750800000, 8)],
+          _seq_two(1356843600000, 3, 1357448400000, 12), TDS + ":926-950")
+
+
+def _fixed_month_starts(y, m, n, off_h):
+    """n local month starts from (y, m) in a fixed-offset zone (UTC,
+    EST = UTC-5 with no DST), as UTC ms: what Calendar.add(MONTH, 1) steps
+    through from previousInterval's first-of-month midnight."""
+    import datetime as dt
+    out = []
+    for k in range(n):
+        yy, mm = y + (m - 1 + k) // 12, (m - 1 + k) % 12 + 1
+        out.append(int(dt.datetime(yy, mm, 1, tzinfo=dt.timezone.utc)
+                       .timestamp()) * 1000 + off_h * 3600000)
+    return out
+
+
+def _pair_points(starts, plus1=False):
+    """the 1month / 2months / 1year tests' data: two points per step, at its
+    start and half way to the next start (+1 ms on the next start for the
+    UTC 1month test)"""
+    pts = []
+    for i in range(len(starts) - 1):
+        a, b = starts[i], starts[i + 1] + (1 if plus1 else 0)
+        pts.append(L(a, 1 << (2 * i)))
+        pts.append(L(a + (b - a) // 2, 1 << (2 * i + 1)))
+    return pts
+
+
+# testDownsampler_1month_alt :989-1038: one point a month (04:00 / 05:00
+# UTC), 1dc buckets: each month's first day at UTC midnight, value 1
+_ALT = [1380600000000, 1383278400000, 1385874000000, 1388552400000,
+        1391230800000, 1393650000000, 1396324800000, 1398916800000,
+        1401595200000, 1404187200000, 1406865600000, 1409544000000]
+_alt_days = _fixed_month_starts(2013, 10, 12, 0)
+
+
+def _seq_list(pairs):
+    def g():
+        for t, v in pairs:
+            yield t, v
+    return g
+
+
+_cal_case("cal_1dc_month_alt", "1dc-sum", None, [L(t, 1) for t in _ALT],
+          _seq_list([(t, 1) for t in _alt_days]), TDS + ":989-1038", n=12)
+# testDownsampler_2months :1040-1077 (2nc over 24 points, 4 a bucket)
+_M13b = _fixed_month_starts(2013, 1, 13, 0)
+assert _M13b == _M13
+_cal_case("cal_2nc_utc", "2nc-sum", None, _pair_points(_M13b),
+          _seq_list([(_M13b[2 * k], float(sum(1 << (4 * k + i) for i in range(4))))
+                     for k in range(6)]), TDS + ":1040-1077", n=6)
+# testDownsampler_1month_timezone :1079-1113 (1nc in EST)
+_MEST = _fixed_month_starts(2013, 1, 13, 5)
+assert _MEST[0] == 1357016400000
+_cal_case("cal_1nc_est", "1nc-sum", EST, _pair_points(_MEST),
+          _seq_pairs(_MEST[:12], 24), TDS + ":1079-1113", n=12)
+# testDownsampler_1year_timezone :1150-1185 (1yc in EST)
+_YEST = [_fixed_month_starts(y, 1, 1, 5)[0] for y in (2013, 2014, 2015)]
+_cal_case("cal_1yc_est", "1yc-sum", EST, _pair_points(_YEST),
+          _seq_pairs(_YEST[:2], 4), TDS + ":1150-1185", n=2)
+# testSeek :1344-1365 (1000 s avg, seek to BASE + 3,600,000: aligned)
+_SEEK3 = [D(BASE + 3600000, 45), D(BASE + 6600000, 40), D(BASE + 8600000, 50)]
+add(kind="view", name="ds_seek", seek=BASE + 3600000,
+    spec=dict(ds_interval_ms=1000000, ds_agg="avg", query_start_ms=0,
+              query_end_ms=0), points=DS_DATA, expect=_SEEK3, tol=1e-7,
+    cite=TDS + ":1344-1365")
+# testSeek_skipPartialInterval :1407-1432 (seek BASE + 3,800,000 is not on
+# the 1000 s grid: the interval holding it is abandoned, Downsampler.java:431)
+add(kind="view", name="ds_seek_skip_partial", seek=BASE + 3800000,
+    spec=dict(ds_interval_ms=1000000, ds_agg="avg", query_start_ms=0,
+              query_end_ms=0), points=DS_DATA,
+    expect=[D(BASE + 6600000, 40), D(BASE + 8600000, 50)], tol=1e-7,
+    cite=TDS + ":1407-1432")
+# testSeek_doubleIteration :1434-1457 (a full iteration, then the seek:
+# the view is re-read from the seek, as a fresh seek)
+add(kind="view", name="ds_seek_double_iteration", seek=BASE + 3600000,
+    spec=dict(ds_interval_ms=1000000, ds_agg="avg", query_start_ms=0,
+              query_end_ms=0), points=DS_DATA, expect=_SEEK3, tol=1e-7,
+    cite=TDS + ":1434-1457")
+# testSeek_abandoningIncompleteInterval :1459-1495 (10 s sum; the first
+# point after each seek: seek(BASE) -> (BASE, 400); every later seek inside
+# [BASE+1 s, BASE+10.1 s) -> (BASE + 10 s, 40))
+_AB = [L(BASE + 100 + 1000 * i, 40) for i in range(11)]
+add(kind="view", name="ds_seek_abandon_0", seek=BASE, prefix=True,
+    spec=dict(ds_interval_ms=10000, ds_agg="sum", query_start_ms=0,
+              query_end_ms=0), points=_AB, expect=[D(BASE, 400)], tol=1e-7,
+    cite=TDS + ":1459-1495")
+for _k in range(1, 11):
+    add(kind="view", name="ds_seek_abandon_%d" % _k, seek=BASE + 1000 * _k,
+        prefix=True,
+        spec=dict(ds_interval_ms=10000, ds_agg="sum", query_start_ms=0,
+                  query_end_ms=0), points=_AB, expect=[D(BASE + 10000, 40)],
+        tol=1e-7, cite=TDS + ":1459-1495")
+
+# ------------------------------------------------ FillingDownsampler
+# testDownsampler_allFullRange :212-230, allFilterOnQuery :232-250,
+# ...OutOfRangeEarly :252-268, ...OutOfRangeLate :270-286 ("0all-sum-nan":
+# one point, or none when the query window misses every point)
+for _nm, _q0, _q1, _exp, _c in (
+        ("all_full_range", 0, LMAX, [D(0, 63)], ":212-230"),
+        ("all_filter_on_query", BASE + 15000, BASE + 45000,
+         [D(BASE + 15000, 14)], ":232-250"),
+        ("all_out_of_range_early", BASE + 65000, BASE + 75000, [], ":252-268"),
+        ("all_out_of_range_late", BASE - 15000, BASE - 5000, [], ":270-286")):
+    add(kind="view", name="fill_" + _nm,
+        spec=dict(ds_string="0all-sum-nan", start_ms=BASE + 5000,
+                  end_ms=BASE + 55000, query_start_ms=_q0, query_end_ms=_q1),
+        points=DS6, expect=_exp, tol=1e-7, cite=TFD + _c)
+# testDownsampler_noData :792-804 (1m-sum-nan over two minutes: two NaNs),
+# testDownsampler_noDataCalendar :806-818 (1mc)
+for _nm, _ds, _c in (("fill_no_data", "1m-sum-nan", ":792-804"),
+                     ("fill_no_data_calendar", "1mc-sum-nan", ":806-818")):
+    add(kind="view", name=_nm,
+        spec=dict(ds_string=_ds, start_ms=BASE, end_ms=BASE + 120000,
+                  query_start_ms=0, query_end_ms=0),
+        points=[], expect=[D(BASE, NAN), D(BASE + 60000, NAN)], tol=0,
+        cite=TFD + _c)
+
+
+def _fcal_case(name, ds, tz, start, end, points, seq, cite):
+    """FillingDownsampler over a calendar grid: the reference test asserts
+    every emitted point against its loop (transcribed as `seq`); how many it
+    emits is the filling grid's bucket count, from previousInterval(start)
+    to previousInterval(end) advanced once when the two coincide
+    (FillingDownsampler.java:113-135, :154-163) — previousInterval is pinned
+    by the TestDateTime KATs above."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__)))))
+    from opentsdb_amd import jcalendar as J
+    iv, unit = J.parse_calendar_interval(ds.split("-")[0][:-1])
+    a = J.previous_interval(start, iv, unit, tz)
+    b = J.previous_interval(end, iv, unit, tz)
+    edges = J.bucket_edges_for_series(a, max(end, b) + 1, iv, unit, tz)
+    if b == a:
+        b = edges[edges.index(a) + 1]
+    n = sum(1 for e in edges if a <= e < b)
+    it = seq()
+    exp = [next(it) for _ in range(n)]
+    add(kind="view", name=name,
+        spec=dict(ds_string=ds, tz=tz, start_ms=start, end_ms=end,
+                  query_start_ms=0, query_end_ms=LMAX),
+        points=points, expect=[D(t, v) for t, v in exp], tol=1e-3, cite=cite)
+
+
+def _fseq(ts0, step_ms, vals, tail=NAN):
+    """ts advances by a fixed step; values from a list, then `tail`"""
+    def g():
+        t, i = ts0, 0
+        while True:
+            yield t, (vals[i] if i < len(vals) else tail)
+            t += step_ms
+            i += 1
+    return g
+
+
+def _fseq_ts(pairs, tail_step=None):
+    """explicit (ts, value) pairs, then (the last ts + tail_step k, NaN)"""
+    def g():
+        for t, v in pairs:
+            yield t, v
+        t = pairs[-1][0]
+        while True:
+            t = t + tail_step if tail_step else t
+            yield t, NAN
+    return g
+
+
+H = 3600000
+# testDownsampler_calendarHour :292-360
+_fcal_case("fcal_1hc_tv", "1hc-sum-nan", TZ_TV, BASE, BASE + 3 * H, PH,
+           _fseq(BASE, H, [6, 15]), TFD + ":292-328")
+_fcal_case("fcal_1hc_af", "1hc-sum-nan", TZ_AF, 1356996600000,
+           1356996600000 + 4 * H, PH, _fseq(1356996600000, H, [1, 9, 11]),
+           TFD + ":330-342")
+_fcal_case("fcal_4hc_af", "4hc-sum-nan", TZ_AF, 1356996600000,
+           1356996600000 + 8 * H, PH,
+           _fseq_ts([(1356996600000, 21), (1357011000000, NAN)]),
+           TFD + ":344-360")
+DY = 86400000
+# testDownsampler_calendarDay :362-492 (the "1d" control: fixed grid)
+add(kind="view", name="fill_1d_control",
+    spec=dict(ds_string="1d-sum-nan", start_ms=DST_TS, end_ms=DST_TS + 4 * DY,
+              query_start_ms=0, query_end_ms=LMAX), points=PD,
+    expect=[D(DST_TS + DY * i, v) for i, v in enumerate([3, 7, 11, NAN])],
+    tol=1e-3, cite=TFD + ":362-392")
+_fcal_case("fcal_1dc_tv", "1dc-sum-nan", TZ_TV, 1450094400000 - DY,
+           DST_TS + 5 * DY, PD, _fseq(1450094400000 - DY, DY, [NAN, 1, 5, 9, 6]),
+           TFD + ":394-419")
+_fcal_case("fcal_1dc_fj", "1dc-sum-nan", TZ_FJ, 1450094400000,
+           DST_TS + 5 * DY, PD, _fseq(1450090800000, DY, [1, 2, 12, 6]),
+           TFD + ":421-444")
+_fcal_case("fcal_1dc_af", "1dc-sum-nan", TZ_AF, 1450121400000,
+           DST_TS + 4 * DY, PD, _fseq(1450121400000, DY, [1, 5, 15]),
+           TFD + ":446-467")
+_fcal_case("fcal_3dc_af", "3dc-sum-nan", TZ_AF, 1450121400000,
+           DST_TS + 6 * DY, PD, _fseq(1450121400000, 3 * DY, [21]),
+           TFD + ":469-484")
+WK = 7 * DY
+# testDownsampler_calendarWeek :487-616 (sequences: the tests' if-chains)
+
+
+def _cycle(first, rest):
+    """value after `first`: the test's if/else chain as a function"""
+    def g():
+        v = first
+        while True:
+            yield v
+            v = rest(v)
+    return g
+
+
+def _wk_ctrl(v):
+    if v == 1:
+        return 5
+    if v == 5:
+        return NAN
+    if v != v:
+        return 9
+    return NAN
+
+
+def _fseq_fn(ts0, step_ms, vals_gen):
+    def g():
+        t = ts0
+        for v in vals_gen():
+            yield t, v
+            t += step_ms
+    return g
+
+
+_fcal_case("fcal_1wc_utc", "1wc-sum-nan", None, 1449964800000,
+           DST_TS + 35 * DY, PW, _fseq_fn(1449964800000, WK, _cycle(1, _wk_ctrl)),
+           TFD + ":487-509")
+
+
+def _wk_tv(v):
+    if v == 1:
+        return 5
+    if v == 5:
+        return NAN
+    if v != v:
+        return 4
+    return 5
+
+
+_fcal_case("fcal_1wc_tv", "1wc-sum-nan", TZ_TV, 1449964800000,
+           DST_TS + 35 * DY, PW, _fseq_fn(1449921600000, WK, _cycle(1, _wk_tv)),
+           TFD + ":511-534")
+_fcal_case("fcal_1wc_fj", "1wc-sum-nan", TZ_FJ, 1449964800000,
+           DST_TS + 35 * DY, PW,
+           _fseq_fn(1449918000000, WK, _cycle(1, lambda v: v + 1)),
+           TFD + ":536-551")
+_fcal_case("fcal_1wc_af", "1wc-sum-nan", TZ_AF, 1449964800000,
+           DST_TS + 35 * DY, PW, _fseq_fn(1449948600000, WK, _cycle(1, _wk_ctrl)),
+           TFD + ":553-576")
+_fcal_case("fcal_2wc_af", "2wc-sum-nan", TZ_AF, 1449964800000,
+           DST_TS + 35 * DY, PW,
+           _fseq_fn(1449948600000, 2 * WK, _cycle(6, lambda v: 9 if v == 6 else NAN)),
+           TFD + ":578-598")
+# testDownsampler_calendarMonth :618-760 ("1n" control: fixed 30-day grid)
+DEC1 = 1448928000000
+add(kind="view", name="fill_1n_control",
+    spec=dict(ds_string="1n-sum-nan", start_ms=DEC1,
+              end_ms=DEC1 + 2592000000 * 5, query_start_ms=0,
+              query_end_ms=LMAX), points=PM,
+    expect=[D(DEC1 + 2592000000 * i, v) for i, v in
+            enumerate([1, 5, 4, 11, NAN])], tol=1e-3, cite=TFD + ":618-648")
+_fcal_case("fcal_1nc_tv", "1nc-sum-nan", TZ_TV, DEC1, DEC1 + 2592000000 * 6,
+           PM, _fseq_ts([(1448884800000, 3), (1451563200000, 3),
+                         (1454241600000, 9), (1456747200000, 6),
+                         (1459425600000, NAN)]), TFD + ":650-676")
+_fcal_case("fcal_1nc_fj", "1nc-sum-nan", TZ_FJ, DEC1, DEC1 + 2592000000 * 6,
+           PM, _fseq_ts([(1448881200000, 1), (1451559600000, 5),
+                         (1454241600000, 9), (1456747200000, 6),
+                         (1459425600000, NAN)]), TFD + ":678-704")
+_fcal_case("fcal_1nc_af", "1nc-sum-nan", TZ_AF, DEC1, DEC1 + 2592000000 * 5,
+           PM, _fseq_ts([(1448911800000, 3), (1451590200000, 3),
+                         (1454268600000, 15), (1456774200000, NAN)]),
+           TFD + ":706-729")
+_fcal_case("fcal_3nc_tv", "3nc-sum-nan", TZ_TV, DEC1, DEC1 + 2592000000 * 9,
+           PM, _fseq_ts([(1443614400000, 3), (1451563200000, 18),
+                         (1459425600000, NAN)]), TFD + ":731-752")
+# testDownsampler_calendarSkipSomePoints :762-790
+_fcal_case("fcal_skip_some", "1hc-sum-nan", TZ_TV, 1356998400000,
+           1357009200000, [L(BASE, 1), L(BASE + 1800000, 2), L(BASE + 7200000, 6)],
+           _fseq(BASE, H, [3, NAN, 6]), TFD + ":762-790")
+
+
+# --------------------------------------------- TestTsdbQueryDownsample (rest)
+# (single series web01 — the tests' tags select it; query [1356998400,
+# 1357041600] s: the SpanGroup window is the scan bounds, Q_WIN).  A point's
+# optional 4th element is its own tolerance (tests assert the ends and the
+# middle with different deltas; float literals as Java's `F` constants).
+TQD = "test/core/TestTsdbQueryDownsample.java"
+
+
+def F32(x):
+    import struct as st
+    return st.unpack("<f", st.pack("<f", x))[0]
+
+
+def _long_ms_web01():
+    """storeLongTimeSeriesMs (BaseTsdbTest.java:641-659): web01"""
+    return [L(1356998400000 + 500 * i, i) for i in range(1, 301)]
+
+
+def _float_steps_web01(step_ms, t0):
+    return [D(t0 + step_ms * (k + 1), v)
+            for k, v in enumerate(_f32_steps(1.25, 76.0, 0.25, True))]
+
+
+_FS = _float_steps_web01(30000, 1356998400000)   # storeFloatTimeSeriesSeconds
+_FMS = _float_steps_web01(500, 1356998400000)    # storeFloatTimeSeriesMs
+_QD = dict(Q_WIN, agg="sum")
+
+
+def _ds_avg_exp(n, step, first, last, mid):
+    return [D(1356998400000 + step * i,
+              first if i == 0 else (last if i >= n - 1 else mid(i)))
+            for i in range(n)]
+
+
+# runLongSingleTSDownsampleMs :174-209 (1000 ms avg)
+add(kind="group_by", name="tsdb_single_ts_downsample_ms",
+    spec=dict(_QD, ds_interval_ms=1000, ds_agg="avg"), groups=[[_long_ms_web01()]],
+    expect=[_ds_avg_exp(151, 1000, 1.0, 300.0, lambda i: i * 2 + 0.5)],
+    tol=0.00001, check_ts_mod=1000, cite=TQD + ":174-209")
+# runLongSingleTSDownsampleAndRateMs :250-285
+add(kind="group_by", name="tsdb_single_ts_downsample_rate_ms",
+    spec=dict(_QD, ds_interval_ms=1000, ds_agg="avg", rate=True),
+    groups=[[_long_ms_web01()]],
+    expect=[[[1356998401000 + 1000 * i, F32(1.5) if i == 0 else
+              (1.5 if i >= 149 else F32(2.0)), 1,
+              0.001 if i == 0 else (0.00001 if i >= 149 else 0.001)]
+             for i in range(150)]],
+    tol=0.001, check_ts_mod=1000, cite=TQD + ":250-285")
+# runFloatSingleTSDownsample :286-322 (60 s avg over storeFloatTimeSeriesSeconds)
+add(kind="group_by", name="tsdb_float_downsample",
+    spec=dict(_QD, ds_interval_ms=60000, ds_agg="avg"), groups=[[_FS]],
+    expect=[_ds_avg_exp(151, 60000, 1.25, 76.0, lambda i: (i + 2.25) / 2)],
+    tol=0.00001, check_ts_mod=60000, cite=TQD + ":286-322")
+# runFloatSingleTSDownsampleMs :323-359
+add(kind="group_by", name="tsdb_float_downsample_ms",
+    spec=dict(_QD, ds_interval_ms=1000, ds_agg="avg"), groups=[[_FMS]],
+    expect=[_ds_avg_exp(151, 1000, 1.25, 76.0, lambda i: (i + 2.25) / 2)],
+    tol=0.00001, check_ts_mod=1000, cite=TQD + ":323-359")
+# runFloatSingleTSDownsampleAndRate :360-399
+add(kind="group_by", name="tsdb_float_downsample_rate",
+    spec=dict(_QD, ds_interval_ms=60000, ds_agg="avg", rate=True), groups=[[_FS]],
+    expect=[[[1356998460000 + 60000 * i,
+              F32(0.00625) if (i == 0 or i >= 149) else F32(0.00833), 1,
+              0.000001 if (i == 0 or i >= 149) else 0.00001]
+             for i in range(150)]],
+    tol=0.00001, check_ts_mod=60000, cite=TQD + ":360-399")
+# runFloatSingleTSDownsampleAndRateMs :400-435
+add(kind="group_by", name="tsdb_float_downsample_rate_ms",
+    spec=dict(_QD, ds_interval_ms=1000, ds_agg="avg", rate=True), groups=[[_FMS]],
+    expect=[[[1356998401000 + 1000 * i,
+              F32(0.375) if (i == 0 or i >= 149) else F32(0.5), 1,
+              0.000001 if (i == 0 or i >= 149) else 0.00001]
+             for i in range(150)]],
+    tol=0.00001, check_ts_mod=1000, cite=TQD + ":400-435")
+# runLongSingleTSDownsampleCount :436-463 (60 s count)
+add(kind="group_by", name="tsdb_downsample_count",
+    spec=dict(_QD, ds_interval_ms=60000, ds_agg="count"), groups=[[WEB01]],
+    expect=[[D(1356998400000 + 60000 * i, 1 if i in (0, 150) else 2)
+             for i in range(151)]],
+    tol=0.00001, cite=TQD + ":436-463")
+# runFloatSingleTSDownsampleAndRateAndCount :563-599 (60 s count, rate)
+add(kind="group_by", name="tsdb_float_downsample_count_rate",
+    spec=dict(_QD, ds_interval_ms=60000, ds_agg="count", rate=True),
+    groups=[[_FS]],
+    expect=[[D(1356998460000 + 60000 * i,
+               F32(0.016666) if i == 0 else (F32(-0.016666) if i == 149 else 0.0))
+             for i in range(150)]],
+    tol=0.00001, check_ts_mod=60000, cite=TQD + ":563-599")
+
+
+def _scan_ms(start_s, end_s):
+    """TsdbQuery.getScanStart/EndTimeSeconds with a 0-interval ("all")
+    downsampler, in ms (TsdbQuery.java:1573-1675; pinned by scan_bounds)"""
+    a = start_s - start_s % 3600
+    b = end_s + (3600 - end_s % 3600)
+    return a * 1000, b * 1000
+
+
+# runLongSingleTSDownsampleAll :464-495, AllSubSet :497-528, AllNoEnd
+# :530-561 (TSQuery "0all-sum": one point at the query start; no end: "now",
+# any instant past the data)
+for _nm, _s0, _s1, _v, _c in (("all", 1356998400, 1357041600, 45150, ":464-495"),
+                              ("all_subset", 1356998500, 1356998600, 15,
+                               ":497-528"),
+                              ("all_no_end", 1356998400, 1500000000, 45150,
+                               ":530-561")):
+    _a, _b = _scan_ms(_s0, _s1)
+    add(kind="group_by", name="tsdb_downsample_" + _nm,
+        spec=dict(start_ms=_a, end_ms=_b, query_start_ms=_s0 * 1000,
+                  query_end_ms=_s1 * 1000, agg="sum", ds_string="0all-sum"),
+        groups=[[WEB01]], expect=[[D(_s0 * 1000, _v)]], tol=0.00001,
+        cite=TQD + _c)
+
+
+# runTSDownsampleWithMissingData :859-907 and its six callers :677-857:
+# {web01, web02} of storeLongTimeSeriesWithMissingData, 30 s downsample
+# with a fill policy, 1,560 points: the first 100 by the test's validator
+# (transcribed as generators), the rest its missing value (NaN or 0).
+def _v_const(c):
+    def g():
+        while True:
+            yield c
+    return g
+
+
+def _v_alt(even0, even_step, odd):
+    def g():
+        e = even0
+        while True:
+            e += even_step
+            yield e
+            yield odd
+    return g
+
+
+def _v_minmin():
+    e, ec, o, oc = -4.0, 6.0, -1.0, 6.0
+    while True:
+        e += ec
+        if e == 152.0:
+            e, ec = 149.0, -6.0
+        yield e
+        o += oc
+        if o == 155.0:
+            o, oc = 145.0, -6.0
+        yield o
+
+
+def _v_minsum():
+    e, ec, o, oc = -7.0, 12.0, -1.0, 12.0
+    while True:
+        e += ec
+        if e == 209.0:
+            e, ec = 197.0, -6.0
+        yield e
+        o += oc
+        if o == 311.0:
+            o, oc = 292.0, -12.0
+        yield o
+
+
+def _v_summin():
+    while True:
+        yield 301.0
+        yield 300.0
+
+
+for _nm, _agg, _dsa, _fill, _val, _c in (
+        ("sum_avg", "sum", "avg", "nan", _v_const(301.5), ":677-689"),
+        ("avg_sum", "avg", "sum", "nan", _v_alt(149.0, 3.0, 301.5), ":691-712"),
+        ("avg_avg", "avg", "avg", "zero", _v_const(150.75), ":714-726"),
+        ("sum_sum", "sum", "sum", "nan", _v_alt(298.0, 6.0, 603.0), ":728-750"),
+        ("min_min", "min", "min", "zero", _v_minmin, ":752-793"),
+        ("min_sum", "min", "sum", "nan", _v_minsum, ":795-837"),
+        ("sum_min", "sum", "min", "nan", _v_summin, ":839-857")):
+    _it = _val()
+    _miss = NAN if _fill == "nan" else 0.0
+    _exp = [D(1356998400000 + 30000 * i, next(_it) if i < 100 else _miss)
+            for i in range(1560)]
+    add(kind="group_by", name="tsdb_wnulls_" + _nm,
+        spec=dict(Q_WIN, agg=_agg, ds_interval_ms=30000, ds_agg=_dsa,
+                  fill=_fill),
+        groups=[_missing_data()], expect=[_exp], tol=0.0001,
+        cite=TQD + _c + ",859-907")
+
+# ------------------------------------------- TestTsdbQueryQueries (rate)
+# runRateCounterDefault :1130-1154 .. runRateCounterAnomallyDrop :1229-1251
+# (one series, 30 s cadence from 1356998430 s, counter rates; the junk
+# first rate is not emitted)
+_T = [1356998430000 + 30000 * k for k in range(4)]
+for _nm, _vals, _ro, _exp, _c in (
+        ("default", [LMAX - 55, LMAX - 25, 5], dict(counter_max=LMAX, reset_value=0),
+         [(_T[1], 1.0), (_T[2], 1.0)], ":1130-1154"),
+        ("default_noop", [30, 60, 90], dict(counter_max=LMAX, reset_value=0),
+         [(_T[1], 1.0), (_T[2], 1.0)], ":1156-1178"),
+        ("max_set", [45, 75, 5], dict(counter_max=100, reset_value=0),
+         [(_T[1], 1.0), (_T[2], 1.0)], ":1180-1202"),
+        ("anomaly", [45, 75, 25], dict(counter_max=10000, reset_value=35),
+         [(_T[1], 1.0), (_T[2], 0.0)], ":1204-1227"),
+        ("anomaly_drop", [45, 75, 25, 55],
+         dict(counter_max=10000, reset_value=35, drop_resets=True),
+         [(_T[1], 1.0), (_T[3], 1.0)], ":1229-1251")):
+    add(kind="group_by", name="tq_rate_counter_" + _nm,
+        spec=dict(Q_WIN, agg="sum", rate=True, counter=True, **_ro),
+        groups=[[[L(t, v) for t, v in zip(_T, _vals)]]],
+        expect=[[D(t, v) for t, v in _exp]], tol=0.001, cite=TQQ + _c)
+
+# runMultiCompact :1253-1302, runMultiCompactAndSingles :1304-1355: one
+# storage row of compacted columns (and single cells), compacted at query
+# time, decoded, one series: points 1..6 at 1 s steps (longs)
+_mq = [bytes([0, (k << 4) | 7]) for k in range(1, 7)]
+_mv = [_Lb(k) for k in range(1, 7)]
+_MC = [(_mq[0] + _mq[1], _mv[0] + _mv[1] + _ZB),
+       (_mq[2] + _mq[3], _mv[2] + _mv[3] + _ZB),
+       (_mq[4] + _mq[5], _mv[4] + _mv[5] + _ZB)]
+_MCS = [_MC[0], (_mq[2], _mv[2]), (_mq[3], _mv[3]), _MC[2]]
+for _nm, _cols, _c in (("multi_compact", _MC, ":1253-1302"),
+                       ("multi_compact_singles", _MCS, ":1304-1355")):
+    add(kind="rows_query", name="tq_" + _nm, base=1356998400,
+        columns=[[q.hex(), v.hex()] for q, v in _cols], fix_duplicates=True,
+        expect=[[1356998401000 + 1000 * k, k + 1] for k in range(6)],
+        cite=TQQ + _c)
+
+# ------------------------------------------- TestAggregationIterator (rest)
+TAI = "test/core/TestAggregationIterator.java"
+# testAggregate_seek :189-207 (one span, seeked once to the start: its
+# points unchanged)
+add(kind="group_by", name="ai_seek", spec=dict(SPEC_AI), groups=[[DP1]],
+    expect=[DP1], tol=0, filter=False, cite=TAI + ":189-207")
+# testDownsample_afterAggregation :150-187 (seven 10 s-avg spans summed,
+# then a 15 s-sum Downsampler over the aggregate)
+add(kind="group_by", name="ai_downsample_after_aggregation",
+    spec=dict(start_ms=BASE + 1000, end_ms=BASE + 100000, agg="sum",
+              ds_interval_ms=10000, ds_agg="avg"),
+    groups=[[DATA_5SEC] * 7],
+    post=dict(ds_interval_ms=15000, ds_agg="sum", query_start_ms=0,
+              query_end_ms=0),
+    expect=[[D(BASE, 7), D(BASE + 15000, 7), D(BASE + 30000, 14),
+             D(BASE + 45000, 7)]], tol=0, filter=False, cite=TAI + ":150-187")
+
 def _enc(x):
     if isinstance(x, float):
         if math.isnan(x):

@@ -143,3 +143,32 @@ def test_dev_offset_across_ranks_chained(engine, world):
     merged = _partials_emulated([engine], spec, hb, world)
     with pytest.raises(AssertionError):
         compare(merged[6:], ref[6:], False, where="merged", floor=0.0)
+
+
+def test_dev_offset_gauge_past_one_chain(engine):
+    """70,000 gauges of ~3e9 +- 1e4 in ONE group on one GPU — past the
+    65,536-member exact chain.  Default: the engine merges the in-order chunk
+    states with Chan's formula; the measured relative error against the
+    reference's one loop is recorded (printed) and bounded by the contract
+    include/otsdb_agg.h states for such groups (<= 1e-9 here, ~1e-11 typ.).
+    With OTSDB_SPEC_EXACT_ORDER the whole group is one chain per bucket:
+    bit for bit the loop (Aggregators.java:547-568)."""
+    import time
+    b = datasets.random_batch(70000, n_series=70000, big_group=True,
+                              span_ms=3600 * 1000, cadence_ms=60000,
+                              value_kind="offset", outside=False)
+    spec = _spec("dev", "max", "none", end=datasets.T0 + 3600 * 1000)
+    ref = pyoracle.group_by(spec, b)
+    got = engine.run(spec, b)
+    assert np.array_equal(got[0].ts, ref[0]["ts"])
+    g = got[0].bits.view(np.float64)
+    r = ref[0]["bits"].view(np.float64)
+    rel = float(np.max(np.abs(g - r) / np.abs(r)))
+    print("dev over 70,000 offset gauges, chunk-merged: max rel err %.3e" % rel)
+    assert rel <= 1e-9
+    spec.flags = abi.SPEC_EXACT_ORDER
+    t = time.perf_counter()
+    got = engine.run(spec, b)
+    dt = time.perf_counter() - t
+    print("exact order: %.1f ms (host entry, incl. transfers)" % (dt * 1e3))
+    compare(got, ref, True, where="dev70k/exact")

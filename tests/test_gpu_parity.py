@@ -319,15 +319,58 @@ def check(engine, spec, batch, exact, where="", floor=0.0):
 
 
 # ------------------------------------------------------------------ KATs
+def _points(dps):
+    pts = np.zeros(len(dps.ts), pyoracle.POINT)
+    pts["ts"], pts["bits"], pts["is_int"] = dps.ts, dps.bits, dps.is_int
+    return pts
+
+
 @pytest.mark.parametrize("c", kat.load_cases("group_by"), ids=lambda c: c["name"])
 def test_reference_kat(engine, c):
     spec = kat.spec_from_case(c["spec"])
     batch = kat.batch_from_case(c)
     got = engine.run(spec, batch)
     for g, exp in enumerate(c["expect"]):
-        pts = np.zeros(len(got[g].ts), pyoracle.POINT)
-        pts["ts"], pts["bits"], pts["is_int"] = got[g].ts, got[g].bits, got[g].is_int
+        pts = _points(got[g])
+        if c.get("post"):
+            # a Downsampler over the aggregate (TestAggregationIterator
+            # testDownsample_afterAggregation): the engine again, over the
+            # aggregate as one span
+            from opentsdb_amd.batch import HostBatch
+            agg1 = HostBatch.from_groups([[[
+                (int(p["ts"]), kat.point_value(p["bits"], p["is_int"]),
+                 0 if p["is_int"] else 1) for p in pts]]])
+            d = dict(c["post"], agg="sum", start_ms=0,
+                     end_ms=core.LONG_MAX // 2)
+            pts = _points(engine.run(kat.spec_from_case(d), agg1)[0])
         kat.check_points(pts, exp, c["tol"], "%s/g%d" % (c["name"], g))
+
+
+@pytest.mark.parametrize("c", [c for c in kat.load_cases("view") if "error" not in c],
+                         ids=lambda c: c["name"])
+def test_reference_view_kat(engine, c):
+    """The reference's Downsampler / FillingDownsampler / RateSpan KATs as
+    the one-span query the engine runs (kat.view_as_query): where that query
+    yields the view's own points (the oracle's group_by reproduces the KAT),
+    the engine must yield the KAT's points; elsewhere (a junk first rate, a
+    filling grid past the iterator's end) it must equal the oracle's query."""
+    spec, batch = kat.view_as_query(c)
+    ref = pyoracle.group_by(spec, batch)[0]
+    got = _points(engine.run(spec, batch)[0])
+    exp = c["expect"]
+    try:
+        kat.check_points(ref[:len(exp)] if c.get("prefix") else ref, exp,
+                         c["tol"], c["name"])
+        same = True
+    except AssertionError:
+        same = False
+    if same:
+        kat.check_points(got[:len(exp)] if c.get("prefix") else got, exp,
+                         c["tol"], c["name"])
+    else:
+        from opentsdb_amd.engine import DataPoints
+        compare([DataPoints(got["ts"], got["bits"], got["is_int"])], [ref],
+                False, where=c["name"])
 
 
 # ------------------------------------------------------- parity matrix

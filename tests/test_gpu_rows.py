@@ -640,3 +640,24 @@ def test_host_cells_entry_matches_oracle(engine, agg, ds):
     got = [DataPoints(ts[offs[g]:offs[g + 1]], val[offs[g]:offs[g + 1]],
                       isi[offs[g]:offs[g + 1]]) for g in range(len(offs) - 1)]
     compare(got, ref, agg in ("max",) and ds == "5m-max", where="host-cells")
+
+
+@pytest.mark.parametrize("c", kat.load_cases("rows_query"), ids=lambda c: c["name"])
+def test_rows_query_kats(engine, c):
+    """TestTsdbQueryQueries' multi-compaction rows (compacted columns, and
+    single cells between them, in one storage row) through the storage-row
+    query (otsdb_agg_run_raw: query-time compaction, span assembly, the raw
+    group-by): the points the test asserts, as longs."""
+    from opentsdb_amd.batch import groups_from_ids
+    cols = [(bytes.fromhex(q), bytes.fromhex(v), j)
+            for j, (q, v) in enumerate(c["columns"])]
+    hraw = storage.HostRawRows([(0, c["base"], cols)], with_ts=True)
+    hraw.n_series = 1
+    g_off, members = groups_from_ids(np.zeros(1, np.int64), 1)
+    spec = core.make_spec(1356998400000, 1357045200000, core.Aggregators.SUM,
+                          None, 1356998400000, 1357041600000)
+    offs, ts, val, isi = storage.run_raw(engine, spec, hraw, g_off, members, 64)
+    got = [[int(t), int(v)] for t, v in zip(ts[offs[0]:offs[1]],
+                                            val[offs[0]:offs[1]])]
+    assert got == c["expect"]
+    assert isi[offs[0]:offs[1]].all()
