@@ -226,7 +226,10 @@ typedef struct {
   /* Optional HOST copy of group_offsets (the same G+1 values) for the
    * device entries: the engine plans its tiles from it instead of reading
    * group_offsets back from the device (one copy + stream sync per call).
-   * NULL = read it back.  Ignored by the host entries.                    */
+   * NULL = read it back.  Ignored by the host entries.  The engine plans
+   * its tiles from this copy and trusts it: it must equal the device array
+   * at the call (a stale copy makes the kernels read members past a group;
+   * debug builds, -DOTSDB_DEBUG_SYNC, compare the last offset).            */
   const int64_t* group_offsets_host;
 } otsdb_batch;
 
@@ -532,8 +535,8 @@ otsdb_status otsdb_prof_read(otsdb_ctx* ctx, double* ms, int64_t* launches,
  * out[1] with the general one, out[2] uniform folds that met a qualifier of
  * other flags and were re-run with the general kernel.                      */
 otsdb_status otsdb_ctx_counters(otsdb_ctx* ctx, int64_t* out, int n);
-/* Test hook: the one-pass compaction's epoch (1 .. 2^24 - 1) the context's
- * next call increments, so tests can drive it across its wrap.            */
+/* Test hook: the one-pass compaction's epoch (1 .. 2^24 - 1, forward only)
+ * the context's next call increments, so tests can drive it to its wrap.  */
 otsdb_status otsdb_test_set_compact_epoch(otsdb_ctx* ctx, uint32_t epoch);
 
 /* ---- synthetic workload generator (bench / tests) ----------- */

@@ -240,8 +240,9 @@ def load(path=None):
     lib.otsdb_prof_enable.restype = C.c_int
     lib.otsdb_prof_read.argtypes = [vp, vp, vp, C.c_int, C.c_int]
     lib.otsdb_prof_read.restype = C.c_int
-    lib.otsdb_ctx_counters.argtypes = [vp, vp, C.c_int]
-    lib.otsdb_ctx_counters.restype = C.c_int
+    if hasattr(lib, "otsdb_ctx_counters"):  # (diagnostics; A/B of old builds)
+        lib.otsdb_ctx_counters.argtypes = [vp, vp, C.c_int]
+        lib.otsdb_ctx_counters.restype = C.c_int
     if hasattr(lib, "otsdb_test_set_compact_epoch"):  # (test hook)
         lib.otsdb_test_set_compact_epoch.argtypes = [vp, C.c_uint32]
         lib.otsdb_test_set_compact_epoch.restype = C.c_int

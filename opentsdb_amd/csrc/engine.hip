@@ -1424,7 +1424,20 @@ otsdb_status read_goff(otsdb_ctx* c, const otsdb_batch* b, bool device,
   if (!b->group_offsets) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "no groups");
   if (device && b->group_offsets_host) {
     // the caller's host copy of the same offsets: no read-back, no sync
+    // (the caller keeps it equal to the device array: include/otsdb_agg.h)
     memcpy(goff.data(), b->group_offsets_host, sizeof(int64_t) * goff.size());
+#ifdef OTSDB_DEBUG_SYNC
+    {  // debug builds: the host copy's total against the device's
+      int64_t last = 0;
+      HIP_TRY(hipMemcpyAsync(&last, b->group_offsets + b->n_groups,
+                             sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (last != goff.back())
+        return fail(OTSDB_E_ILLEGAL_ARGUMENT,
+                    "group_offsets_host[G] %lld != device %lld",
+                    (long long)goff.back(), (long long)last);
+    }
+#endif
   } else if (device) {
     HIP_TRY(hipMemcpyAsync(goff.data(), b->group_offsets,
                            sizeof(int64_t) * goff.size(),
@@ -3351,6 +3364,15 @@ otsdb_status otsdb_test_set_compact_epoch(otsdb_ctx* c, uint32_t epoch) {
   if (!c || epoch == 0 || epoch >= (1u << 24))
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "epoch %u", epoch);
   CtxLock lk(c);
+  // forward only: every granule then carries an epoch below the new one
+  // until the wrap (a step back would reuse epochs of live granules)
+  if (epoch < c->cmp_epoch)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "epoch %u < %u", epoch, c->cmp_epoch);
+  // and by whole ticket-slot rotations: the next call's slot is the one the
+  // last call's final block cleared (k_compact1)
+  if ((epoch - c->cmp_epoch) % kCmpSlots)
+    return fail(OTSDB_E_ILLEGAL_ARGUMENT, "epoch %u: not %u + k x %d", epoch,
+                c->cmp_epoch, kCmpSlots);
   c->cmp_epoch = epoch;
   return OTSDB_OK;
 }

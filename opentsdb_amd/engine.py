@@ -158,7 +158,14 @@ class Engine:
 
 class DeviceBatch:
     """A batch whose arrays are torch tensors resident in HBM (the bench and
-    multi-GPU path).  Tensors are kept alive by this object."""
+    multi-GPU path).  Tensors are kept alive by this object.
+
+    The engine plans its tiles from a host copy of group_offsets
+    (otsdb_batch.group_offsets_host), refreshed when the tensor is replaced
+    or torch bumps its version (an in-place torch op).  A write that torch
+    does not see — through data_ptr by native code, DLPack, or a kernel on
+    another stream — must be followed by invalidate_groups(), or the plan
+    and the device offsets disagree."""
 
     def __init__(self, offsets, ts, val, group_offsets, group_members,
                  is_float=None, series_float=None):
@@ -190,6 +197,12 @@ class DeviceBatch:
         b.group_members = p(self.group_members)
         b.group_offsets_host = self._goff_host().ctypes.data
         return b
+
+    def invalidate_groups(self):
+        """Drop the host copy of group_offsets (and the cached ABI struct):
+        the next call reads the device array again."""
+        self.__dict__.pop("_goff_cache", None)
+        self.__dict__.pop("_abi_cache", None)
 
     def _goff_host(self):
         """A host copy of group_offsets for otsdb_batch.group_offsets_host

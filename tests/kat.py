@@ -134,8 +134,21 @@ def view_as_query(c):
     d = dict(c["spec"])
     d["agg"] = "sum"
     if "start_ms" not in d:
+        # the iterator window: from the first bucket start (or the seek,
+        # which the iterator's seek rounds up the way Downsampler.seek does)
+        # to the last point — tight, so the engine's grid stays small
         d["start_ms"] = c.get("seek") or 0
-        d["end_ms"] = core.LONG_MAX // 2
+        d["end_ms"] = pts[-1][0] if pts else 1
+        iv = 0
+        if d.get("ds_interval_ms"):
+            iv = d["ds_interval_ms"]
+        elif d.get("ds_string") and not d["ds_string"].split("-")[0].endswith(
+                ("c", "all")):
+            iv = core.DownsamplingSpecification(d["ds_string"]).getInterval()
+        if iv and not c.get("seek") and pts:
+            d["start_ms"] = pts[0][0] - pts[0][0] % iv
+        elif not c.get("seek") and pts and not d.get("ds_string"):
+            d["start_ms"] = pts[0][0]
     elif c.get("seek"):
         d["start_ms"] = c["seek"]
     edges = cover = None

@@ -180,30 +180,42 @@ def test_host_group_offsets_match_readback(engine):
         assert np.array_equal(a, z)
 
 
-def test_compaction_epoch_wrap(engine):
+def test_compaction_epoch_wrap():
     """The one-pass compaction takes a look-back granule as this call's by
-    its epoch alone.  A 1,000-group call leaves granules of epoch 10; the
-    epoch is driven across its wrap (2^24 - 1 -> 4, where the engine clears
-    every granule) through small calls, and the next 1,000-group call runs
-    with epoch 10 again over other data: its look-back must not read the
-    old call's granules (other counts) as published (the advisor's round-5
-    finding).  Every call is compared with the oracle."""
-    big = datasets.random_batch(311, n_series=1000, n_groups=1000,
-                                span_ms=3600 * 1000)
-    big2 = datasets.random_batch(313, n_series=1000, n_groups=1000,
-                                 span_ms=3600 * 1000)
-    small = datasets.random_batch(312, n_series=12, n_groups=5)
-    spec = _spec("count", "count")
-    ref_big = pyoracle.group_by(spec, big)
-    ref_small = pyoracle.group_by(spec, small)
-    dbig, dsmall = _device(big), _device(small)
-    lib = engine.lib
-    assert lib.otsdb_test_set_compact_epoch(engine.ctx, 9) == 0
-    compare(_run_device(engine, spec, dbig), ref_big, True, where="big@10")
-    assert lib.otsdb_test_set_compact_epoch(engine.ctx, (1 << 24) - 3) == 0
-    for k in range(8):   # epochs 2^24-2, 2^24-1, 4, 5, ..., 9
+    its epoch alone.  On a fresh context, three small calls (epochs 1-3),
+    then a 1,000-group call leaves granules of epoch 4; the epoch is moved
+    on to 2^24 - 4, three small calls, and the next call wraps to epoch 4
+    again — a 1,000-group call over other data, whose look-back must not
+    read the first one's granules (other counts) as published: the engine
+    clears every granule at the wrap (the advisor's round-5 finding).  Every
+    call is compared with the oracle; the hook refuses to move back."""
+    from opentsdb_amd.engine import Engine
+    engine = Engine(0)
+    try:
+        big = datasets.random_batch(311, n_series=1000, n_groups=1000,
+                                    span_ms=3600 * 1000)
+        big2 = datasets.random_batch(313, n_series=1000, n_groups=1000,
+                                     span_ms=3600 * 1000)
+        small = datasets.random_batch(312, n_series=12, n_groups=5)
+        spec = _spec("count", "count")
+        ref_small = pyoracle.group_by(spec, small)
+        dsmall = _device(small)
+        for k in range(3):   # epochs 1, 2, 3
+            compare(_run_device(engine, spec, dsmall), ref_small, True,
+                    where="small%d" % k)
+        compare(_run_device(engine, spec, _device(big)),
+                pyoracle.group_by(spec, big), True, where="big@4")
+        lib = engine.lib
+        assert lib.otsdb_test_set_compact_epoch(engine.ctx, 3) != 0  # back
+        # (forward by whole rotations of the 4 ticket slots)
+        assert lib.otsdb_test_set_compact_epoch(engine.ctx, (1 << 24) - 3) != 0
+        assert lib.otsdb_test_set_compact_epoch(engine.ctx, (1 << 24) - 4) == 0
+        for k in range(3):   # epochs 2^24-3, 2^24-2, 2^24-1
+            compare(_run_device(engine, spec, dsmall), ref_small, True,
+                    where="small-wrap%d" % k)
+        compare(_run_device(engine, spec, _device(big2)),   # wraps to 4
+                pyoracle.group_by(spec, big2), True, where="big2@4")
         compare(_run_device(engine, spec, dsmall), ref_small, True,
-                where="small%d" % k)
-    compare(_run_device(engine, spec, _device(big2)),
-            pyoracle.group_by(spec, big2), True, where="big2@10")
-    assert lib.otsdb_test_set_compact_epoch(engine.ctx, 0) != 0
+                where="small@5")
+    finally:
+        engine.close()

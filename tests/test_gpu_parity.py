@@ -340,8 +340,10 @@ def test_reference_kat(engine, c):
             agg1 = HostBatch.from_groups([[[
                 (int(p["ts"]), kat.point_value(p["bits"], p["is_int"]),
                  0 if p["is_int"] else 1) for p in pts]]])
-            d = dict(c["post"], agg="sum", start_ms=0,
-                     end_ms=core.LONG_MAX // 2)
+            iv = c["post"]["ds_interval_ms"]
+            t0 = int(pts["ts"][0]) if len(pts) else 0
+            d = dict(c["post"], agg="sum", start_ms=t0 - t0 % iv,
+                     end_ms=int(pts["ts"][-1]) if len(pts) else 1)
             pts = _points(engine.run(kat.spec_from_case(d), agg1)[0])
         kat.check_points(pts, exp, c["tol"], "%s/g%d" % (c["name"], g))
 
