@@ -531,7 +531,15 @@ def main():
     torch.cuda.set_device(local)
     dist = None
     ranks_seen = 1
-    if world > 1:
+    # OTSDB_BENCH_SHARDED=1 at one rank: the cross-rank exchange path over a
+    # world of one (RCCL), to time the protocol itself on a one-GPU box
+    force_sharded = bool(os.environ.get("OTSDB_BENCH_SHARDED"))
+    if force_sharded and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if world > 1 or force_sharded:
         import torch.distributed as dist
         if backend == "nccl":
             dist.init_process_group("nccl",
@@ -547,7 +555,7 @@ def main():
     # exchange: partial all-gather of the shared groups, or the histogram
     # protocol for percentiles (opentsdb_amd/dist.py); host groups stay
     # rank-local
-    sharded = world > 1 and workload.spans_ranks(args.config)
+    sharded = (world > 1 or force_sharded) and workload.spans_ranks(args.config)
     G_glob = (workload.n_groups_global(args.config, n_series * world)
               if sharded else None)
     eng = Engine(local)
@@ -602,6 +610,11 @@ def main():
     stage_ms = read()
     eng.lib.otsdb_prof_enable(eng.ctx, 0)
 
+    sel_counts = None
+    if sharded and cfg["agg"] in ("p99", "p999", "median"):
+        c = eng.counters()  # the last otsdb_sel_* session
+        sel_counts = {"key_matrix_reads": c["sel_key_reads"],
+                      "hist_passes": c["sel_passes"]}
     total_points = n_points * world
     out_points = (last[0].n_points() if sharded
                   else int(res.offsets[-1].item()))
@@ -702,6 +715,7 @@ def main():
                              "group": stage_ms[2], "prep": stage_ms[3],
                              "compact": stage_ms[4]},
                 "generate_s": t_gen,
+                "sel_protocol": sel_counts,
             },
             "roofline": {
                 "bound": "hbm",

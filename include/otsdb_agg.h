@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OTSDB_ABI_VERSION 5
+#define OTSDB_ABI_VERSION 6
 
 /* ------------------------------------------------------------------------ */
 /* Status codes — 1:1 with the exceptions of the reference path.             */
@@ -330,47 +330,63 @@ otsdb_status otsdb_agg_finalize_device(otsdb_ctx* ctx,
                                        otsdb_result* out, void* hip_stream);
 
 /* ---- multi-GPU median / percentiles (series-sharded) -------------------- */
-/* Exact selection across ranks by radix select whose 256-bin histograms are
- * summed over the ranks.  The protocol, every rank in step:
+/* Exact selection across ranks: digit histograms summed over
+ * the ranks, at most two passes over each rank's local keys.  The protocol,
+ * every rank in step:
  *
- *   otsdb_sel_prepare_device(ctx, spec, batch, counts, emit)
+ *   otsdb_sel_prepare_device(ctx, spec, batch, counts, emit, krange)
  *       local shard -> per-(group, bucket) non-NaN contribution counts
- *       (int64 [G*n_buckets]) and emit flags (u8) in DEVICE memory
- *   all-reduce counts (sum) and emit (max)
- *   for pass in 0..7:
- *       otsdb_sel_hist_device(ctx, pass, counts, emit, hist_prev, hist)
- *           (pass 0 reads the global counts/emit; pass > 0 applies the
- *           global histogram of the previous pass, hist_prev) and writes
- *           this rank's histogram: u32 [G*n_buckets][2][256]
- *       all-reduce hist (sum); it becomes hist_prev
- *   otsdb_sel_finish_device(ctx, hist_last, result)
+ *       (int64 [G*n_buckets]), emit flags (u8) and key range (int64
+ *       [G*n_buckets][2]) in DEVICE memory
+ *   all-reduce counts (sum), emit (max), krange (min)
+ *   for pass = 0, 1, ...:
+ *       otsdb_sel_hist_device(ctx, pass, counts, emit, krange, hist_prev,
+ *                             hist, &more)
+ *           pass 0 reads the global counts / emit / krange; a later pass
+ *           applies hist_prev, the global histogram of the pass before (it
+ *           may be `hist` itself).  more == 0: the selection is resolved,
+ *           leave the loop.  more == 1: `hist` holds this rank's histogram
+ *           of the pass, u32 [G*n_buckets][OTSDB_SEL_BINS]; all-reduce it
+ *           (sum)
+ *   otsdb_sel_pick_device(ctx, picks)
+ *       int64 [G*n_buckets][2]: the key of an order statistic whose bin
+ *       holds one key over all ranks, from the rank holding it, else 0
+ *   all-reduce picks (sum)
+ *   otsdb_sel_finish_device(ctx, picks, result)
  *
- * otsdb_sel_hist_device returns without waiting for its kernels: the
- * caller's collective must be ordered after them on hip_stream (an RCCL
- * all-reduce enqueued there is); a binding that reads `hist` from the host
- * or from another stream calls otsdb_sel_hist_wait(ctx, hip_stream) first.
- * 8-bit digits rather than §8e's 11-bit ones: 2 x 256 bins per (group,
- * bucket) keep each all-reduce at 2 KB per bucket (C5: 2.9 MB a pass, against
- * 23.6 MB at 11 bits), at two more passes over the local keys.
+ * Pass 0 bins an offset digit, (key >> s) - (min >> s) over the global key
+ * range (2,048 bins); pass 1 the next 11 bits (2 x 10 when the estimator's
+ * two order statistics sit in different bins) and compacts the local keys
+ * still in play into a candidate pool; later passes and the pick read the
+ * pool only.  Local key-matrix reads: two at most (otsdb_ctx_counters [3]).
+ * otsdb_sel_hist_device reads its plan back (one stream sync) but returns
+ * without waiting for the histogram kernels: the caller's collective must be
+ * ordered after them on hip_stream (an RCCL all-reduce enqueued there is); a
+ * binding that reads `hist` from the host or from another stream calls
+ * otsdb_sel_hist_wait(ctx, hip_stream) first; the same holds for `picks`.
  * Every rank ends with the full result.  The batch's group_offsets span all
  * G global groups (empty where the rank holds no member).  Between prepare
  * and finish the context must not run other queries (the session lives in
  * its workspace).  Replaces PercentileAgg/Median.runDouble over the spans of
  * a group (Aggregators.java:397-431, :657-708) when the spans are spread
  * over GPUs.                                                               */
+#define OTSDB_SEL_BINS 2048
 otsdb_status otsdb_sel_prepare_device(otsdb_ctx* ctx,
                                       const otsdb_query_spec* spec,
                                       const otsdb_batch* batch,
                                       int64_t* counts, uint8_t* emit,
-                                      void* hip_stream);
+                                      int64_t* krange, void* hip_stream);
 otsdb_status otsdb_sel_hist_device(otsdb_ctx* ctx, int32_t pass,
                                    const int64_t* counts, const uint8_t* emit,
-                                   uint32_t* hist_prev, uint32_t* hist,
+                                   const int64_t* krange, uint32_t* hist_prev,
+                                   uint32_t* hist, int32_t* more,
                                    void* hip_stream);
-otsdb_status otsdb_sel_finish_device(otsdb_ctx* ctx, uint32_t* hist_last,
+otsdb_status otsdb_sel_pick_device(otsdb_ctx* ctx, int64_t* picks,
+                                   void* hip_stream);
+otsdb_status otsdb_sel_finish_device(otsdb_ctx* ctx, const int64_t* picks,
                                      otsdb_result* out, void* hip_stream);
-/* Blocks until the kernels otsdb_sel_hist_device enqueued on hip_stream (NULL:
- * the context's stream) are done, so `hist` is readable from anywhere.      */
+/* Blocks until the kernels otsdb_sel_hist_device / _pick_device enqueued on
+ * hip_stream (NULL: the context's stream) are done.                         */
 otsdb_status otsdb_sel_hist_wait(otsdb_ctx* ctx, void* hip_stream);
 
 /* ---- compacted-cell decode (RowSeq) ------------------- */
@@ -533,7 +549,9 @@ otsdb_status otsdb_prof_read(otsdb_ctx* ctx, double* ms, int64_t* launches,
  * operator's view of which cells-fold kernel ran): out[0] cells folds run
  * with the uniform kernel (every kept series one value type and width),
  * out[1] with the general one, out[2] uniform folds that met a qualifier of
- * other flags and were re-run with the general kernel.                      */
+ * other flags and were re-run with the general kernel; out[3] passes over
+ * the local key matrix and out[4] histogram passes of the last otsdb_sel_*
+ * session.                                                                 */
 otsdb_status otsdb_ctx_counters(otsdb_ctx* ctx, int64_t* out, int n);
 /* Test hook: the one-pass compaction's epoch (1 .. 2^24 - 1, forward only)
  * the context's next call increments, so tests can drive it to its wrap.  */

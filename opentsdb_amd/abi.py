@@ -145,7 +145,8 @@ EXPORTS = [
     "otsdb_gen_fill_device", "otsdb_prof_enable", "otsdb_prof_read",
     "otsdb_ctx_counters", "otsdb_test_set_compact_epoch",
     "otsdb_decode_cells_device", "otsdb_sel_prepare_device",
-    "otsdb_sel_hist_device", "otsdb_sel_hist_wait", "otsdb_sel_finish_device",
+    "otsdb_sel_hist_device", "otsdb_sel_hist_wait", "otsdb_sel_pick_device",
+    "otsdb_sel_finish_device",
     "otsdb_encode_cells_device", "otsdb_agg_run_cells_device",
     "otsdb_compact_rows_device", "otsdb_span_assemble_device",
     "otsdb_agg_run_raw_device", "otsdb_agg_run_raw", "otsdb_agg_run_cells",
@@ -209,12 +210,15 @@ def load(path=None):
     lib.otsdb_decode_cells_device.argtypes = [vp, C.POINTER(Cells), i64, vp,
                                               vp, vp, vp, i64, vp]
     lib.otsdb_decode_cells_device.restype = C.c_int
-    lib.otsdb_sel_prepare_device.argtypes = [vp, PS, PB, vp, vp, vp]
+    lib.otsdb_sel_prepare_device.argtypes = [vp, PS, PB, vp, vp, vp, vp]
     lib.otsdb_sel_prepare_device.restype = C.c_int
-    lib.otsdb_sel_hist_device.argtypes = [vp, i32, vp, vp, vp, vp, vp]
+    lib.otsdb_sel_hist_device.argtypes = [vp, i32, vp, vp, vp, vp, vp,
+                                          C.POINTER(C.c_int32), vp]
     lib.otsdb_sel_hist_device.restype = C.c_int
     lib.otsdb_sel_hist_wait.argtypes = [vp, vp]
     lib.otsdb_sel_hist_wait.restype = C.c_int
+    lib.otsdb_sel_pick_device.argtypes = [vp, vp, vp]
+    lib.otsdb_sel_pick_device.restype = C.c_int
     lib.otsdb_sel_finish_device.argtypes = [vp, vp, PR, vp]
     lib.otsdb_sel_finish_device.restype = C.c_int
     lib.otsdb_encode_cells_device.argtypes = [vp, PB, vp, vp, vp,

@@ -179,10 +179,11 @@ struct Work {
   uint32_t* key_cnt = nullptr;  // per (bucket, tile) non-NaN keys (fill mode)
   uint32_t* lg_kept = nullptr;  // per large group: holds a kept series
   SelState* sel = nullptr;
-  uint32_t* hist = nullptr;
+  XSel* xsel = nullptr;        // cross-rank selection (mode 2)
   Packed* comb = nullptr;      // two-level combine: first-level slices
   uint8_t* comb_emit = nullptr;
   uint8_t* redo = nullptr;     // fused-rate series handed back (Params.redo)
+  bool sel_fused = false;      // fill-mode selection: keys + counts by the transpose
 };
 
 }  // namespace
@@ -271,6 +272,20 @@ struct otsdb_ctx {
     Work W;
     int64_t G = 0, NB = 0, M = 0;
     int median = 0;
+    int32_t next_pass = 0;   // the pass otsdb_sel_hist_device expects
+    bool more = false;       // the last planned pass has work
+    bool pool_built = false;  // pass 1 compacted the candidates
+    bool need_pick = false;
+    // diagnostics (otsdb_ctx_counters): passes over the local key matrix
+    // and histogram passes of the last session
+    int64_t key_reads = 0, passes = 0;
+    void* pool = nullptr;    // candidates: keys [cap] | segments [cap]
+    size_t pool_bytes = 0;
+    int64_t pool_cap = 0;
+    // per segment: pool bounds [GB+1] | region offsets [GB+1] | fill [GB] |
+    // the offsets' scan storage
+    void* segmem = nullptr;
+    size_t segmem_bytes = 0, scan_tmp = 0;
   } sel;
 };
 
@@ -1005,7 +1020,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
       W.key_cnt = cv.take<uint32_t>((size_t)((goff.back() + KT_M - 1) / KT_M) * NB);
       W.lg_kept = cv.take<uint32_t>((size_t)T.LG + 1);
       W.sel = cv.take<SelState>((size_t)T.LG * NB);
-      W.hist = cv.take<uint32_t>((size_t)T.LG * NB * 512);
+      if (mode == 2) W.xsel = cv.take<XSel>((size_t)T.LG * NB);
     }
     return cv.off + 256;
   };
@@ -1168,7 +1183,9 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   }
   // percentiles over a FillingDownsampler grid with every group large: the
   // keys transpose applies the fill and counts, no k_transform / k_group
-  const bool sel_fused = is_selection(spec->agg_id) && mode == 0 &&
+  // (cross-rank, mode 2: the same transpose; otsdb_sel_prepare_device
+  // derives the counts from its per-tile counts)
+  const bool sel_fused = is_selection(spec->agg_id) && (mode == 0 || mode == 2) &&
                          P.sentinel && P.fill && !P.rate && !P.run_all &&
                          T.LG > 0 && T.LG == G;
   if (!fold && S > 0 && NB > 0 && !sel_fused) {
@@ -1198,6 +1215,11 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
           hipLaunchKernelGGL(k_keys_transpose<true>, dim3(blocks_for(M, KT_M)),
                              dim3(KT_THREADS), 0, st, NB, M, d_members, W.R, W.keys,
                              W.key_mm, F);
+        W.sel_fused = true;
+        if (mode == 2) {
+          HIP_TRY(hipGetLastError());
+          return OTSDB_OK;
+        }
         hipLaunchKernelGGL(k_seg_select, dim3((unsigned)NSEG), dim3(SS_THREADS),
                            0, st, NB, M, T.LG, T.lg_g, T.lg_off, T.lg_k,
                            (const uint64_t*)W.keys, (const SelState*)nullptr,
@@ -1226,7 +1248,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
           hipLaunchKernelGGL(k_keys_transpose<false>,
                              dim3(blocks_for(M, KT_M)),
                              dim3(KT_THREADS), 0, st, NB, M, d_members, W.R, W.keys,
-                             nullptr, SelFill{});
+                             W.key_mm, SelFill{});
         HIP_TRY(hipGetLastError());
         return OTSDB_OK;
       }
@@ -2582,6 +2604,8 @@ void otsdb_ctx_destroy(otsdb_ctx* c) {
     if (p) hipFree(p);
   if (c->raw_stage) hipFree(c->raw_stage);
   if (c->d_tiles) hipFree(c->d_tiles);
+  if (c->sel.pool) hipFree(c->sel.pool);
+  if (c->sel.segmem) hipFree(c->sel.segmem);
   if (c->cmp_flags) hipFree(c->cmp_flags);
   if (c->d_err) hipFree(c->d_err);
   for (auto e : c->ev_pool) hipEventDestroy(e);
@@ -2881,8 +2905,9 @@ otsdb_status otsdb_agg_finalize_device(otsdb_ctx* c,
 // ---- cross-rank median / percentile -------------------------
 otsdb_status otsdb_sel_prepare_device(otsdb_ctx* c, const otsdb_query_spec* spec,
                                       const otsdb_batch* b, int64_t* counts,
-                                      uint8_t* emit, void* hip_stream) {
-  if (!c || !spec || !b || !counts || !emit)
+                                      uint8_t* emit, int64_t* krange,
+                                      void* hip_stream) {
+  if (!c || !spec || !b || !counts || !emit || !krange)
     return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
   CtxLock lk(c);
   HIP_TRY(hipSetDevice(c->device));
@@ -2906,13 +2931,25 @@ otsdb_status otsdb_sel_prepare_device(otsdb_ctx* c, const otsdb_query_spec* spec
     rc = run_pipeline(c, spec, B, b->group_members, goff, P, W, 2, nullptr,
                       nullptr);
     const int64_t G = (int64_t)goff.size() - 1, GB = G * P.nb;
+    const Tiles T = tiles_of(c, G);
+    if (!rc && T.LG != G)  // build_tiles(sel_all): segment = (group, bucket)
+      rc = fail(OTSDB_E_DEVICE, "selection segments: %lld of %lld groups",
+                (long long)T.LG, (long long)G);
     if (!rc && GB > 0) {
-      hipLaunchKernelGGL(k_dense_to_counts, dim3(blocks_for(GB, 256)),
-                         dim3(256), 0, c->stream, GB, (const double*)W.out_val,
-                         (const uint8_t*)W.out_emit, counts, emit);
+      if (!W.sel_fused)
+        hipLaunchKernelGGL(k_dense_to_counts, dim3(blocks_for(GB, 256)),
+                           dim3(256), 0, c->stream, GB, (const double*)W.out_val,
+                           (const uint8_t*)W.out_emit, counts, emit);
+      hipLaunchKernelGGL(k_xsel_range, dim3((unsigned)GB), dim3(256), 0,
+                         c->stream, P.nb, goff.back(), T.LG, T.lg_off, T.lg_k,
+                         (const uint64_t*)W.keys, (const uint64_t*)W.key_mm,
+                         krange,
+                         W.sel_fused ? (const uint32_t*)W.key_cnt : nullptr,
+                         (const uint32_t*)W.lg_kept, counts, emit);
       HIP_TRY(hipGetLastError());
     }
     if (!rc) {
+      HIP_TRY(hipMemsetAsync((char*)c->d_err + 128, 0, 32, c->stream));
       HIP_TRY(hipMemcpyAsync(&c->h_small[0], c->d_err, sizeof(int),
                              hipMemcpyDeviceToHost, c->stream));
       HIP_TRY(hipStreamSynchronize(c->stream));
@@ -2921,56 +2958,155 @@ otsdb_status otsdb_sel_prepare_device(otsdb_ctx* c, const otsdb_query_spec* spec
                   "Next timestamp is supposed to be strictly greater");
     }
     if (!rc) {
-      c->sel.active = true;
-      c->sel.P = P;
-      c->sel.spec = *spec;
-      c->sel.W = W;
-      c->sel.G = G;
-      c->sel.NB = P.nb;
-      c->sel.M = goff.back();
-      c->sel.median = spec->agg_id == OTSDB_AGG_MEDIAN ? 1 : 0;
+      auto& S = c->sel;
+      S.active = true;
+      S.P = P;
+      S.spec = *spec;
+      S.W = W;
+      S.G = G;
+      S.NB = P.nb;
+      S.M = goff.back();
+      S.median = spec->agg_id == OTSDB_AGG_MEDIAN ? 1 : 0;
+      S.next_pass = 0;
+      S.more = false;
+      S.pool_built = false;
+      S.need_pick = false;
+      S.key_reads = 0;
+      S.passes = 0;
     }
   }
   return rc;
 }
 
+namespace {
+// the protocol's device words, after the error word (d_err + 128 .. 160):
+// per-pass flags, the scans' "broken" mark
+uint32_t* xs_flags(otsdb_ctx* c) { return (uint32_t*)((char*)c->d_err + 128); }
+uint32_t* xs_broken(otsdb_ctx* c) { return (uint32_t*)((char*)c->d_err + 152); }
+
+int64_t* xs_bnd(otsdb_ctx* c) { return (int64_t*)c->sel.segmem; }
+int64_t* xs_off(otsdb_ctx* c) {
+  return (int64_t*)c->sel.segmem + (c->sel.G * c->sel.NB + 1);
+}
+uint32_t* xs_segfill(otsdb_ctx* c) {
+  return (uint32_t*)(xs_off(c) + (c->sel.G * c->sel.NB + 1));
+}
+void* xs_scan_tmp(otsdb_ctx* c) {
+  const int64_t GB = c->sel.G * c->sel.NB;
+  return (char*)c->sel.segmem + (((size_t)(GB + 1) * 16 + (size_t)GB * 4 + 255) & ~(size_t)255);
+}
+
+XPool xs_pool(otsdb_ctx* c) {
+  auto& S = c->sel;
+  XPool p;
+  p.key = (uint64_t*)S.pool;
+  p.seg = S.pool ? (int64_t*)((char*)S.pool + (size_t)S.pool_cap * 8) : nullptr;
+  p.off = xs_off(c);
+  p.fill = xs_segfill(c);
+  p.cap = S.pool_cap;
+  p.flags = xs_broken(c);
+  return p;
+}
+}  // namespace
+
 otsdb_status otsdb_sel_hist_device(otsdb_ctx* c, int32_t pass,
                                    const int64_t* counts, const uint8_t* emit,
-                                   uint32_t* hist_prev, uint32_t* hist_out,
+                                   const int64_t* krange, uint32_t* hist_prev,
+                                   uint32_t* hist_out, int32_t* more,
                                    void* hip_stream) {
-  if (!c || !hist_out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  if (!c || !hist_out || !more) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
   CtxLock lk(c);
-  if (!c->sel.active) return fail(OTSDB_E_ILLEGAL_STATE, "no selection session");
-  if (pass < 0 || pass > 7) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "pass %d", pass);
+  auto& S = c->sel;
+  if (!S.active) return fail(OTSDB_E_ILLEGAL_STATE, "no selection session");
+  if (pass != S.next_pass)
+    return fail(OTSDB_E_ILLEGAL_STATE, "pass %d, expected %d", pass, S.next_pass);
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
-  auto& S = c->sel;
   const int64_t G = S.G, NB = S.NB, GB = G * NB;
   const Tiles T = tiles_of(c, G);
+  HIP_TRY(hipMemsetAsync(xs_flags(c), 0, 4, st));
   if (pass == 0) {
-    if (!counts || !emit) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null counts");
+    if (!counts || !emit || !krange)
+      return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null counts / krange");
     if (GB > 0) {
+      // the per-segment pool bookkeeping (bounds: the trailing one stays 0,
+      // so the scan's last offset is the pool's size)
+      size_t tmp = 0;
+      HIP_TRY(rocprim::exclusive_scan(nullptr, tmp, (const int64_t*)nullptr,
+                                      (int64_t*)nullptr, (int64_t)0,
+                                      (size_t)(GB + 1), rocprim::plus<int64_t>(),
+                                      st));
+      S.scan_tmp = tmp;
+      const size_t need =
+          (((size_t)(GB + 1) * 16 + (size_t)GB * 4 + 255) & ~(size_t)255) + tmp;
+      otsdb_status rc = ensure(&S.segmem, &S.segmem_bytes, need);
+      if (rc) return rc;
+      HIP_TRY(hipMemsetAsync(xs_bnd(c), 0, (size_t)(GB + 1) * 8, st));
       hipLaunchKernelGGL(k_counts_to_dense, dim3(blocks_for(GB, 256)), dim3(256),
                          0, st, GB, counts, emit, S.W.out_val, S.W.out_emit);
-      hipLaunchKernelGGL(k_sel_init, dim3(blocks_for(GB, 256)), dim3(256), 0,
-                         st, NB, G, T.lg_g, (const double*)S.W.out_val,
-                         (const uint8_t*)S.W.out_emit, S.W.sel, S.median,
-                         S.P.pct);
+      hipLaunchKernelGGL(k_xsel_init, dim3(blocks_for(GB, 256)), dim3(256), 0,
+                         st, GB, counts, emit, krange, S.W.xsel, S.median,
+                         S.P.pct, xs_flags(c));
     }
   } else {
     if (!hist_prev) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null hist_prev");
+    if (!S.more) return fail(OTSDB_E_ILLEGAL_STATE, "no pass planned");
     if (GB > 0)
-      hipLaunchKernelGGL(k_radix_select, dim3(blocks_for(GB * 2, 256)),
-                         dim3(256), 0, st, pass - 1, GB, hist_prev, S.W.sel);
+      hipLaunchKernelGGL(k_xsel_apply, dim3(blocks_for(GB, 4)), dim3(256), 0,
+                         st, GB, T.lg_k, NB, (const uint32_t*)hist_prev,
+                         S.W.xsel, xs_flags(c), xs_bnd(c));
+    if (pass == 1 && GB > 0) {  // the pool's regions: offsets, size off[GB]
+      size_t tmp = S.scan_tmp;
+      HIP_TRY(rocprim::exclusive_scan(xs_scan_tmp(c), tmp, (const int64_t*)xs_bnd(c),
+                                      xs_off(c), (int64_t)0, (size_t)(GB + 1),
+                                      rocprim::plus<int64_t>(), st));
+      HIP_TRY(hipMemcpyAsync(&c->h_small[5], xs_off(c) + GB, 8,
+                             hipMemcpyDeviceToHost, st));
+    }
   }
-  if (GB > 0) {
-    HIP_TRY(hipMemsetAsync(hist_out, 0, (size_t)GB * 512 * 4, st));
+  HIP_TRY(hipGetLastError());
+  // the plan is taken from all-reduced data: every rank reads the same flags
+  HIP_TRY(hipMemcpyAsync(&c->h_small[4], xs_flags(c), 4, hipMemcpyDeviceToHost,
+                         st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const uint32_t flags = (uint32_t)(c->h_small[4] & 0xFFFFFFFF);
+  const int64_t bound = pass == 1 ? c->h_small[5] : 0;
+  if (flags & XS_BROKEN) {
+    S.active = false;
+    return fail(OTSDB_E_DEVICE, "selection: the ranks' counts and keys disagree");
+  }
+  S.more = (flags & XS_MORE) != 0;
+  S.need_pick = (flags & XS_PICK) != 0;
+  S.next_pass = pass + 1;
+  *more = S.more ? 1 : 0;
+  if (!S.more || GB == 0) return OTSDB_OK;
+  HIP_TRY(hipMemsetAsync(hist_out, 0, (size_t)GB * XS_BINS * 4, st));
+  if (pass <= 1) {
+    int mode = 1;
+    if (pass == 1) {  // the candidates: every later pass and the pick read them
+      const int64_t cap = bound > 0 ? bound : 1;
+      otsdb_status rc = ensure(&S.pool, &S.pool_bytes, (size_t)cap * 16);
+      if (rc) return rc;
+      S.pool_cap = cap;
+      HIP_TRY(hipMemsetAsync((char*)S.pool + (size_t)cap * 8, 0xFF,
+                             (size_t)cap * 8, st));  // every slot unfilled
+      HIP_TRY(hipMemsetAsync(xs_segfill(c), 0, (size_t)GB * 4, st));
+      S.pool_built = true;
+      mode |= 2;
+    }
     if (T.LGCH > 0)
-      hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)(T.LGCH * NB)), dim3(256),
-                         0, st, pass, NB, S.M, G, T.lg_off, T.lg_k, T.lg_ch0,
-                         (const uint64_t*)S.W.keys, (const SelState*)S.W.sel,
-                         hist_out);
+      hipLaunchKernelGGL(k_xsel_scan, dim3((unsigned)(T.LGCH * NB)), dim3(XS_THREADS), 0,
+                         st, mode, NB, S.M, T.LG, T.lg_off, T.lg_k, T.lg_ch0,
+                         (const uint64_t*)S.W.keys, (const XSel*)S.W.xsel,
+                         hist_out, xs_pool(c), (int64_t*)nullptr);
+    ++S.key_reads;
+  } else {
+    const int64_t nblk = std::min<int64_t>(blocks_for(S.pool_cap, 256), 8192);
+    hipLaunchKernelGGL(k_xsel_pool, dim3((unsigned)nblk), dim3(256), 0, st, 1,
+                       xs_pool(c), (const XSel*)S.W.xsel, hist_out,
+                       (int64_t*)nullptr);
   }
+  ++S.passes;
   // no host sync: the caller's collective on the same stream consumes
   // hist_out (RCCL enqueues behind it; a gloo staging copy waits for it)
   HIP_TRY(hipGetLastError());
@@ -2984,25 +3120,55 @@ otsdb_status otsdb_sel_hist_wait(otsdb_ctx* c, void* hip_stream) {
   return OTSDB_OK;
 }
 
-otsdb_status otsdb_sel_finish_device(otsdb_ctx* c, uint32_t* hist_last,
-                                     otsdb_result* out, void* hip_stream) {
-  if (!c || !hist_last || !out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+otsdb_status otsdb_sel_pick_device(otsdb_ctx* c, int64_t* picks,
+                                   void* hip_stream) {
+  if (!c || !picks) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
   CtxLock lk(c);
-  if (!c->sel.active) return fail(OTSDB_E_ILLEGAL_STATE, "no selection session");
-  HIP_TRY(hipSetDevice(c->device));
-  StreamBinding bind(c, hip_stream);
   auto& S = c->sel;
+  if (!S.active) return fail(OTSDB_E_ILLEGAL_STATE, "no selection session");
+  if (S.next_pass == 0 || S.more)
+    return fail(OTSDB_E_ILLEGAL_STATE, "selection not resolved: run its passes");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = hip_stream ? (hipStream_t)hip_stream : c->stream;
   const int64_t G = S.G, NB = S.NB, GB = G * NB;
   const Tiles T = tiles_of(c, G);
-  HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
-  if (GB > 0) {
-    hipLaunchKernelGGL(k_radix_select, dim3(blocks_for(GB * 2, 256)), dim3(256),
-                       0, c->stream, 7, GB, hist_last, S.W.sel);
-    hipLaunchKernelGGL(k_sel_finish, dim3(blocks_for(GB, 256)), dim3(256), 0,
-                       c->stream, NB, G, T.lg_g, (const SelState*)S.W.sel,
-                       (const uint8_t*)S.W.out_emit, S.W.out_val, c->d_err,
-                       S.median, S.P.pct);
+  if (GB > 0) HIP_TRY(hipMemsetAsync(picks, 0, (size_t)GB * 16, st));
+  if (S.need_pick && GB > 0) {
+    if (S.pool_built) {
+      const int64_t nblk = std::min<int64_t>(blocks_for(S.pool_cap, 256), 8192);
+      hipLaunchKernelGGL(k_xsel_pool, dim3((unsigned)nblk), dim3(256), 0, st, 4,
+                         xs_pool(c), (const XSel*)S.W.xsel, (uint32_t*)nullptr,
+                         picks);
+    } else if (T.LGCH > 0) {
+      hipLaunchKernelGGL(k_xsel_scan, dim3((unsigned)(T.LGCH * NB)), dim3(XS_THREADS), 0,
+                         st, 4, NB, S.M, T.LG, T.lg_off, T.lg_k, T.lg_ch0,
+                         (const uint64_t*)S.W.keys, (const XSel*)S.W.xsel,
+                         (uint32_t*)nullptr, xs_pool(c), picks);
+      ++S.key_reads;
+    }
   }
+  S.next_pass = -1;  // picked
+  HIP_TRY(hipGetLastError());
+  return OTSDB_OK;
+}
+
+otsdb_status otsdb_sel_finish_device(otsdb_ctx* c, const int64_t* picks,
+                                     otsdb_result* out, void* hip_stream) {
+  if (!c || !picks || !out) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
+  CtxLock lk(c);
+  auto& S = c->sel;
+  if (!S.active) return fail(OTSDB_E_ILLEGAL_STATE, "no selection session");
+  if (S.next_pass != -1)
+    return fail(OTSDB_E_ILLEGAL_STATE, "otsdb_sel_pick_device first");
+  HIP_TRY(hipSetDevice(c->device));
+  StreamBinding bind(c, hip_stream);
+  const int64_t G = S.G, NB = S.NB, GB = G * NB;
+  HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
+  if (GB > 0)
+    hipLaunchKernelGGL(k_xsel_finish, dim3(blocks_for(GB, 256)), dim3(256), 0,
+                       c->stream, GB, (const XSel*)S.W.xsel, picks,
+                       (const uint8_t*)S.W.out_emit, S.W.out_val, c->d_err,
+                       S.median, S.P.pct, (const uint32_t*)xs_broken(c));
   otsdb_status rc = compact(c, S.P, G, S.W.out_val, S.W.out_emit, S.W.counts, out);
   if (!rc) rc = finish(c, G, out);
   S.active = false;
@@ -3354,9 +3520,9 @@ otsdb_status otsdb_prof_read(otsdb_ctx* c, double* ms, int64_t* launches,
 otsdb_status otsdb_ctx_counters(otsdb_ctx* c, int64_t* out, int n) {
   if (!c || (n > 0 && !out)) return fail(OTSDB_E_ILLEGAL_ARGUMENT, "null");
   CtxLock lk(c);
-  const int64_t v[3] = {c->n_cells_uniform, c->n_cells_general,
-                        c->n_cells_uni_miss};
-  for (int i = 0; i < n && i < 3; ++i) out[i] = v[i];
+  const int64_t v[5] = {c->n_cells_uniform, c->n_cells_general,
+                        c->n_cells_uni_miss, c->sel.key_reads, c->sel.passes};
+  for (int i = 0; i < n && i < 5; ++i) out[i] = v[i];
   return OTSDB_OK;
 }
 

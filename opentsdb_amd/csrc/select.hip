@@ -8,11 +8,11 @@
 //                    64x64 LDS tiles so both the read and the write coalesce
 //  k_sel_init        per (group, bucket): n (non-NaN contributions) -> the
 //                    one or two target ranks the estimator needs
-//  k_radix_hist      per pass (8 bits of key): LDS histograms of the keys
-//                    that still match each target's prefix, flushed with one
-//                    global atomic per non-empty bin
-//  k_radix_select    per (segment, target): picks the digit holding the rank
-//  k_sel_finish      keys -> doubles -> estimator, "Got Infinity" check
+//  k_seg_select      one workgroup per (group, bucket) segment: min / max,
+//                    11-bit digit passes, LDS gather + count select
+//  k_xsel_*          the cross-rank protocol (otsdb_sel_*): offset digit,
+//                    one more digit pass that also compacts the candidates,
+//                    pool passes, the unique key picked by its rank
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -22,7 +22,7 @@
 namespace otsdb {
 
 constexpr uint64_t KEY_NONE = ~0ULL;
-constexpr int SEL_CHUNK = 8192;  // keys per histogram block
+constexpr int SEL_CHUNK = 1 << 17;  // keys per k_xsel_scan block
 #ifndef OTSDB_KT_M  // members per k_keys_transpose tile: 64 (4 waves) or 128
 #define OTSDB_KT_M 64  // (8 waves, 1 KB key runs per bucket)
 #endif
@@ -232,113 +232,6 @@ __global__ void k_sel_init(int64_t nb, int64_t n_lg,
   sel[seg] = sel_state_of(count_emit[o] ? (int64_t)count_val[o] : 0, median, p);
 }
 
-__global__ __launch_bounds__(256) void k_radix_hist(
-    int pass, int64_t nb, int64_t M, int64_t n_lg,
-    const int64_t* __restrict__ lg_off, const int64_t* __restrict__ lg_k,
-    const int64_t* __restrict__ lg_ch0, const uint64_t* __restrict__ keys,
-    const SelState* __restrict__ sel, uint32_t* __restrict__ hist) {
-  __shared__ uint32_t h[2][256];
-  const int tid = threadIdx.x;
-  h[0][tid] = 0;
-  h[1][tid] = 0;
-  // block -> (large group, bucket, chunk)
-  const int64_t bid = blockIdx.x;
-  int64_t a = 0, z = n_lg;
-  while (z - a > 1) {
-    const int64_t mid = (a + z) >> 1;
-    if (lg_ch0[mid] * nb <= bid) a = mid;
-    else z = mid;
-  }
-  const int64_t lg = a;
-  const int64_t k = lg_k[lg];
-  const int64_t nch = (k + SEL_CHUNK - 1) / SEL_CHUNK;
-  const int64_t local = bid - lg_ch0[lg] * nb;
-  const int64_t b = local / nch, c = local - b * nch;
-  const int64_t seg = lg * nb + b;
-  const SelState s = sel[seg];
-  __syncthreads();
-  if (s.ntarget == 0) return;
-  const int shift = 56 - 8 * pass;
-  const uint64_t* col = keys + b * M + lg_off[lg];
-  const int64_t i1 = (c + 1) * SEL_CHUNK < k ? (c + 1) * SEL_CHUNK : k;
-  for (int64_t i = c * SEL_CHUNK + tid; i < i1; i += 256) {
-    const uint64_t key = col[i];
-    if (key == KEY_NONE) continue;
-    const unsigned d = (unsigned)(key >> shift) & 255u;
-    for (int t = 0; t < s.ntarget; ++t) {
-      if (pass == 0 || (key >> (shift + 8)) == (s.prefix[t] >> (shift + 8)))
-        atomicAdd(&h[t][d], 1u);
-    }
-  }
-  __syncthreads();
-  uint32_t* g = hist + seg * 512;
-  for (int t = 0; t < s.ntarget; ++t)
-    if (h[t][tid]) atomicAdd(&g[t * 256 + tid], h[t][tid]);
-}
-
-__global__ void k_radix_select(int pass, int64_t n_seg,
-                               uint32_t* __restrict__ hist,
-                               SelState* __restrict__ sel) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_seg * 2) return;
-  const int64_t seg = i >> 1;
-  const int t = (int)(i & 1);
-  SelState& s = sel[seg];
-  uint32_t* h = hist + seg * 512;
-  if (t >= s.ntarget) {
-    if (t == 1 && s.ntarget == 1) {
-      // keep target 1 in step with target 0 (same rank)
-    }
-    for (int d = 0; d < 256; ++d) h[t * 256 + d] = 0;
-    return;
-  }
-  const int shift = 56 - 8 * pass;
-  int64_t r = s.rank[t];
-  int64_t cum = 0;
-  int d = 0;
-  for (; d < 255; ++d) {
-    const int64_t c = h[t * 256 + d];
-    if (cum + c > r) break;
-    cum += c;
-  }
-  s.prefix[t] |= (uint64_t)d << shift;
-  s.rank[t] = r - cum;
-  for (int e = 0; e < 256; ++e) h[t * 256 + e] = 0;
-}
-
-__global__ void k_sel_finish(int64_t nb, int64_t n_lg,
-                             const int64_t* __restrict__ lg_g,
-                             const SelState* __restrict__ sel,
-                             const uint8_t* __restrict__ emit,
-                             double* __restrict__ out_val, int* err_word,
-                             int median, double p) {
-  const int64_t seg = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (seg >= n_lg * nb) return;
-  const int64_t lg = seg / nb, b = seg - lg * nb;
-  const int64_t o = lg_g[lg] * nb + b;
-  if (!emit[o]) return;
-  const SelState s = sel[seg];
-  double r;
-  if (s.n == 0) {
-    r = qnan();
-  } else if (median || s.n == 1) {
-    r = key_value(s.prefix[0]);
-  } else {
-    const double pos = p * (double)(s.n + 1);
-    if (pos < 1 || pos >= (double)s.n) {
-      r = key_value(s.prefix[0]);
-    } else {
-      const double fpos = __builtin_floor(pos);
-      const double dif = pos - fpos;
-      const double lower = key_value(s.prefix[0]);
-      const double upper = key_value(s.ntarget == 2 ? s.prefix[1] : s.prefix[0]);
-      r = lower + dif * (upper - lower);
-    }
-  }
-  if (is_inf(r)) atomicOr(err_word, ERR_INFINITY);
-  out_val[o] = r;
-}
-
 // cross-rank protocol (otsdb_sel_*): dense (group, bucket) non-NaN counts
 // as doubles <-> the int64 counts ranks all-reduce
 __global__ void k_dense_to_counts(int64_t GB, const double* __restrict__ val,
@@ -448,8 +341,7 @@ DEV double sel_value(int median, int64_t n, double pos, double lo, double hi) {
 
 // ------------------------------------------------------------------------
 // k_seg_select: the whole selection of one segment (large group, bucket) in
-// one workgroup, replacing k_radix_hist/k_radix_select's eight grid-wide
-// passes for rank-local groups.  (1) min / max key of the segment: bits above
+// one workgroup, for rank-local groups.  (1) min / max key of the segment: bits above
 // the highest differing bit are common to every key and need no pass; (2)
 // 11-bit digit passes (2,048-bin LDS histograms per target) only while a
 // target still has more than SS_CAP candidates; (3) the <= SS_CAP candidates
@@ -951,6 +843,478 @@ __global__ __launch_bounds__(64) void k_ds_select(Params P, BatchDev B,
     SM.of_has[s] = (uint8_t)(1 | (nk << 1));
     SM.of_rate[s] = r1;
   }
+}
+
+// ------------------------------------------------------------------------
+// Cross-rank median / percentile (otsdb_sel_*).  The members of
+// a (group, bucket) segment are spread over the ranks; each rank holds its
+// members' keys as [B][M] columns (k_keys_transpose).  Exact selection with
+// at most two reads of the local key matrix:
+//   prepare  local non-NaN counts and each segment's min / max key (krange,
+//            from k_keys_transpose's tile partials); the caller all-reduces
+//   pass 0   an OFFSET digit, (key >> s1) - (min >> s1) with s1 the smallest
+//            shift whose range fits 2,048 bins (k_seg_select's first pass):
+//            one histogram both targets share              [key read 1]
+//   pass 1   the next digit of each open target (11 bits, or 2 x 10 bits
+//            when the two targets' bins differ); the keys still matching a
+//            target are appended to a candidate pool       [key read 2]
+//   pass 2+  histograms over the pool only
+// A target is resolved when its prefix covers every bit, or when its bin
+// holds ONE key over all ranks: the rank holding that key writes it into
+// `picks` (the caller sums them) — from the pool, or from the key matrix
+// when no pass 1 ran [key read 2].  Every decision is taken from all-reduced
+// data, so the ranks plan the same passes.  The pool's capacity is bounded
+// per segment by min(local members, the global counts of the targets' bins).
+// Segment index = dense (group, bucket) index: the protocol lists every
+// group as large (build_tiles sel_all), lg_g the identity.
+// ------------------------------------------------------------------------
+constexpr int XS_BINS = 2048;
+constexpr uint64_t XS_SIGN = 0x8000000000000000ULL;
+enum : uint32_t { XS_MORE = 1, XS_PICK = 2, XS_BROKEN = 4 };
+
+struct XSel {
+  uint64_t prefix[2];  // the target's resolved bits (those >= shift)
+  int64_t rank[2];     // its rank inside that bin
+  int64_t cnt[2];      // keys in that bin over all ranks
+  int64_t n;           // non-NaN contributions over all ranks
+  uint64_t base;       // offset pass: min >> s1
+  int32_t shift[2];    // bits below the prefix (64: none resolved)
+  int32_t w[2];        // the planned pass's digit width (0: not in it)
+  int32_t ntarget;
+  int32_t split;       // planned pass: two 1,024-bin halves (else one 2,048)
+  int32_t offset;      // planned pass is the offset digit
+  int32_t s1;
+  uint8_t done[2];     // 0 open, 1 the prefix is the key, 2 one key in its bin
+  uint8_t _pad[6];
+};
+
+DEV bool xs_match(const XSel& s, int t, uint64_t key) {
+  return s.shift[t] >= 64 || (key >> s.shift[t]) == (s.prefix[t] >> s.shift[t]);
+}
+DEV uint32_t xs_digit(const XSel& s, int t, uint64_t key) {
+  return (uint32_t)(key >> (s.shift[t] - s.w[t])) & ((1u << s.w[t]) - 1u);
+}
+// keys the pool keeps: those of a target not yet resolved to its prefix
+DEV bool xs_keep(const XSel& s, uint64_t key) {
+  return (s.ntarget > 0 && s.done[0] != 1 && xs_match(s, 0, key)) ||
+         (s.ntarget > 1 && s.done[1] != 1 && xs_match(s, 1, key));
+}
+// the bin a key counts in for the planned pass, or -1
+DEV int xs_bin(const XSel& s, uint64_t key) {
+  if (s.offset) return (int)((key >> s.s1) - s.base);
+  if (!s.split) {
+    const int t = s.w[0] ? 0 : 1;
+    return xs_match(s, t, key) ? (int)xs_digit(s, t, key) : -1;
+  }
+  return -1;  // split: per target (xs_bins2)
+}
+// plans the next digit pass of the open targets; false: none is open
+DEV bool xs_plan(XSel& s) {
+  s.w[0] = s.w[1] = 0;
+  s.offset = 0;
+  s.split = 0;
+  const bool o0 = s.ntarget > 0 && s.done[0] == 0;
+  const bool o1 = s.ntarget > 1 && s.done[1] == 0;
+  if (!o0 && !o1) return false;
+  const bool same = o0 && o1 && s.prefix[0] == s.prefix[1] && s.shift[0] == s.shift[1];
+  s.split = (o0 && o1 && !same) ? 1 : 0;
+  const int wmax = s.split ? 10 : 11;
+  if (o0) s.w[0] = s.shift[0] < wmax ? s.shift[0] : wmax;
+  if (o1) s.w[1] = s.shift[1] < wmax ? s.shift[1] : wmax;
+  return true;
+}
+// one key of the pass: LDS (or global) histogram h of the segment
+DEV void xs_count(const XSel& s, uint64_t key, uint32_t* h) {
+  if (!s.split) {
+    const int d = xs_bin(s, key);
+    if (d >= 0) atomicAdd(&h[d], 1u);
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+    if (s.w[t] && xs_match(s, t, key)) atomicAdd(&h[t * 1024 + xs_digit(s, t, key)], 1u);
+}
+
+// prepare: the segment's local min / max non-NONE key as all-reducible
+// int64 (min of key ^ sign, and of ~(max ^ sign)); empty: INT64_MAX twice.
+// cnt_p (fill mode, k_keys_transpose<true>): also the segment's non-NaN
+// count and emit flag (every bucket of a group holding a kept series)
+__global__ __launch_bounds__(256) void k_xsel_range(
+    int64_t nb, int64_t M, int64_t n_lg, const int64_t* __restrict__ lg_off,
+    const int64_t* __restrict__ lg_k, const uint64_t* __restrict__ keys,
+    const uint64_t* __restrict__ mm, int64_t* __restrict__ krange,
+    const uint32_t* __restrict__ cnt_p, const uint32_t* __restrict__ kept,
+    int64_t* __restrict__ counts, uint8_t* __restrict__ emit) {
+  __shared__ uint64_t red[3][4];
+  const int tid = threadIdx.x;
+  const int64_t seg = blockIdx.x;
+  if (seg >= n_lg * nb) return;
+  const int64_t lg = seg / nb, b = seg - lg * nb;
+  const int64_t o0 = lg_off[lg], k = lg_k[lg];
+  const uint64_t* col = keys + b * M + o0;
+  uint64_t mn = ~0ULL, mx = 0, nn = 0;
+  auto fold = [&](uint64_t key) {
+    if (key == KEY_NONE) return;
+    mn = key < mn ? key : mn;
+    mx = key > mx ? key : mx;
+    ++nn;
+  };
+  // k_keys_transpose's per-(bucket, KT_M-member tile) partials for the
+  // tiles wholly inside the segment, the keys of the partial tiles directly
+  const int64_t ntiles = (M + KT_M - 1) / KT_M;
+  const int64_t t_lo = (o0 + KT_M - 1) / KT_M, t_hi = (o0 + k) / KT_M;
+  if (t_hi > t_lo) {
+    const uint64_t* pm = mm + 2 * (b * ntiles);
+    for (int64_t t = t_lo + tid; t < t_hi; t += 256) {
+      mn = pm[2 * t] < mn ? pm[2 * t] : mn;
+      mx = pm[2 * t + 1] > mx ? pm[2 * t + 1] : mx;
+      if (cnt_p) nn += cnt_p[b * ntiles + t];
+    }
+    const int64_t e0 = t_lo * KT_M - o0, e1 = t_hi * KT_M - o0;
+    for (int64_t i = tid; i < e0; i += 256) fold(col[i]);
+    for (int64_t i = e1 + tid; i < k; i += 256) fold(col[i]);
+  } else {
+    for (int64_t i = tid; i < k; i += 256) fold(col[i]);
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint64_t a = __shfl_xor(mn, d), z = __shfl_xor(mx, d);
+    mn = a < mn ? a : mn;
+    mx = z > mx ? z : mx;
+    nn += __shfl_xor(nn, d);
+  }
+  if (LANE == 0) {
+    red[0][tid >> 6] = mn;
+    red[1][tid >> 6] = mx;
+    red[2][tid >> 6] = nn;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int j = 1; j < 4; ++j) {
+      mn = red[0][j] < mn ? red[0][j] : mn;
+      mx = red[1][j] > mx ? red[1][j] : mx;
+      nn += red[2][j];
+    }
+    krange[2 * seg] = (int64_t)(mn ^ XS_SIGN);
+    krange[2 * seg + 1] = ~(int64_t)(mx ^ XS_SIGN);
+    if (cnt_p) {
+      const bool e = kept[lg] != 0;
+      counts[seg] = e ? (int64_t)nn : 0;
+      emit[seg] = e ? 1 : 0;
+    }
+  }
+}
+
+// pass 0: the global counts and key range -> targets, the offset pass
+__global__ void k_xsel_init(int64_t n_seg, const int64_t* __restrict__ counts,
+                            const uint8_t* __restrict__ emit,
+                            const int64_t* __restrict__ krange,
+                            XSel* __restrict__ sel, int median, double p,
+                            uint32_t* __restrict__ flags) {
+  const int64_t seg = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (seg >= n_seg) return;
+  const int64_t n = emit[seg] ? counts[seg] : 0;
+  const SelState ss = sel_state_of(n, median, p);
+  XSel x;
+  x.n = n;
+  x.ntarget = ss.ntarget;
+  x.base = 0;
+  x.s1 = 0;
+  x.offset = 0;
+  x.split = 0;
+  x._pad[0] = x._pad[1] = x._pad[2] = x._pad[3] = x._pad[4] = x._pad[5] = 0;
+  for (int t = 0; t < 2; ++t) {
+    x.prefix[t] = 0;
+    x.rank[t] = ss.rank[t];
+    x.cnt[t] = n;
+    x.shift[t] = 64;
+    x.w[t] = 0;
+    x.done[t] = 0;
+  }
+  if (x.ntarget > 0) {
+    const uint64_t mn = (uint64_t)krange[2 * seg] ^ XS_SIGN;
+    const uint64_t mx = (uint64_t)~krange[2 * seg + 1] ^ XS_SIGN;
+    if (mn >= mx) {  // one distinct key (mn > mx: counted keys but none seen)
+      if (mn > mx) atomicOr(flags, (uint32_t)XS_BROKEN);
+      for (int t = 0; t < x.ntarget; ++t) {
+        x.prefix[t] = mn;
+        x.shift[t] = 0;
+        x.done[t] = 1;
+      }
+    } else {
+      int s1 = 64 - __builtin_clzll(mx - mn) - 11;
+      if (s1 < 0) s1 = 0;
+      while ((mx >> s1) - (mn >> s1) >= (uint64_t)XS_BINS) ++s1;
+      x.s1 = s1;
+      x.base = mn >> s1;
+      x.offset = 1;
+      atomicOr(flags, (uint32_t)XS_MORE);
+    }
+  }
+  sel[seg] = x;
+}
+
+// the keys of one (segment, SEL_CHUNK chunk) per block: the planned pass's
+// histogram (mode 1), candidates appended to the pool (mode 2), the unique
+// key of a target picked (mode 4)
+// the pool: one region per segment, [off[seg], off[seg + 1]) sized by the
+// apply's bound and filled through a per-segment counter; unfilled slots
+// keep seg = -1
+struct XPool {
+  uint64_t* key;
+  int64_t* seg;
+  const int64_t* off;  // [n_seg + 1] exclusive scan of the bounds
+  uint32_t* fill;      // [n_seg]
+  int64_t cap;
+  uint32_t* flags;
+};
+
+constexpr int XS_THREADS = 1024;
+__global__ __launch_bounds__(XS_THREADS) void k_xsel_scan(
+    int mode, int64_t nb, int64_t M, int64_t n_lg,
+    const int64_t* __restrict__ lg_off, const int64_t* __restrict__ lg_k,
+    const int64_t* __restrict__ lg_ch0, const uint64_t* __restrict__ keys,
+    const XSel* __restrict__ sel, uint32_t* __restrict__ hist, XPool pool,
+    int64_t* __restrict__ picks) {
+  __shared__ uint32_t h[XS_BINS];
+  const int tid = threadIdx.x, lane = LANE;
+  const int64_t bid = blockIdx.x;
+  int64_t a = 0, z = n_lg;
+  while (z - a > 1) {
+    const int64_t mid = (a + z) >> 1;
+    if (lg_ch0[mid] * nb <= bid) a = mid;
+    else z = mid;
+  }
+  const int64_t lg = a;
+  const int64_t k = lg_k[lg];
+  const int64_t nch = (k + SEL_CHUNK - 1) / SEL_CHUNK;
+  const int64_t local = bid - lg_ch0[lg] * nb;
+  const int64_t b = local / nch, c = local - b * nch;
+  const int64_t seg = lg * nb + b;
+  const XSel s = sel[seg];
+  const bool hon = (mode & 1) && (s.offset || s.w[0] || s.w[1]);
+  const bool app = (mode & 2) && s.ntarget > 0 && (s.done[0] != 1 ||
+                                                   (s.ntarget > 1 && s.done[1] != 1));
+  const bool pk = (mode & 4) && (s.done[0] == 2 || (s.ntarget > 1 && s.done[1] == 2));
+  if (!hon && !app && !pk) return;  // block-uniform
+  if (hon)
+    for (int j = tid; j < XS_BINS; j += XS_THREADS) h[j] = 0;
+  __syncthreads();
+  const uint64_t* col = keys + b * M + lg_off[lg];
+  const int64_t i0 = c * SEL_CHUNK;
+  const int64_t i1 = i0 + SEL_CHUNK < k ? i0 + SEL_CHUNK : k;
+  auto one = [&](uint64_t key) {
+    const bool valid = key != KEY_NONE;
+    if (hon && valid) xs_count(s, key, h);
+    if (app) {  // wave ballot: one pool atomic per wave and key slot
+      const bool cand = valid && xs_keep(s, key);
+      const uint64_t m = __ballot(cand);
+      if (m) {
+        const int lead = __builtin_ctzll(m);
+        uint32_t at = 0;
+        if (lane == lead) at = atomicAdd(&pool.fill[seg], (uint32_t)__popcll(m));
+        at = (uint32_t)__builtin_amdgcn_readlane((int)at, lead);
+        if (cand) {
+          const int64_t q = pool.off[seg] + at + __popcll(m & ((1ULL << lane) - 1));
+          if (q < pool.off[seg + 1]) {
+            pool.key[q] = key;
+            pool.seg[q] = seg;
+          } else {
+            atomicOr(pool.flags, (uint32_t)XS_BROKEN);
+          }
+        }
+      }
+    }
+    if (pk && valid) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        if (t < s.ntarget && s.done[t] == 2 && xs_match(s, t, key))
+          picks[2 * seg + t] = (int64_t)key;
+    }
+  };
+  // XS_UNROLL keys a lane in flight (wave-strided, so each load is 512
+  // coalesced bytes); every lane runs the same trip count (the ballots)
+  constexpr int XS_UNROLL = 8;
+  const int64_t w0 = i0 + (tid - lane) * XS_UNROLL;
+  for (int64_t i = w0; i < i1; i += XS_THREADS * XS_UNROLL) {
+    uint64_t kk[XS_UNROLL];
+#pragma unroll
+    for (int j = 0; j < XS_UNROLL; ++j) {
+      const int64_t x = i + 64 * j + lane;
+      kk[j] = x < i1 ? col[x] : KEY_NONE;
+    }
+#pragma unroll
+    for (int j = 0; j < XS_UNROLL; ++j) one(kk[j]);
+  }
+  if (!hon) return;
+  __syncthreads();
+  uint32_t* g = hist + seg * XS_BINS;
+  for (int j = tid; j < XS_BINS; j += XS_THREADS)
+    if (h[j]) atomicAdd(&g[j], h[j]);
+}
+
+// passes 2+ and the pick over the pool: a few keys per segment, global
+// atomics
+__global__ __launch_bounds__(256) void k_xsel_pool(
+    int mode, XPool pool, const XSel* __restrict__ sel, uint32_t* __restrict__ hist,
+    int64_t* __restrict__ picks) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pool.cap;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t seg = pool.seg[i];
+    if (seg < 0) continue;  // an unfilled slot
+    const uint64_t key = pool.key[i];
+    const XSel& s = sel[seg];
+    if ((mode & 1) && (s.w[0] || s.w[1])) xs_count(s, key, hist + seg * XS_BINS);
+    if (mode & 4) {
+      for (int t = 0; t < 2; ++t)
+        if (t < s.ntarget && s.done[t] == 2 && xs_match(s, t, key))
+          picks[2 * seg + t] = (int64_t)key;
+    }
+  }
+}
+
+// one wave per segment: the global histogram of the pass just run -> each
+// target's digit, rank and bin count; resolution; the next pass planned.
+// flags: XS_MORE a pass is planned, XS_PICK a target waits for its key
+// (set once: a flag word every segment hits is read before its atomic);
+// bnd[seg] = the segment's pool bound
+__global__ __launch_bounds__(256) void k_xsel_apply(
+    int64_t n_seg, const int64_t* __restrict__ seg_k,  // local members (lg_k)
+    int64_t nb, const uint32_t* __restrict__ hist, XSel* __restrict__ sel,
+    uint32_t* __restrict__ flags, int64_t* __restrict__ bnd) {
+  const int64_t seg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (seg >= n_seg) return;  // wave-uniform
+  const int lane = LANE;
+  XSel s = sel[seg];
+  const bool ran = s.offset || s.w[0] || s.w[1];
+  if (ran) {
+    const uint32_t* h = hist + seg * XS_BINS;
+    for (int t = 0; t < 2; ++t) {
+      const bool in = s.offset ? (t < s.ntarget && s.done[t] == 0) : s.w[t] > 0;
+      if (!in) continue;
+      const uint32_t* ht = h + (s.split ? t * 1024 : 0);
+      const int per = (s.split ? 1024 : XS_BINS) / 64;  // 16 / 32 bins a lane
+      // the lane's bins in registers (16-byte loads), summed and searched
+      // there
+      uint32_t cb[32];
+      const uint4* hv = reinterpret_cast<const uint4*>(ht + lane * per);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (q < per / 4) v = hv[q];
+        cb[4 * q] = v.x;
+        cb[4 * q + 1] = v.y;
+        cb[4 * q + 2] = v.z;
+        cb[4 * q + 3] = v.w;
+      }
+      uint32_t sum = 0;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) sum += cb[j];
+      uint32_t incl = sum;
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d);
+        if (lane >= d) incl += y;
+      }
+      const int64_t excl = (int64_t)incl - sum;
+      const int64_t rr = s.rank[t];
+      const bool mine = rr >= excl && rr < (int64_t)incl;
+      int64_t below = 0, cnt = 0;
+      int dig = 0;
+      if (mine) {
+        int64_t cum = excl;
+        int jj = per - 1;
+        bool found = false;
+#pragma unroll
+        for (int j = 0; j < 31; ++j) {
+          if (!found && j < per - 1) {
+            if (rr < cum + cb[j]) {
+              jj = j;
+              found = true;
+            } else {
+              cum += cb[j];
+            }
+          }
+        }
+        uint32_t cj = 0;
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+          if (j == jj) cj = cb[j];
+        dig = lane * per + jj;
+        below = cum;
+        cnt = cj;
+      }
+      const uint64_t who = __ballot(mine);
+      if (!who) {  // the rank is past the bins: the ranks' data disagree
+        if (lane == 0) atomicOr(flags, (uint32_t)XS_BROKEN);
+        s.done[t] = 1;
+        s.shift[t] = 0;
+        continue;
+      }
+      const int src = __builtin_ctzll(who);
+      dig = __shfl(dig, src);
+      below = readlane_l(below, src);
+      cnt = readlane_l(cnt, src);
+      s.rank[t] = rr - below;
+      s.cnt[t] = cnt;
+      if (s.offset) {
+        s.prefix[t] = (s.base + (uint64_t)dig) << s.s1;
+        s.shift[t] = s.s1;
+      } else {
+        s.shift[t] -= s.w[t];
+        s.prefix[t] |= (uint64_t)dig << s.shift[t];
+      }
+      if (s.shift[t] == 0) s.done[t] = 1;
+      else if (cnt == 1) s.done[t] = 2;
+    }
+  }
+  const bool more = xs_plan(s);
+  if (lane == 0) {
+    sel[seg] = s;
+    uint32_t f = more ? (uint32_t)XS_MORE : 0u;
+    if (s.done[0] == 2 || (s.ntarget > 1 && s.done[1] == 2)) f |= XS_PICK;
+    if (f && (__hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
+              f) != f)
+      atomicOr(flags, f);
+    // the pool's bound: local keys matching a target not resolved to its
+    // prefix (one bin when the two share it)
+    int64_t cb = 0;
+    const bool k0 = s.ntarget > 0 && s.done[0] != 1;
+    const bool k1 = s.ntarget > 1 && s.done[1] != 1;
+    if (k0) cb += s.cnt[0];
+    if (k1 && !(k0 && s.prefix[0] == s.prefix[1] && s.shift[0] == s.shift[1]))
+      cb += s.cnt[1];
+    const int64_t lk = seg_k[seg / nb];
+    if (cb > lk) cb = lk;
+    bnd[seg] = cb;
+  }
+}
+
+// the estimator over the resolved order statistics (k_seg_select's tail)
+__global__ void k_xsel_finish(int64_t n_seg, const XSel* __restrict__ sel,
+                              const int64_t* __restrict__ picks,
+                              const uint8_t* __restrict__ emit,
+                              double* __restrict__ out_val, int* err_word,
+                              int median, double p,
+                              const uint32_t* __restrict__ broken) {
+  const int64_t seg = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (seg == 0 && *broken) atomicOr(err_word, ERR_INTERNAL);  // pool overflow
+  if (seg >= n_seg || !emit[seg]) return;
+  const XSel s = sel[seg];
+  double r = qnan();
+  if (s.ntarget > 0) {
+    uint64_t v[2] = {0, 0};
+    for (int t = 0; t < s.ntarget; ++t) {
+      if (s.done[t] == 1) v[t] = s.prefix[t];
+      else if (s.done[t] == 2) v[t] = (uint64_t)picks[2 * seg + t];
+      else atomicOr(err_word, ERR_INTERNAL);
+    }
+    if (s.ntarget == 1) v[1] = v[0];
+    double pos = 0.0;
+    int64_t r0, r1;
+    sel_ranks(median, p, s.n, &r0, &r1, &pos);
+    r = sel_value(median, s.n, pos, key_value(v[0]), key_value(v[1]));
+  }
+  if (is_inf(r)) atomicOr(err_word, ERR_INFINITY);
+  out_val[seg] = r;
 }
 
 }  // namespace otsdb

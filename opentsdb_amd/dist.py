@@ -7,8 +7,10 @@ per-(group, bucket) partials on every rank (otsdb_agg_partials_device),
 all-gathered over RCCL (torch.distributed, backend "nccl"; "gloo" in CPU
 tests) and merged in rank order, which is series order, by
 otsdb_agg_finalize_device.  Median / percentiles across ranks run the
-otsdb_sel_* protocol instead: all-reduced contribution counts, then eight
-radix-select passes whose 256-bin histograms are all-reduced (exact).
+otsdb_sel_* protocol instead: all-reduced contribution counts and key
+ranges, then digit passes whose 2,048-bin histograms are all-reduced until
+every order statistic is resolved (exact; two passes over the local keys at
+most, see select.hip).
 Order-sensitive aggregators (`dev`: StdDev.runDouble is one sequential
 Welford loop, Aggregators.java:547-568, whose result on offset data depends
 on its order at ~1e-11) hand their states on instead of merging them: rank 0
@@ -82,7 +84,8 @@ def all_reduce(t, op="sum", group=None):
     """In-place all-reduce of a device tensor (staged through the host for
     gloo)."""
     import torch.distributed as dist
-    o = dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX
+    o = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
+         "min": dist.ReduceOp.MIN}[op]
     if _staged(group):
         h = t.cpu()
         dist.all_reduce(h, op=o, group=group)
@@ -353,11 +356,11 @@ def run_sharded(engine, spec, dbatch, n_groups_global, torch_mod=None,
 
 class ShardedSelect:
     """One rank's side of the otsdb_sel_* protocol (include/otsdb_agg.h):
-    prepare -> counts/emit; hist(pass) x 8; finish.  The collectives between
-    the steps are the caller's (run_sharded_select, or an in-process
-    emulation in the GPU tests)."""
+    prepare -> counts / emit / key range; hist_pass(p) while it reports
+    more; pick; finish.  The collectives between the steps are the caller's
+    (run_sharded_select, or an in-process emulation in the GPU tests)."""
 
-    HIST_WORDS = 512  # u32 per (group, bucket): 2 targets x 256 bins
+    BINS = 2048  # OTSDB_SEL_BINS: u32 per (group, bucket) and pass
 
     @staticmethod
     def _stream():
@@ -379,36 +382,44 @@ class ShardedSelect:
         n = max(self.GB, 1)
         self.counts = torch.zeros(n, dtype=torch.int64, device=self.dev)
         self.emit = torch.zeros(n, dtype=torch.uint8, device=self.dev)
-        self.hist = torch.zeros(n * self.HIST_WORDS, dtype=torch.int32,
+        self.krange = torch.zeros(2 * n, dtype=torch.int64, device=self.dev)
+        self.hist = torch.zeros(n * self.BINS, dtype=torch.int32,
                                 device=self.dev)
-        self.prev = torch.zeros_like(self.hist)
+        self.picks = torch.zeros(2 * n, dtype=torch.int64, device=self.dev)
 
     def prepare(self):
         import ctypes as C
         b = self.dbatch.as_abi()
         self.engine._check(self.engine.lib.otsdb_sel_prepare_device(
             self.engine.ctx, C.byref(self.spec), C.byref(b),
-            self.counts.data_ptr(), self.emit.data_ptr(), self._stream()))
-        return self.counts, self.emit
+            self.counts.data_ptr(), self.emit.data_ptr(),
+            self.krange.data_ptr(), self._stream()))
+        return self.counts, self.emit, self.krange
 
     def hist_pass(self, p):
-        """Local histogram of pass p; for p > 0 self.prev must hold the
-        all-reduced histogram of pass p - 1."""
+        """Pass p: applies self.hist (for p > 0 it must hold the all-reduced
+        histogram of pass p - 1) and, when a pass is planned, overwrites it
+        with this rank's histogram of pass p.  Returns whether it did."""
+        import ctypes as C
+        more = C.c_int32(0)
         self.engine._check(self.engine.lib.otsdb_sel_hist_device(
             self.engine.ctx, int(p), self.counts.data_ptr(),
-            self.emit.data_ptr(), self.prev.data_ptr(), self.hist.data_ptr(),
+            self.emit.data_ptr(), self.krange.data_ptr(),
+            self.hist.data_ptr(), self.hist.data_ptr(), C.byref(more),
             self._stream()))
-        return self.hist
+        return bool(more.value)
 
     def wait(self):
-        """The histogram kernels are done (otsdb_sel_hist_wait): for a
-        host-staged collective that does not read through torch's current
+        """The histogram / pick kernels are done (otsdb_sel_hist_wait): for
+        a host-staged collective that does not read through torch's current
         stream."""
         self.engine._check(self.engine.lib.otsdb_sel_hist_wait(
             self.engine.ctx, self._stream()))
 
-    def set_prev(self, global_hist):
-        self.prev.copy_(global_hist)
+    def pick(self):
+        self.engine._check(self.engine.lib.otsdb_sel_pick_device(
+            self.engine.ctx, self.picks.data_ptr(), self._stream()))
+        return self.picks
 
     def finish(self):
         import ctypes as C
@@ -417,23 +428,37 @@ class ShardedSelect:
         res = DeviceResult(torch, self.G, max(self.GB, 1), self.dev)
         r = res.as_abi()
         self.engine._check(self.engine.lib.otsdb_sel_finish_device(
-            self.engine.ctx, self.prev.data_ptr(), C.byref(r), self._stream()))
+            self.engine.ctx, self.picks.data_ptr(), C.byref(r),
+            self._stream()))
         return res
 
 
+# passes the protocol can plan: the offset digit resolves >= 10 of a key's
+# 64 bits, every later pass >= 10 more
+MAX_SEL_PASSES = 7
+
+
 def run_sharded_select(engine, spec, dbatch, n_groups_global, group=None):
-    """Median / percentile over series-sharded groups: exact radix select
-    with RCCL all-reduces of the counts and of each pass's histograms."""
+    """Median / percentile over series-sharded groups: exact selection with
+    all-reduces of the counts, key ranges, each pass's histograms and the
+    picked keys."""
     sel = ShardedSelect(engine, spec, dbatch, n_groups_global)
-    counts, emit = sel.prepare()
+    counts, emit, krange = sel.prepare()
     all_reduce(counts, "sum", group)
     all_reduce(emit, "max", group)
-    for p in range(8):
-        h = sel.hist_pass(p)
+    all_reduce(krange, "min", group)
+    p = 0
+    while sel.hist_pass(p):
+        if p >= MAX_SEL_PASSES:
+            raise RuntimeError("selection: pass %d planned" % p)
         if _staged(group):
-            sel.wait()  # the host copy below reads h
-        all_reduce(h, "sum", group)
-        sel.set_prev(h)
+            sel.wait()  # the host copy below reads the histogram
+        all_reduce(sel.hist, "sum", group)
+        p += 1
+    picks = sel.pick()
+    if _staged(group):
+        sel.wait()
+    all_reduce(picks, "sum", group)
     return sel.finish()
 
 

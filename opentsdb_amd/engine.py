@@ -109,11 +109,13 @@ class Engine:
 
     def counters(self):
         """otsdb_ctx_counters: {cells folds run uniform / general, uniform
-        folds re-run with the general kernel}."""
-        out = (C.c_int64 * 3)()
-        self._check(self.lib.otsdb_ctx_counters(self.ctx, out, 3))
+        folds re-run with the general kernel; the last otsdb_sel_* session's
+        passes over the local keys and histogram passes}."""
+        out = (C.c_int64 * 5)()
+        self._check(self.lib.otsdb_ctx_counters(self.ctx, out, 5))
         return dict(cells_uniform=out[0], cells_general=out[1],
-                    cells_uniform_miss=out[2])
+                    cells_uniform_miss=out[2], sel_key_reads=out[3],
+                    sel_passes=out[4])
 
     def close(self):
         if self.ctx:

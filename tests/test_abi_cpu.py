@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.otsdb_abi_version() == 5
+    assert lib.otsdb_abi_version() == 6
 
 
 def test_struct_sizes_match_header():

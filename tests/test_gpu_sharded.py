@@ -71,26 +71,44 @@ def _partials_emulated(engines, spec, hb, world):
     return _host(res, G)
 
 
-def _select_emulated(engines, spec, hb, world):
+def _select_emulated(engines, spec, hb, world, stats=None):
+    """The otsdb_sel_* protocol with the collectives emulated in-process
+    (one context per rank)."""
     import torch
     G = hb.n_groups
     sels = [odist.ShardedSelect(engines[r], spec,
                                 odist.to_device(odist.shard_host_batch(hb, world, r)),
                                 G) for r in range(world)]
-    cs, es = zip(*[s.prepare() for s in sels])
+    cs, es, ks = zip(*[s.prepare() for s in sels])
     counts = torch.stack(cs).sum(0)
     emit = torch.stack(es).max(0).values
+    krange = torch.stack(ks).min(0).values
     for s in sels:
         s.counts.copy_(counts)
         s.emit.copy_(emit)
-    for p in range(8):
-        h = torch.stack([s.hist_pass(p).clone() for s in sels]).sum(0)
+        s.krange.copy_(krange)
+    p = 0
+    while True:
+        more = [s.hist_pass(p) for s in sels]
+        assert len(set(more)) == 1, "ranks planned different passes"
+        if not more[0]:
+            break
+        h = torch.stack([s.hist for s in sels]).sum(0)
         for s in sels:
-            s.set_prev(h.to(torch.int32))
+            s.hist.copy_(h.to(torch.int32))
+        p += 1
+        assert p <= odist.MAX_SEL_PASSES
+    picks = torch.stack([s.pick().clone() for s in sels]).sum(0)
+    for s in sels:
+        s.picks.copy_(picks)
     outs = [_host(s.finish(), G) for s in sels]
     for o in outs[1:]:  # every rank ends with the same result
         for a, b in zip(outs[0], o):
             assert np.array_equal(a.ts, b.ts) and np.array_equal(a.bits, b.bits)
+    if stats is not None:
+        for e in engines[:world]:
+            c = e.counters()
+            stats.append((c["sel_key_reads"], c["sel_passes"]))
     return outs[0]
 
 
@@ -127,6 +145,52 @@ def test_percentiles_across_ranks(engines, agg, world):
         got = _select_emulated(engines, spec, hb, world)
         compare(got, ref, ds == "max",
                 where="w%d/%s/%s" % (world, agg, fill))
+
+
+def _edge_values(kind, rng, m):
+    """Bucket values that stress the cross-rank selection's planning."""
+    if kind == "ties":  # one distinct key: resolved from the key range alone
+        return np.full(m, 42.0)
+    if kind == "clustered":  # the offset digit puts ~all keys in one bin
+        v = 1.0 + rng.random(m) * 1e-12
+        v[rng.random(m) < 0.005] = 1e6
+        return v
+    if kind == "signed":  # both signs, +-0.0, subnormals, wide exponents
+        v = rng.standard_normal(m) * 10.0 ** rng.integers(-300, 300, m)
+        z = rng.random(m)
+        v[z < 0.05] = 0.0
+        v[(z >= 0.05) & (z < 0.1)] = -0.0
+        v[(z >= 0.1) & (z < 0.12)] = 5e-324
+        return v
+    if kind == "dups":  # few distinct values: bins of many equal keys
+        return rng.integers(0, 5, m).astype(np.float64) * 0.25
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("kind", ["ties", "clustered", "signed", "dups"])
+def test_selection_protocol_edges(engines, kind, world):
+    """The otsdb_sel_* planning on adversarial keys: bit-identical to the
+    oracle, every rank planning the same passes, at most two passes over a
+    rank's local keys (otsdb_ctx_counters) and MAX_SEL_PASSES histogram
+    passes."""
+    hb = datasets.random_batch(207, n_series=160, n_groups=2, nan_frac=0.0,
+                               span_ms=3600 * 1000, cadence_ms=20000)
+    rng = np.random.default_rng(11)
+    hb.val = np.ascontiguousarray(
+        _edge_values(kind, rng, len(hb.val)).view(np.int64))
+    hb.is_float = np.ones(len(hb.val), np.uint8)
+    for agg in ("p99", "median", "ep50r7", "p999"):
+        spec = _spec(agg, "max", "none", end=datasets.T0 + 3600 * 1000)
+        ref = pyoracle.group_by(spec, hb)
+        stats = []
+        got = _select_emulated(engines, spec, hb, world, stats)
+        compare(got, ref, True, where="w%d/%s/%s" % (world, kind, agg))
+        for reads, passes in stats:
+            assert reads <= 2 and passes <= odist.MAX_SEL_PASSES, (
+                kind, agg, reads, passes)
+        if kind == "ties":
+            assert all(r == 0 and p == 0 for r, p in stats), stats
 
 
 def _free_port():
