@@ -56,7 +56,21 @@ def main(tag):
             dst = os.path.join(PROF, "%s_%s_kernel_stats.csv" % (tag, what))
             shutil.copy(ks, dst)
             done.append(dst)
-    p = os.path.join(OUT, "r5_gpu_suite.log")
+    for cfg in ("C5",):  # the cross-rank protocol at a world of one
+        p = os.path.join(OUT, "bench_%s_sharded.log" % cfg)
+        if os.path.exists(p):
+            line = last_json_line(p)
+            if line:
+                dst = os.path.join(PROF, "%s_bench_%s_sharded.json" % (tag, cfg))
+                with open(dst, "w") as f:
+                    f.write(line + "\n")
+                done.append(dst)
+        ks = first("ks_%s_sharded/**/*kernel_stats.csv" % cfg)
+        if ks:
+            dst = os.path.join(PROF, "%s_%s_sharded_kernel_stats.csv" % (tag, cfg))
+            shutil.copy(ks, dst)
+            done.append(dst)
+    p = os.path.join(OUT, "%s_gpu_suite.log" % tag)
     if os.path.exists(p):
         with open(p) as f:
             tail = f.read().splitlines()[-3:]
