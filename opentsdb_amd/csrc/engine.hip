@@ -96,6 +96,13 @@ inline int64_t align_down(int64_t t, int64_t iv) { return t - jmod(t, iv); }
 
 constexpr int64_t kChunk = 256;  // series per cross-series chunk
 
+// k_keys_transpose's grid: KT_M members x OTSDB_KT_SLICES bucket slices
+dim3 kt_grid(int64_t M, int64_t NB) {
+  const int64_t ntb = (NB + 63) / 64;
+  const int64_t sl = ntb < OTSDB_KT_SLICES ? (ntb > 0 ? ntb : 1) : OTSDB_KT_SLICES;
+  return dim3((unsigned)((M + KT_M - 1) / KT_M), (unsigned)sl);
+}
+
 // members per tile of the ordered fold: one tile is one workgroup that
 // streams all its members' points, so big groups (C3's 7.8k-series
 // datacenters per GPU) are cut finer than kChunk — 256-member tiles of one
@@ -1212,7 +1219,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         SelFill F{W.SM.keep, W.SM.kf, W.SM.kl, P.fill_value, W.key_cnt,
                   T.lg_off, T.LG, W.lg_kept};
         if (M > 0)
-          hipLaunchKernelGGL(k_keys_transpose<true>, dim3(blocks_for(M, KT_M)),
+          hipLaunchKernelGGL(k_keys_transpose<true>, kt_grid(M, NB),
                              dim3(KT_THREADS), 0, st, NB, M, d_members, W.R, W.keys,
                              W.key_mm, F);
         W.sel_fused = true;
@@ -1246,7 +1253,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         const int64_t M = goff.back();
         if (M > 0)
           hipLaunchKernelGGL(k_keys_transpose<false>,
-                             dim3(blocks_for(M, KT_M)),
+                             kt_grid(M, NB),
                              dim3(KT_THREADS), 0, st, NB, M, d_members, W.R, W.keys,
                              W.key_mm, SelFill{});
         HIP_TRY(hipGetLastError());
@@ -1263,7 +1270,7 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
         const int64_t M = goff.back();
         const int64_t NSEG = T.LG * NB;
         hipLaunchKernelGGL(k_keys_transpose<false>,
-                           dim3(blocks_for(M, KT_M)),
+                           kt_grid(M, NB),
                            dim3(KT_THREADS), 0, st, NB, M, d_members, W.R, W.keys,
                            W.key_mm, SelFill{});
         hipLaunchKernelGGL(k_sel_init, dim3(blocks_for(NSEG, 256)), dim3(256),

@@ -57,7 +57,11 @@ struct SelFill {
   uint32_t* kept;          // [n_lg] the group has a kept series
 };
 
-// One workgroup per KT_M members sweeps their rows tile by tile (64 buckets):
+#ifndef OTSDB_KT_SLICES  // bucket slices per KT_M members (grid.y): C5's
+#define OTSDB_KT_SLICES 4  // 1,953 member tiles are ~1.9 rounds of the
+#endif                     // 1,024 workgroups its LDS lets the chip hold
+// One workgroup per KT_M members and bucket slice (blockIdx.y) sweeps their
+// rows tile by tile (64 buckets):
 // the members' row offsets are read once, and the next tile's values and
 // states are loaded into registers before the current tile leaves LDS, so
 // each wave keeps a tile's loads in flight while it stores the previous one.
@@ -122,8 +126,13 @@ __global__ __launch_bounds__(KT_THREADS) void k_keys_transpose(
       if (!FILL) st[r] = in ? R.state[off] : (uint8_t)0;
     }
   };
-  load(0);
-  for (int64_t b0 = 0; b0 < nb; b0 += 64) {
+  // this workgroup's bucket slice: whole 64-bucket tiles
+  const int64_t ntb = (nb + 63) / 64;
+  const int64_t tps = (ntb + gridDim.y - 1) / gridDim.y;
+  const int64_t bs = (int64_t)blockIdx.y * tps * 64;
+  const int64_t be = bs + tps * 64 < nb ? bs + tps * 64 : nb;
+  if (bs < be) load(bs);
+  for (int64_t b0 = bs; b0 < be; b0 += 64) {
     // the keys of this thread's 16 members at bucket b0 + bi, and their
     // min / max / count (the tile's per-bucket partial, from registers)
     uint64_t mn = KEY_NONE, mx = 0;
@@ -154,7 +163,7 @@ __global__ __launch_bounds__(KT_THREADS) void k_keys_transpose(
       s_cnt[w][bi] = nk;
     }
     __syncthreads();
-    if (b0 + 64 < nb) load(b0 + 64);
+    if (b0 + 64 < be) load(b0 + 64);
     // stores: KT_M consecutive members per bucket, 4 buckets at a time
     const int sm = tid % KT_M, sg = tid / KT_M;
     const int64_t m = m0 + sm;
