@@ -193,6 +193,20 @@ def test_selection_protocol_edges(engines, kind, world):
             assert all(r == 0 and p == 0 for r, p in stats), stats
 
 
+@pytest.mark.parametrize("agg", ["p99", "median"])
+def test_selection_with_an_empty_rank(engines, agg):
+    """Three ranks over two series: one rank holds no series at all (empty
+    key matrix, every segment's local range empty) and still plans the same
+    passes and ends with the full result."""
+    hb = datasets.random_batch(209, n_series=2, n_groups=1, nan_frac=0.0,
+                               empty_frac=0.0, span_ms=3600 * 1000,
+                               cadence_ms=20000)
+    spec = _spec(agg, "avg", "none", end=datasets.T0 + 3600 * 1000)
+    ref = pyoracle.group_by(spec, hb)
+    got = _select_emulated(engines, spec, hb, 3)
+    compare(got, ref, False, where="empty-rank/%s" % agg)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
