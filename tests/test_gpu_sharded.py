@@ -147,6 +147,33 @@ def test_percentiles_across_ranks(engines, agg, world):
                 where="w%d/%s/%s" % (world, agg, fill))
 
 
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("agg", ["p99", "median", "ep95r3"])
+def test_percentiles_across_ranks_fills_rate_calendar(engines, agg, world):
+    """The protocol under the other paths into the key matrix: fill zero /
+    null (the transpose applies the fill and counts the keys), counter rates
+    (the rate-fused bucketize rows), `all`, and a calendar grid."""
+    import copy
+    from opentsdb_amd import core as ocore, jcalendar
+    hb = datasets.random_batch(211, n_series=70, n_groups=2, nan_frac=0.03,
+                               span_ms=3 * 3600 * 1000, cadence_ms=20000)
+    cases = [("sum", "zero", False, "1m"), ("avg", "null", False, "1m"),
+             ("max", "none", False, "30m"), ("avg", "none", False, "0all")]
+    for ds, fill, rate, iv in cases:
+        spec = _spec(agg, ds, fill, rate=rate, interval=iv)
+        ref = pyoracle.group_by(spec, hb)
+        got = _select_emulated(engines, spec, hb, world)
+        compare(got, ref, ds == "max", where="w%d/%s/%s-%s-%s" % (
+            world, agg, iv, ds, fill))
+    hc = datasets.random_batch(213, n_series=60, n_groups=2, counter=True,
+                               span_ms=3 * 3600 * 1000, cadence_ms=20000)
+    ro = ocore.RateOptions(True, 2**63 - 1, 0)
+    spec = _spec(agg, "sum", "none", rate=True, ro=ro)
+    ref = pyoracle.group_by(spec, hc)
+    got = _select_emulated(engines, spec, hc, world)
+    compare(got, ref, False, where="w%d/%s/rate" % (world, agg))
+
+
 def _edge_values(kind, rng, m):
     """Bucket values that stress the cross-rank selection's planning."""
     if kind == "ties":  # one distinct key: resolved from the key range alone
