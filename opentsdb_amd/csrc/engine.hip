@@ -112,6 +112,14 @@ dim3 kt_grid(int64_t M, int64_t NB) {
 #define OTSDB_FOLD_CHUNK 32
 #endif
 constexpr int64_t kFoldChunk = OTSDB_FOLD_CHUNK;
+// groups of more than kFoldChunk members (C3's 7.8k-series datacenters):
+// tiles of kFoldChunkLarge, twice as many workgroups again for the grid's
+// last round (C3 fold: 32 -> 2.59 ms, 16 -> 2.50, 8 -> 2.46); groups up to
+// kFoldChunk members (C1 / C2 hosts) stay one tile
+#ifndef OTSDB_FOLD_CHUNK_LARGE  // tuning builds override
+#define OTSDB_FOLD_CHUNK_LARGE 8
+#endif
+constexpr int64_t kFoldChunkLarge = OTSDB_FOLD_CHUNK_LARGE;
 #ifndef OTSDB_FOLD_CTX  // tuning builds: 0 = no preloaded member contexts
 #define OTSDB_FOLD_CTX 1
 #endif
@@ -933,12 +941,13 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
                 "exact-order dev across ranks: hand the chains on "
                 "(otsdb_agg_partials_chained_device)");
   otsdb_status rc = build_tiles(
-      c, goff, mode == 2, fold ? kFoldChunk : kChunk,
+      c, goff, mode == 2,
+      fold ? (ordered ? kFoldChunk : kFoldChunkLarge) : kChunk,
       ordered ? (fold ? kOrderedFoldChunk
                       : (exact ? INT64_MAX
                                : (mode == 1 && !ginit ? kOrderedChunkMerged
                                                       : kOrderedChunk)))
-              : 0);
+              : (fold ? kFoldChunk : 0));
   if (rc) return rc;
   const Tiles T = tiles_of(c, G);
   P.fold_wb = 0;  // (P may come from an earlier pipeline run)
@@ -946,10 +955,15 @@ otsdb_status run_pipeline(otsdb_ctx* c, const otsdb_query_spec* spec,
   if (fold && OTSDB_FOLD_CTX) {
     // tiles of up to 64 members load every member context at workgroup
     // start (k_fold; ds_tu.hip drops it when the LDS would cost occupancy)
+    // (non-ordered: the largest tile, a group kept whole or one chunk of a
+    // larger one; ordered: bounded by its whole-group size)
     int64_t tile_max = 0;
-    for (size_t g = 0; g + 1 < goff.size(); ++g)
-      tile_max = std::max(tile_max, goff[g + 1] - goff[g]);
-    tile_max = std::min(tile_max, ordered ? kOrderedFoldChunk : kFoldChunk);
+    for (size_t g = 0; g + 1 < goff.size(); ++g) {
+      const int64_t k = goff[g + 1] - goff[g];
+      tile_max = std::max(
+          tile_max, ordered ? std::min(k, kOrderedFoldChunk)
+                            : (k <= kFoldChunk ? k : std::min(k, kFoldChunkLarge)));
+    }
     if (tile_max > 0 && tile_max <= 64) P.fold_ctx = (int32_t)tile_max;
   }
   // few tiles (small queries, e.g. C1's 100 groups of 10 series): narrower
