@@ -85,7 +85,7 @@ bool launch_cells(DsKernel k, const DsLaunch& a) {
       return with_monoid(a.agg_id, [&](auto tag) {
         using A = decltype(tag);
         hipLaunchKernelGGL((k_fold<M, A, 8, 4>),
-                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(256),
+                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(FOLD_THREADS),
                            (unsigned)fold_lds_bytes<A>(a.P),
                            a.st, a.P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
                            a.tm1, a.single, a.members, a.wc, a.NW, a.partial,
@@ -103,7 +103,7 @@ bool launch_cells(DsKernel k, const DsLaunch& a) {
       return with_monoid(a.agg_id, [&](auto tag) {
         using A = decltype(tag);
         hipLaunchKernelGGL((k_fold<M, A, 8, 12>),
-                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(256),
+                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(FOLD_THREADS),
                            (unsigned)fold_lds_bytes<A>(a.P),
                            a.st, a.P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
                            a.tm1, a.single, a.members, a.wc, a.NW, a.partial,
@@ -115,7 +115,7 @@ bool launch_cells(DsKernel k, const DsLaunch& a) {
       return with_monoid(a.agg_id, [&](auto tag) {
         using A = decltype(tag);
         hipLaunchKernelGGL((k_fold<M, A, 8, 10>),
-                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(256),
+                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(FOLD_THREADS),
                            (unsigned)fold_lds_bytes<A>(a.P),
                            a.st, a.P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
                            a.tm1, a.single, a.members, a.wc, a.NW, a.partial,
@@ -127,7 +127,7 @@ bool launch_cells(DsKernel k, const DsLaunch& a) {
       return with_monoid(a.agg_id, [&](auto tag) {
         using A = decltype(tag);
         hipLaunchKernelGGL((k_fold<M, A, 8, 2>),
-                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(256),
+                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(FOLD_THREADS),
                            (unsigned)fold_lds_bytes<A>(a.P),
                            a.st, a.P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
                            a.tm1, a.single, a.members, a.wc, a.NW, a.partial,
@@ -199,7 +199,7 @@ bool launch_ds(DsKernel k, const DsLaunch& a) {
         else
           P.fold_ctx = 0;
         hipLaunchKernelGGL((k_fold<M, A, 8>),
-                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(256),
+                           dim3((unsigned)(a.n_tiles * a.NW)), dim3(FOLD_THREADS),
                            (unsigned)lds,
                            a.st, P, a.B, a.SM, a.n_tiles, a.tg, a.tm0,
                            a.tm1, a.single, a.members, a.wc, a.NW, a.partial,

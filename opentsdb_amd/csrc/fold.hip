@@ -70,6 +70,11 @@ namespace otsdb {
 #define OTSDB_CELLS_FOLD_WAVES 4
 #endif
 constexpr int FOLD_WIN = 128;  // per-wave ring of closed bucket values
+#ifndef OTSDB_FOLD_WG_WAVES  // wavefronts per fold workgroup (A/B builds)
+#define OTSDB_FOLD_WG_WAVES 4
+#endif
+constexpr int FOLD_WG = OTSDB_FOLD_WG_WAVES;
+constexpr int FOLD_THREADS = 64 * FOLD_WG;
 constexpr int FOLD_FL = OTSDB_FOLD_FL;  // flush once this many buckets are final
 constexpr int32_t kProgDone = INT32_MAX;
 
@@ -583,7 +588,7 @@ DEV void fold_member_cells_u(const Params& P, const CellsDev& C, FoldSink<A>& F,
                              const FoldMember* mc, const CellsMember* cm);
 
 template <class M, class A, int K, int CELLS = 0>
-__global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
+__global__ __launch_bounds__(FOLD_THREADS, CELLS ? OTSDB_CELLS_FOLD_WAVES
                                         : OTSDB_FOLD_WAVES) void k_fold(
     Params P, BatchDev B, SeriesMeta SM, int64_t n_tiles,
     const int64_t* __restrict__ tile_g, const int64_t* __restrict__ tile_m0,
@@ -600,12 +605,12 @@ __global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
   extern __shared__ __attribute__((aligned(16))) unsigned char fold_dyn[];
   A* st = reinterpret_cast<A*>(fold_dyn);
   uint8_t* emit = fold_dyn + fold_lds_states<A>(P);
-  __shared__ double ring[4][FOLD_WIN];
+  __shared__ double ring[FOLD_WG][FOLD_WIN];
   __shared__ int32_t prog[256];
   __shared__ int s_next;
   __shared__ FoldKernel kc;
-  __shared__ FoldMember mc[4];
-  __shared__ CellsMember cm[CELLS ? 4 : 1];
+  __shared__ FoldMember mc[FOLD_WG];
+  __shared__ CellsMember cm[CELLS ? FOLD_WG : 1];
   const int tid = threadIdx.x, lane = LANE, w = tid >> 6;
   const int64_t nb = P.nb;
   int32_t W0, W1;
@@ -639,11 +644,11 @@ __global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
     }
   }
   const int nw = W1 - W0;
-  for (int b = tid; b < nw; b += 256) {
+  for (int b = tid; b < nw; b += FOLD_THREADS) {
     st[b] = A::init();
     emit[b] = 0;
   }
-  prog[tid] = 0;
+  for (int j = tid; j < 256; j += FOLD_THREADS) prog[j] = 0;
   for (int i = lane; i < FOLD_WIN; i += 64) ring[w][i] = absent_value();
   __syncthreads();
   if (CELLS && s_next < 0) return;  // (block-uniform)
@@ -693,7 +698,7 @@ __global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
   const bool ctx_on = !CELLS && P.fold_ctx > 0 && n_mem <= P.fold_ctx;
   FoldMember* ctx = reinterpret_cast<FoldMember*>(fold_dyn + fold_lds_bytes<A>(P));
   if (ctx_on) {
-    for (int64_t j = tid; j < n_mem; j += 256) ctx[j] = member_ctx(kc.members[kc.m0 + j]);
+    for (int64_t j = tid; j < n_mem; j += FOLD_THREADS) ctx[j] = member_ctx(kc.members[kc.m0 + j]);
     __syncthreads();
   }
   for (;;) {
@@ -746,7 +751,7 @@ __global__ __launch_bounds__(256, CELLS ? OTSDB_CELLS_FOLD_WAVES
   const bool fin = kc.fin;
   const int64_t g = kc.g, t = kc.t;
   int e = 0;
-  for (int b = tid; b < nw; b += 256) {
+  for (int b = tid; b < nw; b += FOLD_THREADS) {
     const int64_t gb = W0 + b;
     if (fin) {
       double r = 0.0;
